@@ -1,0 +1,73 @@
+"""Pin the CPU oracle against vectors generated from the reference itself (tests/golden/make_golden.py)."""
+import numpy as np
+import torch
+
+from _det import det_tensor, fill_module
+from oracle import tlc, pipeline as opipe
+from oracle.unet import ResidualAttentionBlock, ControlNetConditioningEmbedding
+
+SIZES = [(64, 64), (128, 128), (128, 192), (200, 136), (256, 256), (512, 512), (540, 960),
+         (96, 300), (135, 240), (1024, 1024)]
+
+
+def test_tlc_origins_match_reference(golden):
+    for h, w in SIZES:
+        idx, _ = tlc.tile_origins(h, w, (128, 128), 0.5)
+        np.testing.assert_array_equal(np.array(idx, dtype=np.int64), golden[f"tlc_{h}x{w}_idx"])
+    # tile counts quoted in SURVEY 8 (C3 4096^2 -> 49 tiles)
+    assert int(golden["tlc_512x512_ntiles"]) == 49
+
+
+def test_gaussian_weights_bitexact(golden):
+    for kh, kw in [(128, 128), (64, 64), (128, 96)]:
+        w = tlc.gaussian_weights(kw, kh)
+        np.testing.assert_array_equal(w[0].numpy(), golden[f"gauss_{kh}x{kw}"])
+
+
+def test_tlc_blend_matches_reference(golden):
+    for h, w in SIZES:
+        if h * w > 200 * 200:
+            continue
+        la = tlc.LocalAttention((128, 128), 0.5)
+        x = det_tensor((1, 4, h, w), 1000 + h * 7 + w)
+        tiles = la.grids(x)
+        outs = tiles * (1.0 + 0.01 * torch.arange(tiles.shape[0]).view(-1, 1, 1, 1)) + 0.05
+        np.testing.assert_array_equal(la.grids_inverse(outs).numpy(), golden[f"tlc_{h}x{w}_inv"])
+
+
+def test_rescale_noise_cfg(golden):
+    a = det_tensor((1, 4, 16, 16), 11)
+    b = det_tensor((1, 4, 16, 16), 12, 0.5)
+    np.testing.assert_allclose(opipe.rescale_noise_cfg(a, b, 0.7).numpy(), golden["rescale_cfg_out"], rtol=1e-6, atol=1e-6)
+
+
+def test_information_transformer_block(golden):
+    blk = fill_module(ResidualAttentionBlock(640, 8), 2000).eval()
+    row = det_tensor((1, 64, 640), 21)
+    with torch.no_grad():
+        same = blk(torch.cat([row, row], 0)).numpy()
+        diff = blk(torch.cat([row, det_tensor((1, 64, 640), 22)], 0)).numpy()
+    np.testing.assert_allclose(same, golden["rab_same_out"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(diff, golden["rab_diff_out"], rtol=1e-5, atol=1e-5)
+
+
+def test_information_transformer_identical_rows_reduce_pointwise():
+    """SURVEY key finding 5: with identical CFG rows, MHA over the batch axis == out_proj(v_proj(x))."""
+    blk = fill_module(ResidualAttentionBlock(640, 8), 2000).eval()
+    row = det_tensor((1, 64, 640), 21)
+    x = torch.cat([row, row], 0)
+    with torch.no_grad():
+        full = blk(x)
+        h = blk.ln_1(x)
+        wv = blk.attn.in_proj_weight[1280:]
+        bv = blk.attn.in_proj_bias[1280:]
+        y = x + blk.attn.out_proj(h @ wv.T + bv)
+        y = y + blk.mlp(blk.ln_2(y))
+    torch.testing.assert_close(full, y, rtol=1e-5, atol=1e-5)
+
+
+def test_condition_embedding(golden):
+    cne = fill_module(ControlNetConditioningEmbedding(320, 512), 3000).eval()
+    with torch.no_grad():
+        out = cne(det_tensor((1, 512, 8, 8), 31)).numpy()
+    np.testing.assert_allclose(out, golden["cne_out"], rtol=1e-5, atol=1e-5)
