@@ -1,0 +1,301 @@
+// Attention kernels for gfx950.
+//
+// flash_attn_d64: head_dim 64 flash attention (SDPA replacement for the 140 attn1/attn2 calls of a
+// UNet forward).  One workgroup = 4 waves = 128 queries of one (batch, head); each wave owns 32
+// queries.  K/V tiles of 64 keys are staged by global_load_lds into a double buffer.  The score
+// tile is computed transposed, S^T = K Q^T (A = K rows from LDS, B = Q fragments held in VGPRs),
+// so each lane owns one query column: the row max needs only two cross-lane shuffles, and the
+// accumulator, packed to bf16/f16 in registers, is directly the B operand of O^T = V^T P^T (guide
+// section 3, "an accumulator tile as the next MFMA's operand").  V^T fragments come from
+// ds_read_b64_tr_b16 on a row-major V tile (T10).  Softmax is online, exp2-based, fp32.
+//
+// mha_seq_axis: the information transformer's MultiheadAttention over the batch axis (L = CFG pair).
+// softmax_rows: fp32 row softmax for the single-head d=512 VAE mid attention (GEMM + softmax + GEMM).
+#include "fd_common.h"
+
+template <typename T>
+__global__ void __launch_bounds__(256) flash_attn_d64_kernel(
+    const T* __restrict__ Q, long long ldq, long long qbs, const T* __restrict__ K, long long ldk, long long kbs,
+    const T* __restrict__ V, long long ldv, long long vbs, T* __restrict__ O, long long ldo, long long obs,
+    int Lq, int Lk, int kv_mod, float scale_log2) {
+  typedef typename VecT<T>::v8 V8;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kvb = kv_mod > 0 ? (b % kv_mod) : b;
+  const T* Qb = Q + (long long)b * qbs + h * 64;
+  const T* Kb = K + (long long)kvb * kbs + h * 64;
+  const T* Vb = V + (long long)kvb * vbs + h * 64;
+  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  // Q fragments (B operand): lane holds Q[q0 + qb*16 + fr][ds*32 + 8*fg .. +7]
+  V8 qf[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    int q = q0 + qb * 16 + fr;
+    q = q < Lq ? q : Lq - 1;
+#pragma unroll
+    for (int ds = 0; ds < 2; ++ds) qf[qb][ds] = *(const V8*)(Qb + (long long)q * ldq + ds * 32 + fg * 8);
+  }
+
+  const int lrow = lane >> 3, slot = lane & 7;
+  auto stage = [&](int t, int buf) {
+    unsigned char* sk = smem + buf * 16384;
+    unsigned char* sv = sk + 8192;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (i * 4 + wave) * 8 + lrow;
+      int key = t * 64 + row;
+      key = key < Lk ? key : Lk - 1;
+      const int ck = slot ^ ((row >> 1) & 7);
+      const int cv = slot ^ (((row >> 1) & 3) << 1);
+      __builtin_amdgcn_global_load_lds((const void*)(Kb + (long long)key * ldk + ck * 8),
+                                       LDS_PTR(sk + (i * 4 + wave) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Vb + (long long)key * ldv + cv * 8),
+                                       LDS_PTR(sv + (i * 4 + wave) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 o[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) o[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float mrow[2] = {-INFINITY, -INFINITY}, lrow_sum[2] = {0.f, 0.f};
+
+  const int nt = (Lk + 63) / 64;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nt) stage(t + 1, buf ^ 1);
+    const unsigned char* sk = smem + buf * 16384;
+    const unsigned char* sv = sk + 8192;
+
+    // ---- S^T = K Q^T
+    f32x4 st[4][2];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      st[kb][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      st[kb][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const int r = kb * 16 + fr;
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds) {
+        const V8 kf = *(const V8*)(sk + r * 128 + (((ds * 4 + fg) ^ ((r >> 1) & 7)) << 4));
+        st[kb][0] = mfma16x16x32(kf, qf[0][ds], st[kb][0]);
+        st[kb][1] = mfma16x16x32(kf, qf[1][ds], st[kb][1]);
+      }
+    }
+    // ---- mask the key tail
+    if (t * 64 + 64 > Lk) {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = t * 64 + kb * 16 + fg * 4 + i;
+          if (key >= Lk) {
+            st[kb][0][i] = -INFINITY;
+            st[kb][1][i] = -INFINITY;
+          }
+        }
+    }
+    // ---- online softmax (one query per lane column; keys over fg groups, kb, i)
+    V8 pf[2][2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[kb][qb][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(mrow[qb], mx * scale_log2);
+      const float alpha = exp2f(mrow[qb] - mnew);
+      float ls = 0.f;
+      float pv[4][4];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = exp2f(st[kb][qb][i] * scale_log2 - mnew);
+          pv[kb][i] = e;
+          ls += e;
+        }
+      lrow_sum[qb] = lrow_sum[qb] * alpha + ls;
+      mrow[qb] = mnew;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        V8 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = (T)pv[2 * s][i];
+          v[4 + i] = (T)pv[2 * s + 1][i];
+        }
+        pf[qb][s] = v;
+      }
+    }
+    // ---- O^T += V^T P^T   (A = V^T via transposed LDS reads)
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        s16x4 lo, hi;
+        {
+          const int q = fr >> 2, pp = lane & 3;
+          const int col = db * 16 + 4 * pp;
+          const int r0 = 32 * s + 4 * fg + q, r1 = r0 + 16;
+          const int ch = col >> 3, boff = (col & 7) * 2;
+          const int a0 = r0 * 128 + ((ch ^ (((r0 >> 1) & 3) << 1)) << 4) + boff;
+          const int a1 = r1 * 128 + ((ch ^ (((r1 >> 1) & 3) << 1)) << 4) + boff;
+          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(sv + a0));
+          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(sv + a1));
+        }
+        V8 vf;
+        {
+          typedef __attribute__((ext_vector_type(8))) short s16x8;
+          s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          vf = __builtin_bit_cast(V8, w);
+        }
+        o[db][0] = mfma16x16x32(vf, pf[0][s], o[db][0]);
+        o[db][1] = mfma16x16x32(vf, pf[1][s], o[db][1]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- finalise: lane holds O^T[d = db*16 + 4*fg + j][q = qb*16 + fr]
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float l = lrow_sum[qb];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+    const int q = q0 + qb * 16 + fr;
+    if (q >= Lq) continue;
+    T* orow = O + (long long)b * obs + (long long)q * ldo + h * 64;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      typedef __attribute__((ext_vector_type(4))) T T4;
+      T4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = (T)(o[db][qb][j] * inv);
+      *(T4*)(orow + db * 16 + fg * 4) = w;
+    }
+  }
+}
+
+extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const void* k, long long ldk,
+                                   long long kbs, const void* v, long long ldv, long long vbs, void* o, long long ldo,
+                                   long long obs, int batch, int heads, int Lq, int Lk, int kv_mod, float scale,
+                                   int dtype, void* stream) {
+  if (!q || !k || !v || !o) return FD_ERR_ARG;
+  if (batch <= 0 || heads <= 0 || Lq <= 0 || Lk <= 0 || kv_mod < 0) return FD_ERR_SHAPE;
+  if ((ldq | ldk | ldv | ldo) & 7) return FD_ERR_SHAPE;
+  dim3 grid((Lq + 127) / 128, heads, batch), block(256);
+  const float sl2 = scale * 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(flash_attn_d64_kernel<T>, grid, block, 0, s, (const T*)q, ldq, qbs,
+                                          (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk,
+                                          kv_mod, sl2));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// MultiheadAttention over the sequence axis L (the CFG pair) for every pixel n, grouped: rows
+// [g*L, (g+1)*L) of the batch form one attention problem.  qkv [Btot][N][3E] -> o [Btot][N][E].
+// One thread per (group, n, head, l_query); hd = E / heads.
+template <typename T>
+__global__ void mha_seq_axis_kernel(const T* __restrict__ qkv, T* __restrict__ o, int L, int groups, int N, int E,
+                                    int heads) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)groups * N * heads * L;
+  if (idx >= total) return;
+  const int l1 = idx % L;
+  long long r = idx / L;
+  const int h = r % heads;
+  r /= heads;
+  const int n = r % N;
+  const int g = r / N;
+  const int hd = E / heads;
+  const float scale = rsqrtf((float)hd);
+  const long long E3 = 3LL * E;
+  const T* qrow = qkv + ((long long)(g * L + l1) * N + n) * E3 + h * hd;
+  float s[8];
+  float mx = -INFINITY;
+  for (int l2 = 0; l2 < L; ++l2) {
+    const T* krow = qkv + ((long long)(g * L + l2) * N + n) * E3 + E + h * hd;
+    float acc = 0.f;
+    for (int d = 0; d < hd; ++d) acc += (float)qrow[d] * (float)krow[d];
+    s[l2] = acc * scale;
+    mx = fmaxf(mx, s[l2]);
+  }
+  float den = 0.f;
+  for (int l2 = 0; l2 < L; ++l2) {
+    s[l2] = __expf(s[l2] - mx);
+    den += s[l2];
+  }
+  const float inv = 1.f / den;
+  T* orow = o + ((long long)(g * L + l1) * N + n) * E + h * hd;
+  for (int d = 0; d < hd; ++d) {
+    float acc = 0.f;
+    for (int l2 = 0; l2 < L; ++l2)
+      acc += s[l2] * (float)qkv[((long long)(g * L + l2) * N + n) * E3 + 2 * E + h * hd + d];
+    orow[d] = (T)(acc * inv);
+  }
+}
+
+extern "C" int fd_mha_seq_axis(const void* qkv, void* o, int L, int groups, int N, int E, int heads,
+                                       int dtype, void* stream) {
+  if (!qkv || !o) return FD_ERR_ARG;
+  if (L <= 0 || L > 8 || groups <= 0 || N <= 0 || E % heads) return FD_ERR_SHAPE;
+  const long long total = (long long)groups * N * heads * L;
+  dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(mha_seq_axis_kernel<T>, grid, block, 0, s, (const T*)qkv, (T*)o, L, groups,
+                                          N, E, heads));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// fp32 row softmax: p[r][c] = exp(scale*s - max) / sum  (one 256-thread block per row)
+template <typename TO>
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ s, TO* __restrict__ p, int C,
+                                                           float scale) {
+  __shared__ float red[8];
+  const long long r = blockIdx.x;
+  const float* row = s + r * C;
+  TO* out = p + r * C;
+  float mx = -INFINITY;
+  for (int c = threadIdx.x; c < C; c += 256) mx = fmaxf(mx, row[c] * scale);
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int c = threadIdx.x; c < C; c += 256) sum += __expf(row[c] * scale - mx);
+  sum = wave_sum(sum);
+  if ((threadIdx.x & 63) == 0) red[4 + (threadIdx.x >> 6)] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  for (int c = threadIdx.x; c < C; c += 256) out[c] = (TO)(__expf(row[c] * scale - mx) * inv);
+}
+
+extern "C" int fd_softmax_rows(const float* s, void* p, int R, int C, float scale, int dtype, void* stream) {
+  if (!s || !p) return FD_ERR_ARG;
+  if (R <= 0 || C <= 0) return FD_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  FD_DISPATCH_O(dtype, hipLaunchKernelGGL(softmax_rows_kernel<TO>, dim3(R), dim3(256), 0, st, s, (TO*)p, C, scale));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}

@@ -1,0 +1,554 @@
+// Elementwise, layout, direct-conv and denoise-loop kernels (all HBM- or latency-bound).
+#include <math.h>
+
+#include "fd_common.h"
+
+static inline dim3 grid1d(long long n, int per_thread = 1) {
+  long long blocks = (n + 256LL * per_thread - 1) / (256LL * per_thread);
+  if (blocks > 65535LL * 32) blocks = 65535LL * 32;
+  return dim3((unsigned)blocks);
+}
+
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void concat_channels_kernel(const T* __restrict__ a, int C1, const T* __restrict__ b, int C2,
+                                       T* __restrict__ y, long long M) {
+  typedef typename VecT<T>::v8 V8;
+  const int C = C1 + C2, VPR = C / 8;
+  const long long total = M * VPR;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long m = e / VPR;
+    const int v = e - m * VPR;
+    const int c = v * 8;
+    const V8 val = c < C1 ? *(const V8*)(a + m * C1 + c) : *(const V8*)(b + m * C2 + (c - C1));
+    *(V8*)(y + m * C + c) = val;
+  }
+}
+
+extern "C" int fd_concat_channels(const void* a, int C1, const void* b, int C2, void* y, long long M, int dtype,
+                                  void* stream) {
+  if (!a || !b || !y) return FD_ERR_ARG;
+  if (C1 % 8 || C2 % 8 || M <= 0) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(concat_channels_kernel<T>, grid1d(M * (C1 + C2) / 8), dim3(256), 0, s,
+                                          (const T*)a, C1, (const T*)b, C2, (T*)y, M));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+template <typename TI, typename TO>
+__global__ void unary_kernel(const TI* __restrict__ x, TO* __restrict__ y, long long n, int act) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = (TO)act_f((float)x[i], act);
+}
+
+#define FD_DISPATCH_I(dtype, ...)          \
+  if ((dtype) == FD_BF16) {                \
+    typedef bf16 TI;                       \
+    __VA_ARGS__;                           \
+  } else if ((dtype) == FD_F16) {          \
+    typedef f16 TI;                        \
+    __VA_ARGS__;                           \
+  } else if ((dtype) == FD_F32) {          \
+    typedef float TI;                      \
+    __VA_ARGS__;                           \
+  } else {                                 \
+    return FD_ERR_DTYPE;                   \
+  }
+
+extern "C" int fd_unary(const void* x, void* y, long long n, int act, int dtype, int out_dtype, void* stream) {
+  if (!x || !y) return FD_ERR_ARG;
+  if (n <= 0) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_I(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((unary_kernel<TI, TO>), grid1d(n), dim3(256), 0, s,
+                                                                   (const TI*)x, (TO*)y, n, act)));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+template <typename TI, typename TO>
+__global__ void add_strided_kernel(const TI* __restrict__ x, long long ldx, const TI* __restrict__ a, long long lda,
+                                   TO* __restrict__ y, long long ldy, int M, int N) {
+  const long long total = (long long)M * N;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long m = e / N;
+    const int n = e - m * N;
+    float v = (float)x[m * ldx + n];
+    if (a) v += (float)a[m * lda + n];
+    y[m * ldy + n] = (TO)v;
+  }
+}
+
+extern "C" int fd_add_strided(const void* x, long long ldx, const void* a, long long lda, void* y, long long ldy, int M,
+                              int N, int dtype, int out_dtype, void* stream) {
+  if (!x || !y) return FD_ERR_ARG;
+  if (M <= 0 || N <= 0) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_I(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((add_strided_kernel<TI, TO>),
+                                                                   grid1d((long long)M * N), dim3(256), 0, s,
+                                                                   (const TI*)x, ldx, (const TI*)a, lda, (TO*)y, ldy, M,
+                                                                   N)));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// layout transposes.  NCHW [n][C][HW] <-> NHWC [n][HW][C]; 32x32 LDS tiles.
+template <typename TI, typename TO, bool TO_NHWC>
+__global__ void layout_kernel(const TI* __restrict__ x, TO* __restrict__ y, int C, int HW, float scale) {
+  __shared__ float tile[32][33];
+  const int n = blockIdx.z;
+  // tile over (C, HW)
+  const int c0 = blockIdx.y * 32, p0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: ty 0..7
+  const long long base = (long long)n * C * HW;
+  for (int k = ty; k < 32; k += 8) {
+    if (TO_NHWC) {  // read NCHW: rows c, cols p
+      const int c = c0 + k, p = p0 + tx;
+      tile[k][tx] = (c < C && p < HW) ? (float)x[base + (long long)c * HW + p] : 0.f;
+    } else {  // read NHWC: rows p, cols c
+      const int p = p0 + k, c = c0 + tx;
+      tile[k][tx] = (c < C && p < HW) ? (float)x[base + (long long)p * C + c] : 0.f;
+    }
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    if (TO_NHWC) {  // write NHWC: rows p, cols c
+      const int p = p0 + k, c = c0 + tx;
+      if (c < C && p < HW) y[base + (long long)p * C + c] = (TO)(tile[tx][k] * scale);
+    } else {
+      const int c = c0 + k, p = p0 + tx;
+      if (c < C && p < HW) y[base + (long long)c * HW + p] = (TO)(tile[tx][k] * scale);
+    }
+  }
+}
+
+extern "C" int fd_nchw_to_nhwc(const void* x, void* y, int nimg, int C, int HW, float scale, int dtype, int out_dtype,
+                               void* stream) {
+  if (!x || !y) return FD_ERR_ARG;
+  if (nimg <= 0 || C <= 0 || HW <= 0) return FD_ERR_SHAPE;
+  dim3 grid((HW + 31) / 32, (C + 31) / 32, nimg);
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_I(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((layout_kernel<TI, TO, true>), grid, dim3(256), 0,
+                                                                   s, (const TI*)x, (TO*)y, C, HW, scale)));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+extern "C" int fd_nhwc_to_nchw(const void* x, void* y, int nimg, int C, int HW, float scale, int dtype, int out_dtype,
+                               void* stream) {
+  if (!x || !y) return FD_ERR_ARG;
+  if (nimg <= 0 || C <= 0 || HW <= 0) return FD_ERR_SHAPE;
+  dim3 grid((HW + 31) / 32, (C + 31) / 32, nimg);
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_I(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((layout_kernel<TI, TO, false>), grid, dim3(256), 0,
+                                                                   s, (const TI*)x, (TO*)y, C, HW, scale)));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+template <typename T>
+__global__ void transpose_kernel(const T* __restrict__ x, long long ldx, T* __restrict__ y, long long ldy, int R, int C,
+                                 long long sx, long long sy) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const T* xb = x + (long long)b * sx;
+  T* yb = y + (long long)b * sy;
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    tile[k][tx] = (r < R && c < C) ? (float)xb[(long long)r * ldx + c] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (r < R && c < C) yb[(long long)c * ldy + r] = (T)tile[tx][k];
+  }
+}
+
+extern "C" int fd_transpose(const void* x, long long ldx, void* y, long long ldy, int R, int C, int batch, long long sx,
+                            long long sy, int dtype, void* stream) {
+  if (!x || !y) return FD_ERR_ARG;
+  if (R <= 0 || C <= 0 || batch <= 0) return FD_ERR_SHAPE;
+  dim3 grid((C + 31) / 32, (R + 31) / 32, batch);
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(transpose_kernel<T>, grid, dim3(256), 0, s, (const T*)x, ldx, (T*)y, ldy, R,
+                                          C, sx, sy));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Direct conv for Cin < 64.  One thread per (pixel, cout); consecutive threads = consecutive cout.
+template <typename TI, typename TO>
+__global__ void conv_direct_kernel(const TI* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+                                   TO* __restrict__ y, int nimg, int Hin, int Win, int Cin, int Cout, int Hout,
+                                   int Wout, int ks, int stride, int pad, float in_scale) {
+  const long long total = (long long)nimg * Hout * Wout * Cout;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int co = e % Cout;
+    long long pix = e / Cout;
+    const int ox = pix % Wout;
+    pix /= Wout;
+    const int oy = pix % Hout;
+    const int img = pix / Hout;
+    float acc = bias ? bias[co] : 0.f;
+    const float* wr = w + (long long)co * ks * ks * Cin;
+    for (int ky = 0; ky < ks; ++ky) {
+      const int iy = oy * stride - pad + ky;
+      if (iy < 0 || iy >= Hin) continue;
+      for (int kx = 0; kx < ks; ++kx) {
+        const int ix = ox * stride - pad + kx;
+        if (ix < 0 || ix >= Win) continue;
+        const TI* xp = x + (((long long)img * Hin + iy) * Win + ix) * Cin;
+        const float* wp = wr + (ky * ks + kx) * Cin;
+        for (int c = 0; c < Cin; ++c) acc += (float)xp[c] * in_scale * wp[c];
+      }
+    }
+    y[e] = (TO)acc;
+  }
+}
+
+extern "C" int fd_conv2d_direct(const void* x, const float* w, const float* bias, void* y, int nimg, int Hin, int Win,
+                                int Cin, int Cout, int ksize, int stride, int pad, float in_scale, int dtype,
+                                int out_dtype, void* stream) {
+  if (!x || !w || !y) return FD_ERR_ARG;
+  if (nimg <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || Cout <= 0 || ksize <= 0 || stride <= 0) return FD_ERR_SHAPE;
+  const int Hout = (Hin + 2 * pad - ksize) / stride + 1, Wout = (Win + 2 * pad - ksize) / stride + 1;
+  const long long total = (long long)nimg * Hout * Wout * Cout;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_I(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv_direct_kernel<TI, TO>), grid1d(total),
+                                                                   dim3(256), 0, s, (const TI*)x, w, bias, (TO*)y, nimg,
+                                                                   Hin, Win, Cin, Cout, Hout, Wout, ksize, stride, pad,
+                                                                   in_scale)));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// SDXL time features (diffusers get_timestep_embedding: half = dim/2, exponent = -ln(1e4) * i / half,
+// emb = [cos, sin] after flip_sin_to_cos).
+__device__ __forceinline__ float sinus_feat(float t, int i, int dim) {
+  const int half = dim / 2;
+  const int k = i < half ? i : i - half;  // flipped: first half cos, second half sin
+  const float freq = expf(-9.210340371976184f * (float)k / (float)half);
+  const float a = t * freq;
+  return i < half ? cosf(a) : sinf(a);
+}
+
+template <typename TO>
+__global__ void time_features_kernel(const float* __restrict__ t, const float* __restrict__ tids,
+                                     const float* __restrict__ text, TO* __restrict__ tfeat, TO* __restrict__ afeat,
+                                     int batch) {
+  const int b = blockIdx.x;
+  for (int i = threadIdx.x; i < 320; i += blockDim.x) tfeat[b * 320 + i] = (TO)sinus_feat(t[b], i, 320);
+  for (int i = threadIdx.x; i < 2816; i += blockDim.x) {
+    float v;
+    if (i < 1280) {
+      v = text[b * 1280 + i];
+    } else {
+      const int j = i - 1280, which = j / 256, k = j % 256;
+      v = sinus_feat(tids[b * 6 + which], k, 256);
+    }
+    afeat[b * 2816 + i] = (TO)v;
+  }
+}
+
+extern "C" int fd_time_features(const float* t, const float* time_ids, const float* text_embeds, void* tfeat,
+                                void* afeat, int batch, int dtype, void* stream) {
+  if (!t || !time_ids || !text_embeds || !tfeat || !afeat) return FD_ERR_ARG;
+  if (batch <= 0) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_O(dtype, hipLaunchKernelGGL(time_features_kernel<TO>, dim3(batch), dim3(256), 0, s, t, time_ids,
+                                          text_embeds, (TO*)tfeat, (TO*)afeat, batch));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// TLC denoise-loop fusions.  Tile t (global index tid = tile_begin + t) has origin
+// (row_org[tid / nc], col_org[tid % nc]) on the latent canvas (LocalAttention.grids order).
+template <typename TO>
+__global__ void tlc_scale_input_kernel(const float* __restrict__ canvas, const int* __restrict__ row_org,
+                                       const int* __restrict__ col_org, int nc, int H, int W, int kh, int kw,
+                                       int tile_begin, int ntiles, int cfg, float inv_s, TO* __restrict__ out) {
+  const long long per = (long long)kh * kw;
+  const long long total = (long long)ntiles * per;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int t = e / per;
+    const int p = e - (long long)t * per;
+    const int y = p / kw, x = p - y * kw;
+    const int tid = tile_begin + t;
+    const int oy = row_org[tid / nc] + y, ox = col_org[tid % nc] + x;
+    float v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[c] = canvas[((long long)c * H + oy) * W + ox] * inv_s;
+    for (int d = 0; d < cfg; ++d) {
+      TO* o = out + (((long long)(t * cfg + d)) * per + p) * 4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) o[c] = (TO)v[c];
+    }
+  }
+}
+
+extern "C" int fd_tlc_scale_input(const float* canvas, const int* row_org, int nr, const int* col_org, int nc, int H,
+                                  int W, int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma, void* out,
+                                  int dtype, void* stream) {
+  if (!canvas || !row_org || !col_org || !out) return FD_ERR_ARG;
+  if (ntiles <= 0 || tile_begin < 0 || tile_begin + ntiles > nr * nc || kh > H || kw > W || cfg <= 0)
+    return FD_ERR_SHAPE;
+  const float inv_s = 1.0f / sqrtf(sigma * sigma + 1.0f);
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_O(dtype, hipLaunchKernelGGL(tlc_scale_input_kernel<TO>, grid1d((long long)ntiles * kh * kw), dim3(256), 0,
+                                          s, canvas, row_org, col_org, nc, H, W, kh, kw, tile_begin, ntiles, cfg, inv_s,
+                                          (TO*)out));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// CFG combine + Euler step for each tile; x taken from the canvas at the tile origin.
+template <typename TI>
+__global__ void tlc_cfg_euler_kernel(const TI* __restrict__ eps, const float* __restrict__ canvas,
+                                     const int* __restrict__ row_org, const int* __restrict__ col_org, int nc, int H,
+                                     int W, int kh, int kw, int tile_begin, int ntiles, int cfg, float g, float sigma,
+                                     float sigma_next, float* __restrict__ out) {
+  const long long per = (long long)kh * kw;
+  const long long total = (long long)ntiles * per;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int t = e / per;
+    const int p = e - (long long)t * per;
+    const int y = p / kw, x = p - y * kw;
+    const int tid = tile_begin + t;
+    const int oy = row_org[tid / nc] + y, ox = col_org[tid % nc] + x;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float ev;
+      if (cfg == 2) {
+        const float u = (float)eps[(((long long)(t * 2)) * per + p) * 4 + c];
+        const float cc = (float)eps[(((long long)(t * 2 + 1)) * per + p) * 4 + c];
+        ev = u + g * (cc - u);
+      } else {
+        ev = (float)eps[((long long)t * per + p) * 4 + c];
+      }
+      const float xv = canvas[((long long)c * H + oy) * W + ox];
+      // EulerDiscreteScheduler.step, gamma = 0: pred = x - sigma*eps; d = (x - pred)/sigma; x + d*dt
+      const float pred = xv - sigma * ev;
+      const float d = (xv - pred) / sigma;
+      out[((long long)t * 4 + c) * per + p] = xv + d * (sigma_next - sigma);
+    }
+  }
+}
+
+// guidance_rescale > 0: one block per tile (needs the tile-wide std of the CFG and text predictions)
+template <typename TI>
+__global__ void __launch_bounds__(256) tlc_cfg_rescale_euler_kernel(
+    const TI* __restrict__ eps, const float* __restrict__ canvas, const int* __restrict__ row_org,
+    const int* __restrict__ col_org, int nc, int H, int W, int kh, int kw, int tile_begin, float g, float rescale,
+    float sigma, float sigma_next, float* __restrict__ out) {
+  __shared__ double red[4][4];
+  const int t = blockIdx.x;
+  const long long per = (long long)kh * kw;
+  const long long n = per * 4;
+  double s_cfg = 0, q_cfg = 0, s_txt = 0, q_txt = 0;
+  for (long long e = threadIdx.x; e < n; e += 256) {
+    const float u = (float)eps[(long long)(t * 2) * n + e];
+    const float c = (float)eps[(long long)(t * 2 + 1) * n + e];
+    const float v = u + g * (c - u);
+    s_cfg += v; q_cfg += (double)v * v; s_txt += c; q_txt += (double)c * c;
+  }
+  // block reduce (doubles)
+  for (int o = 32; o > 0; o >>= 1) {
+    s_cfg += __shfl_xor(s_cfg, o, 64); q_cfg += __shfl_xor(q_cfg, o, 64);
+    s_txt += __shfl_xor(s_txt, o, 64); q_txt += __shfl_xor(q_txt, o, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[w][0] = s_cfg; red[w][1] = q_cfg; red[w][2] = s_txt; red[w][3] = q_txt; }
+  __syncthreads();
+  double S[4];
+  for (int k = 0; k < 4; ++k) S[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  // torch.std: unbiased
+  const double var_cfg = (S[1] - S[0] * S[0] / n) / (n - 1), var_txt = (S[3] - S[2] * S[2] / n) / (n - 1);
+  const float ratio = (float)(sqrt(var_txt) / sqrt(var_cfg));
+  const int tid = tile_begin + t;
+  const int r0 = row_org[tid / nc], c0 = col_org[tid % nc];
+  for (long long e = threadIdx.x; e < n; e += 256) {
+    // eps layout NHWC [p][c]; out layout NCHW [c][p]
+    const int c = e & 3;
+    const long long p = e >> 2;
+    const float u = (float)eps[(long long)(t * 2) * n + e];
+    const float cc = (float)eps[(long long)(t * 2 + 1) * n + e];
+    const float v = u + g * (cc - u);
+    const float ev = rescale * (v * ratio) + (1.f - rescale) * v;
+    const int y = p / kw, x = p - (long long)y * kw;
+    const float xv = canvas[((long long)c * H + r0 + y) * W + c0 + x];
+    const float pred = xv - sigma * ev;
+    const float d = (xv - pred) / sigma;
+    out[((long long)t * 4 + c) * per + p] = xv + d * (sigma_next - sigma);
+  }
+}
+
+extern "C" int fd_tlc_cfg_euler_step(const void* eps, const float* canvas, const int* row_org, int nr,
+                                     const int* col_org, int nc, int H, int W, int kh, int kw, int tile_begin,
+                                     int ntiles, int cfg, float guidance, float guidance_rescale, float sigma,
+                                     float sigma_next, float* out_tiles, int dtype, void* stream) {
+  if (!eps || !canvas || !row_org || !col_org || !out_tiles) return FD_ERR_ARG;
+  if (ntiles <= 0 || tile_begin < 0 || tile_begin + ntiles > nr * nc || (cfg != 1 && cfg != 2)) return FD_ERR_SHAPE;
+  if (sigma == 0.f) return FD_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (guidance_rescale > 0.f && cfg == 2) {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL(tlc_cfg_rescale_euler_kernel<T>, dim3(ntiles), dim3(256), 0, s,
+                                            (const T*)eps, canvas, row_org, col_org, nc, H, W, kh, kw, tile_begin,
+                                            guidance, guidance_rescale, sigma, sigma_next, out_tiles));
+  } else {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL(tlc_cfg_euler_kernel<T>, grid1d((long long)ntiles * kh * kw), dim3(256), 0,
+                                            s, (const T*)eps, canvas, row_org, col_org, nc, H, W, kh, kw, tile_begin,
+                                            ntiles, cfg, guidance, sigma, sigma_next, out_tiles));
+  }
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// grids_inverse: per canvas element, accumulate the covering tiles in tile order (row-major over the
+// origin grid), fp64 product rounded to fp32 per add -- the reference's  preds(fp32) += tile * w(fp64).
+__global__ void tlc_blend_kernel(const float* __restrict__ tiles, const double* __restrict__ wts,
+                                 const int* __restrict__ row_org, int nr, const int* __restrict__ col_org, int nc, int C,
+                                 int H, int W, int kh, int kw, float* __restrict__ canvas) {
+  const long long total = (long long)C * H * W;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int x = e % W;
+    const int y = (e / W) % H;
+    const int c = e / ((long long)W * H);
+    float pred = 0.f, cnt = 0.f;
+    for (int r = 0; r < nr; ++r) {
+      const int dy = y - row_org[r];
+      if (dy < 0 || dy >= kh) continue;
+      for (int q = 0; q < nc; ++q) {
+        const int dx = x - col_org[q];
+        if (dx < 0 || dx >= kw) continue;
+        const int t = r * nc + q;
+        const double w = wts[dy * kw + dx];
+        const float v = tiles[(((long long)t * C + c) * kh + dy) * kw + dx];
+        pred = (float)((double)pred + (double)v * w);
+        cnt = (float)((double)cnt + w);
+      }
+    }
+    canvas[e] = pred / cnt;
+  }
+}
+
+extern "C" int fd_tlc_blend(const float* tiles, const double* weights, const int* row_org, int nr, const int* col_org,
+                            int nc, int C, int H, int W, int kh, int kw, float* canvas, void* stream) {
+  if (!tiles || !weights || !row_org || !col_org || !canvas) return FD_ERR_ARG;
+  if (nr <= 0 || nc <= 0 || C <= 0 || kh > H || kw > W) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(tlc_blend_kernel, grid1d((long long)C * H * W), dim3(256), 0, s, tiles, weights, row_org, nr,
+                     col_org, nc, C, H, W, kh, kw, canvas);
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// grids on an NHWC canvas (image latents, 512 ch): tiles [n*cfg][kh][kw][C]
+template <typename T>
+__global__ void tlc_grids_nhwc_kernel(const T* __restrict__ canvas, const int* __restrict__ row_org,
+                                      const int* __restrict__ col_org, int nc, int H, int W, int C, int kh, int kw,
+                                      int tile_begin, int ntiles, int cfg, T* __restrict__ out) {
+  typedef typename VecT<T>::v8 V8;
+  const int VPR = C / 8;
+  const long long per = (long long)kh * kw * VPR;
+  const long long total = (long long)ntiles * per;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int t = e / per;
+    const long long r = e - (long long)t * per;
+    const int v = r % VPR;
+    const long long p = r / VPR;
+    const int y = p / kw, x = p - (long long)y * kw;
+    const int tid = tile_begin + t;
+    const int oy = row_org[tid / nc] + y, ox = col_org[tid % nc] + x;
+    const V8 val = *(const V8*)(canvas + ((long long)oy * W + ox) * C + v * 8);
+    for (int d = 0; d < cfg; ++d) *(V8*)(out + (((long long)(t * cfg + d)) * kh * kw + p) * C + v * 8) = val;
+  }
+}
+
+extern "C" int fd_tlc_grids_nhwc(const void* canvas, const int* row_org, int nr, const int* col_org, int nc, int H,
+                                 int W, int C, int kh, int kw, int tile_begin, int ntiles, int cfg, void* out, int dtype,
+                                 void* stream) {
+  if (!canvas || !row_org || !col_org || !out) return FD_ERR_ARG;
+  if (C % 8 || ntiles <= 0 || tile_begin + ntiles > nr * nc || kh > H || kw > W || cfg <= 0) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(tlc_grids_nhwc_kernel<T>, grid1d((long long)ntiles * kh * kw * C / 8),
+                                          dim3(256), 0, s, (const T*)canvas, row_org, col_org, nc, H, W, C, kh, kw,
+                                          tile_begin, ntiles, cfg, (T*)out));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// DiagonalGaussianDistribution.sample + scaling + DDPM add_noise at t=999 (pipeline:1271-1276), fused:
+// moments NHWC [HW][8] (mean 0..3, logvar 4..7) -> canvas fp32 NCHW [4][HW]
+//   z = (mean + exp(0.5*clamp(logvar,-30,20)) * post_eps) * scaling;  lat = a*z + b*(noise*init_sigma)
+template <typename TI>
+__global__ void vae_sample_add_noise_kernel(const TI* __restrict__ moments, const float* __restrict__ post_eps,
+                                            const float* __restrict__ noise, float* __restrict__ out, int HW,
+                                            float scaling, float init_sigma, float a, float b, int start_lr) {
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < 4LL * HW; e += (long long)gridDim.x * blockDim.x) {
+    const int c = e / HW;
+    const long long p = e - (long long)c * HW;
+    const float nz = noise[e] * init_sigma;
+    if (!start_lr) {
+      out[e] = nz;
+      continue;
+    }
+    const float mean = (float)moments[p * 8 + c];
+    float lv = (float)moments[p * 8 + 4 + c];
+    lv = fminf(fmaxf(lv, -30.f), 20.f);
+    const float z = (mean + expf(0.5f * lv) * post_eps[e]) * scaling;
+    out[e] = a * z + b * nz;
+  }
+}
+
+extern "C" int fd_vae_sample_add_noise(const void* moments, const float* post_eps, const float* noise, float* out,
+                                       int HW, float scaling, float init_sigma, float a, float b, int start_lr,
+                                       int dtype, void* stream) {
+  if (!noise || !out || (start_lr && (!moments || !post_eps))) return FD_ERR_ARG;
+  if (HW <= 0) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_I(dtype, hipLaunchKernelGGL(vae_sample_add_noise_kernel<TI>, grid1d(4LL * HW), dim3(256), 0, s,
+                                          (const TI*)moments, post_eps, noise, out, HW, scaling, init_sigma, a, b,
+                                          start_lr));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// VaeImageProcessor.postprocess in float: NHWC [HW][3] -> uint8 HWC  ((x/2+0.5).clamp(0,1)*255).round()
+template <typename TI>
+__global__ void postprocess_kernel(const TI* __restrict__ x, unsigned char* __restrict__ y, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float v = (float)x[i] / 2.f + 0.5f;
+    v = fminf(fmaxf(v, 0.f), 1.f);
+    y[i] = (unsigned char)rintf(v * 255.f);
+  }
+}
+
+extern "C" int fd_postprocess_u8(const void* x, void* y, long long n, int dtype, void* stream) {
+  if (!x || !y) return FD_ERR_ARG;
+  if (n <= 0) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_I(dtype, hipLaunchKernelGGL(postprocess_kernel<TI>, grid1d(n), dim3(256), 0, s, (const TI*)x,
+                                          (unsigned char*)y, n));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+extern "C" int fd_device_check(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return FD_ERR_HIP;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return FD_ERR_HIP;
+  const char* a = prop.gcnArchName;
+  if (!(a[0] == 'g' && a[1] == 'f' && a[2] == 'x' && a[3] == '9' && a[4] == '5' && a[5] == '0')) return FD_ERR_ARCH;
+  return FD_OK;
+}
+
+extern "C" const char* fd_version(void) { return "libfaithdiff_hip 0.1 gfx950"; }

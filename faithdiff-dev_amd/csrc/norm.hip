@@ -1,0 +1,233 @@
+// GroupNorm (+ fused SiLU) and LayerNorm for NHWC activations, fp32 statistics.  HBM-bound.
+//
+// GroupNorm runs as two launches so that a (batch, group) reduction of up to 16384 x 80 elements is
+// spread over the whole chip: (1) gn_partial: one block per (image, row-chunk) reads its rows once,
+// coalesced (16-B vectors along C), and writes per-group (sum, sumsq) partials; (2) gn_apply: every
+// block folds the partials of its image in fp64 (Chan-free E[x^2]-E[x]^2 in double), builds per-channel
+// scale/shift in LDS and streams its rows: y = x*scale[c] + shift[c] (+ SiLU), one FMA per element.
+#include "fd_common.h"
+
+#define GN_MAXC 2560
+
+static inline int gn_rows_per_chunk(int HW) {
+  // ~64 rows per chunk, at most 256 chunks per image
+  int r = 64;
+  while ((HW + r - 1) / r > 256) r *= 2;
+  return r;
+}
+
+template <typename T, int NV>
+__global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ x, float2* __restrict__ part, int HW,
+                                                         int C, int groups, int rows_per_chunk) {
+  typedef typename VecT<T>::v8 V8;
+  // per-(row-slot, channel) partials, reduced in a fixed order (bitwise reproducible; no atomics)
+  __shared__ float lds_s[256 * 8 * NV], lds_q[256 * 8 * NV];
+  __shared__ float ch_s[GN_MAXC], ch_q[GN_MAXC];
+  const int img = blockIdx.y, chunk = blockIdx.x;
+  const int VPR = C / (8 * NV);  // thread slots per row (each slot = NV vectors of 8)
+  const int RP = 256 / VPR;      // rows per pass
+  const int t = threadIdx.x;
+  const int v = t % VPR, ro = t / VPR;
+  float s[8 * NV], q[8 * NV];
+#pragma unroll
+  for (int i = 0; i < 8 * NV; ++i) s[i] = q[i] = 0.f;
+  const int r0 = chunk * rows_per_chunk;
+  const int r1 = min(r0 + rows_per_chunk, HW);
+  if (ro < RP) {
+    for (int r = r0 + ro; r < r1; r += RP) {
+      const T* row = x + ((long long)img * HW + r) * C;
+#pragma unroll
+      for (int n = 0; n < NV; ++n) {
+        const V8 val = *(const V8*)(row + (v + n * VPR) * 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float f = (float)val[i];
+          s[n * 8 + i] += f;
+          q[n * 8 + i] += f * f;
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NV; ++n)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        lds_s[ro * C + (v + n * VPR) * 8 + i] = s[n * 8 + i];
+        lds_q[ro * C + (v + n * VPR) * 8 + i] = q[n * 8 + i];
+      }
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < RP; ++r) {
+      a += lds_s[r * C + c];
+      b += lds_q[r * C + c];
+    }
+    ch_s[c] = a;
+    ch_q[c] = b;
+  }
+  __syncthreads();
+  const int cpg = C / groups;
+  if (t < groups) {
+    float a = 0.f, b = 0.f;
+    for (int c = t * cpg; c < (t + 1) * cpg; ++c) {
+      a += ch_s[c];
+      b += ch_q[c];
+    }
+    part[((long long)img * gridDim.x + chunk) * groups + t] = make_float2(a, b);
+  }
+}
+
+template <typename T, int NV>
+__global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                       const float2* __restrict__ part, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, int HW, int C, int groups,
+                                                       int nchunks, int rows_per_block, float eps, int silu) {
+  typedef typename VecT<T>::v8 V8;
+  __shared__ float sc[GN_MAXC], sh[GN_MAXC];
+  __shared__ float mean_s[64], rstd_s[64];
+  const int img = blockIdx.y;
+  const int t = threadIdx.x;
+  const int cpg = C / groups;
+  if (t < groups) {
+    double s = 0.0, q = 0.0;
+    const float2* p = part + (long long)img * nchunks * groups + t;
+    for (int c = 0; c < nchunks; ++c) {
+      const float2 v = p[(long long)c * groups];
+      s += v.x;
+      q += v.y;
+    }
+    const double n = (double)HW * cpg;
+    const double mean = s / n;
+    double var = q / n - mean * mean;
+    if (var < 0) var = 0;
+    mean_s[t] = (float)mean;
+    rstd_s[t] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += 256) {
+    const int g = c / cpg;
+    const float a = rstd_s[g] * (gamma ? gamma[c] : 1.f);
+    sc[c] = a;
+    sh[c] = (beta ? beta[c] : 0.f) - mean_s[g] * a;
+  }
+  __syncthreads();
+  const int VPR = C / 8;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(r0 + rows_per_block, HW);
+  const long long base = (long long)img * HW * C;
+  for (long long e = (long long)r0 * VPR + t; e < (long long)r1 * VPR; e += 256) {
+    const long long r = e / VPR;
+    const int v = e - r * VPR;
+    const V8 val = *(const V8*)(x + base + r * C + v * 8);
+    V8 out;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float f = (float)val[i] * sc[v * 8 + i] + sh[v * 8 + i];
+      if (silu) f = silu_f(f);
+      out[i] = (T)f;
+    }
+    *(V8*)(y + base + r * C + v * 8) = out;
+  }
+  (void)NV;
+}
+
+extern "C" long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups) {
+  const int rpc = gn_rows_per_chunk(HW);
+  const int nch = (HW + rpc - 1) / rpc;
+  return (long long)nimg * nch * groups * sizeof(float2);
+}
+
+extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
+                             int groups, float eps, int silu, int dtype, void* ws, void* stream) {
+  if (!x || !y || !ws) return FD_ERR_ARG;
+  if (nimg <= 0 || HW <= 0 || C <= 0 || groups <= 0 || groups > 64 || C % groups || C % 8 || C > GN_MAXC)
+    return FD_ERR_SHAPE;
+  const int rpc = gn_rows_per_chunk(HW);
+  const int nch = (HW + rpc - 1) / rpc;
+  hipStream_t s = (hipStream_t)stream;
+  const int NV = (C / 8 > 256) ? 2 : 1;
+  if (NV == 2 && (C % 16)) return FD_ERR_SHAPE;
+  // apply: ~32 rows per block
+  const int rpb = 32;
+  const int nblk = (HW + rpb - 1) / rpb;
+  if (NV == 1) {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_partial_kernel<T, 1>), dim3(nch, nimg), dim3(256), 0, s, (const T*)x,
+                                            (float2*)ws, HW, C, groups, rpc));
+  } else {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_partial_kernel<T, 2>), dim3(nch, nimg), dim3(256), 0, s, (const T*)x,
+                                            (float2*)ws, HW, C, groups, rpc));
+  }
+  FD_LAUNCH_CHECK();
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
+                                          (T*)y, (const float2*)ws, gamma, beta, HW, C, groups, nch, rpb, eps, silu));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// LayerNorm: one wave per row, 4 rows per 256-thread block; row kept in registers (C <= 2048).
+template <typename T>
+__global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x, long long ldx, T* __restrict__ y,
+                                                         long long ldy, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, int M, int C, float eps) {
+  typedef typename VecT<T>::v8 V8;
+  constexpr int MAXV = 4;  // up to 4 vectors of 8 per lane => C <= 2048
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int VPR = C / 8;
+  const T* xr = x + row * ldx;
+  float vals[MAXV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int v = lane + k * 64;
+    if (v < VPR) {
+      const V8 val = *(const V8*)(xr + v * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        vals[k][i] = (float)val[i];
+        s += vals[k][i];
+      }
+    }
+  }
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int v = lane + k * 64;
+    if (v < VPR) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = vals[k][i] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / C + eps);
+  T* yr = y + row * ldy;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int v = lane + k * 64;
+    if (v < VPR) {
+      V8 out;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = v * 8 + i;
+        out[i] = (T)((vals[k][i] - mean) * rstd * gamma[c] + beta[c]);
+      }
+      *(V8*)(yr + v * 8) = out;
+    }
+  }
+}
+
+extern "C" int fd_layer_norm(const void* x, long long ldx, void* y, long long ldy, const float* gamma,
+                             const float* beta, int M, int C, float eps, int dtype, void* stream) {
+  if (!x || !y || !gamma || !beta) return FD_ERR_ARG;
+  if (M <= 0 || C <= 0 || C % 8 || C > 2048 || (ldx & 7) || (ldy & 7)) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(layer_norm_kernel<T>, dim3((M + 3) / 4), dim3(256), 0, s, (const T*)x, ldx,
+                                          (T*)y, ldy, gamma, beta, M, C, eps));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}

@@ -1,0 +1,209 @@
+"""Architecture spec of the FaithDiff/SDXL UNet, the sdxl-vae-fp16-fix AutoencoderKL and the FaithDiff
+denoise encoder: parameter names (diffusers 0.28 state-dict keys) and shapes, plus a seeded random init.
+
+The reference loads real checkpoints by HF name (create_FaithDiff_model.py:13-16, CKPT_PTH.py:3-5); none
+exist offline, so the ``random-init`` path (BASELINE.json north star) draws every tensor from a per-key
+seeded generator: results do not depend on iteration order, and the same (key, seed) gives the same
+values on every host.  Zero-initialised modules of the reference (condition_embedding.conv_out,
+spatial_ch_projs, ext:209,399) are NOT zero here, so that the conditioning path is exercised.
+"""
+import zlib
+
+import torch
+
+UNET_CH = (320, 640, 1280)
+UNET_LAYERS = (0, 2, 10)
+UNET_HEADS = (5, 10, 20)
+VAE_CH = (128, 256, 512, 512)
+
+
+def _lin(d, name, n, k, bias=True):
+    d[name + ".weight"] = (n, k)
+    if bias:
+        d[name + ".bias"] = (n,)
+
+
+def _conv(d, name, co, ci, k=3, bias=True):
+    d[name + ".weight"] = (co, ci, k, k)
+    if bias:
+        d[name + ".bias"] = (co,)
+
+
+def _norm(d, name, c):
+    d[name + ".weight"] = (c,)
+    d[name + ".bias"] = (c,)
+
+
+def _resnet(d, p, cin, cout, temb=True):
+    _norm(d, p + ".norm1", cin)
+    _conv(d, p + ".conv1", cout, cin)
+    if temb:
+        _lin(d, p + ".time_emb_proj", cout, 1280)
+    _norm(d, p + ".norm2", cout)
+    _conv(d, p + ".conv2", cout, cout)
+    if cin != cout:
+        _conv(d, p + ".conv_shortcut", cout, cin, 1)
+
+
+def _t2d(d, p, c, layers):
+    _norm(d, p + ".norm", c)
+    _lin(d, p + ".proj_in", c, c)
+    for i in range(layers):
+        b = f"{p}.transformer_blocks.{i}"
+        _norm(d, b + ".norm1", c)
+        for n in ("to_q", "to_k", "to_v"):
+            _lin(d, f"{b}.attn1.{n}", c, c, bias=False)
+        _lin(d, b + ".attn1.to_out.0", c, c)
+        _norm(d, b + ".norm2", c)
+        _lin(d, b + ".attn2.to_q", c, c, bias=False)
+        _lin(d, b + ".attn2.to_k", c, 2048, bias=False)
+        _lin(d, b + ".attn2.to_v", c, 2048, bias=False)
+        _lin(d, b + ".attn2.to_out.0", c, c)
+        _norm(d, b + ".norm3", c)
+        _lin(d, b + ".ff.net.0.proj", 8 * c, c)
+        _lin(d, b + ".ff.net.2", c, 4 * c)
+    _lin(d, p + ".proj_out", c, c)
+
+
+def up_skip_channels():
+    C = UNET_CH
+    return [[C[2], C[2], C[1]], [C[1], C[1], C[0]], [C[0], C[0], C[0]]]
+
+
+def unet_param_shapes(with_extras=True):
+    """diffusers key -> shape for the SDXL UNet (+ FaithDiff extras, ext:389-403)."""
+    d = {}
+    C, Lr = UNET_CH, UNET_LAYERS
+    _conv(d, "conv_in", C[0], 4)
+    _lin(d, "time_embedding.linear_1", 1280, 320)
+    _lin(d, "time_embedding.linear_2", 1280, 1280)
+    _lin(d, "add_embedding.linear_1", 1280, 2816)
+    _lin(d, "add_embedding.linear_2", 1280, 1280)
+    prev = C[0]
+    for i in range(3):
+        for j in range(2):
+            _resnet(d, f"down_blocks.{i}.resnets.{j}", prev if j == 0 else C[i], C[i])
+            if Lr[i]:
+                _t2d(d, f"down_blocks.{i}.attentions.{j}", C[i], Lr[i])
+        if i < 2:
+            _conv(d, f"down_blocks.{i}.downsamplers.0.conv", C[i], C[i])
+        prev = C[i]
+    _resnet(d, "mid_block.resnets.0", C[2], C[2])
+    _t2d(d, "mid_block.attentions.0", C[2], Lr[2])
+    _resnet(d, "mid_block.resnets.1", C[2], C[2])
+    skips = up_skip_channels()
+    prev = C[2]
+    for i in range(3):
+        lvl = 2 - i
+        co = C[lvl]
+        for j in range(3):
+            cin = (prev if j == 0 else co) + skips[i][j]
+            _resnet(d, f"up_blocks.{i}.resnets.{j}", cin, co)
+            if Lr[lvl]:
+                _t2d(d, f"up_blocks.{i}.attentions.{j}", co, Lr[lvl])
+        if i < 2:
+            _conv(d, f"up_blocks.{i}.upsamplers.0.conv", co, co)
+        prev = co
+    _norm(d, "conv_norm_out", C[0])
+    _conv(d, "conv_out", 4, C[0])
+    if with_extras:
+        for i in range(2):
+            p = f"information_transformer_layes.{i}"
+            d[p + ".attn.in_proj_weight"] = (1920, 640)
+            d[p + ".attn.in_proj_bias"] = (1920,)
+            _lin(d, p + ".attn.out_proj", 640, 640)
+            _norm(d, p + ".ln_1", 640)
+            _lin(d, p + ".mlp.c_fc", 1280, 640)
+            _lin(d, p + ".mlp.c_proj", 640, 1280)
+            _norm(d, p + ".ln_2", 640)
+        _lin(d, "spatial_ch_projs", 320, 640)
+        _conv(d, "condition_embedding.conv_in", 512, 512)
+        _norm(d, "condition_embedding.norm_in", 512)
+        _conv(d, "condition_embedding.conv_out", 320, 512)
+    return d
+
+
+def _vae_attn(d, p, c):
+    _norm(d, p + ".group_norm", c)
+    for n in ("to_q", "to_k", "to_v", "to_out.0"):
+        _lin(d, f"{p}.{n}", c, c)
+
+
+def encoder_param_shapes(prefix="", with_out=True):
+    """VAE encoder trunk (diffusers Encoder); with_out=False is the FaithDiff denoise encoder (ext:39-196)."""
+    d = {}
+    ch = VAE_CH
+    _conv(d, prefix + "conv_in", ch[0], 3)
+    prev = ch[0]
+    for i, c in enumerate(ch):
+        for j in range(2):
+            _resnet(d, f"{prefix}down_blocks.{i}.resnets.{j}", prev if j == 0 else c, c, temb=False)
+        if i < 3:
+            _conv(d, f"{prefix}down_blocks.{i}.downsamplers.0.conv", c, c)
+        prev = c
+    _resnet(d, prefix + "mid_block.resnets.0", ch[-1], ch[-1], temb=False)
+    _vae_attn(d, prefix + "mid_block.attentions.0", ch[-1])
+    _resnet(d, prefix + "mid_block.resnets.1", ch[-1], ch[-1], temb=False)
+    if with_out:
+        _norm(d, prefix + "conv_norm_out", ch[-1])
+        _conv(d, prefix + "conv_out", 8, ch[-1])
+    return d
+
+
+def vae_param_shapes():
+    d = encoder_param_shapes("encoder.", True)
+    rch = tuple(reversed(VAE_CH))
+    _conv(d, "decoder.conv_in", rch[0], 4)
+    _resnet(d, "decoder.mid_block.resnets.0", rch[0], rch[0], temb=False)
+    _vae_attn(d, "decoder.mid_block.attentions.0", rch[0])
+    _resnet(d, "decoder.mid_block.resnets.1", rch[0], rch[0], temb=False)
+    prev = rch[0]
+    for i, c in enumerate(rch):
+        for j in range(3):
+            _resnet(d, f"decoder.up_blocks.{i}.resnets.{j}", prev if j == 0 else c, c, temb=False)
+        if i < 3:
+            _conv(d, f"decoder.up_blocks.{i}.upsamplers.0.conv", c, c)
+        prev = c
+    _norm(d, "decoder.conv_norm_out", rch[-1])
+    _conv(d, "decoder.conv_out", 3, rch[-1])
+    _conv(d, "quant_conv", 8, 8, 1)
+    _conv(d, "post_quant_conv", 4, 4, 1)
+    return d
+
+
+def _is_norm(name):
+    leaf = name.rsplit(".", 2)
+    return any(t in name for t in ("norm", "ln_")) and not name.endswith("weight") is False
+
+
+def random_init(shapes, seed=0, device="cpu", dtype=torch.float32, gain=1.0):
+    """Seeded per-key init: weights U(-1,1)*gain/sqrt(fan_in); biases U(-1,1)*0.05;
+    norm weights 1 + 0.1*U(-1,1); norm biases 0.05*U(-1,1)."""
+    sd = {}
+    for name, shape in shapes.items():
+        g = torch.Generator(device=device).manual_seed((zlib.crc32(name.encode()) ^ (seed * 0x9E3779B1)) & 0x7FFFFFFF)
+        u = torch.rand(shape, generator=g, device=device, dtype=torch.float32) * 2 - 1
+        is_norm = (".norm" in name or ".ln_" in name or name.startswith("conv_norm_out") or "group_norm" in name
+                   or "norm_in" in name or "conv_norm_out" in name)
+        if len(shape) == 1:
+            if is_norm and name.endswith("weight"):
+                t = 1.0 + 0.1 * u
+            else:
+                t = 0.05 * u
+        else:
+            fan_in = 1
+            for s in shape[1:]:
+                fan_in *= s
+            t = u * (gain / fan_in ** 0.5)
+        sd[name] = t.to(dtype)
+    return sd
+
+
+def count(shapes):
+    n = 0
+    for s in shapes.values():
+        k = 1
+        for x in s:
+            k *= x
+        n += k
+    return n

@@ -1,0 +1,257 @@
+"""Tensor-level wrappers over the C ABI.  Tensors are device buffers only; all arithmetic is HIP.
+
+Layout conventions: activations NHWC, flattened to [M, C] with M = n*H*W; Linear weights [N, K];
+3x3 conv weights pre-packed [Cout, 9*Cin] (tap-major, see pack_conv3x3).
+"""
+import ctypes
+
+import torch
+
+from . import lib as L
+
+_GN_WS = {}
+
+
+def _gn_ws(nbytes, device):
+    key = device
+    ws = _GN_WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _GN_WS[key] = ws
+    return ws
+
+
+def reserve_gn_workspace(nbytes, device):
+    """Pre-size the GroupNorm workspace (call before hipGraph capture)."""
+    _gn_ws(nbytes, device)
+
+
+# --------------------------------------------------------------------------------------- packing
+def pack_conv3x3(w):
+    """[Cout, Cin, 3, 3] -> [Cout, 9*Cin] with k = (ky*3 + kx)*Cin + c (tap-major, channel-contiguous)."""
+    co, ci, kh, kw = w.shape
+    return w.permute(0, 2, 3, 1).reshape(co, kh * kw * ci).contiguous()
+
+
+def pack_geglu(w, b):
+    """GEGLU proj [2F, K] -> rows interleaved in groups of 32 = [16 hidden | 16 gate] (fd_gemm GEGLU)."""
+    F2, K = w.shape
+    F = F2 // 2
+    h, g = w[:F].reshape(F // 16, 16, K), w[F:].reshape(F // 16, 16, K)
+    wp = torch.stack([h, g], dim=1).reshape(F2, K).contiguous()
+    bh, bg = b[:F].reshape(F // 16, 16), b[F:].reshape(F // 16, 16)
+    bp = torch.stack([bh, bg], dim=1).reshape(F2).contiguous()
+    return wp, bp
+
+
+# --------------------------------------------------------------------------------------- GEMM / conv
+def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=1, alpha=1.0, act="none",
+         out_dtype=None, batch=1, M=None, N=None, K=None, lda=None, ldw=None, ldc=None, ldr=None,
+         stride_a=0, stride_w=0, stride_c=0, stride_r=0):
+    """out[M, N (N/2 for geglu)] = epi(alpha * a[M, K] @ w[N, K]^T); strides default to the tensors'."""
+    K = a.shape[-1] if K is None else K
+    N = w.shape[-2] if N is None else N
+    ldw = w.stride(-2) if ldw is None else ldw
+    lda = a.stride(-2) if lda is None else lda
+    M = (a.numel() // a.shape[-1]) // batch if M is None else M
+    nout = N // 2 if act == "geglu" else N
+    odt = out_dtype or a.dtype
+    if out is None:
+        out = torch.empty((batch, M, nout) if batch > 1 else (M, nout), dtype=odt, device=a.device)
+    p = L.GemmParams()
+    p.A, p.B, p.C = a.data_ptr(), w.data_ptr(), out.data_ptr()
+    p.lda, p.ldb = lda, ldw
+    p.ldc = out.stride(-2) if ldc is None else ldc
+    p.strideA, p.strideB, p.strideC = stride_a, stride_w, stride_c
+    p.M, p.N, p.K, p.batch = M, N, K, batch
+    p.bias = bias.data_ptr() if bias is not None else None
+    if residual is not None:
+        p.residual = residual.data_ptr()
+        p.ldr = residual.stride(-2) if ldr is None else ldr
+        p.strideR = stride_r
+    if rowbias is not None:
+        p.rowbias, p.rowbias_ld = rowbias.data_ptr(), rowbias.stride(0)
+    p.rows_per_group = rows_per_group
+    p.alpha = alpha
+    p.act = L.ACT[act]
+    p.dtype = L.dtype_code(a.dtype)
+    p.out_dtype = L.dtype_code(odt)
+    L.check(L.load().fd_gemm(ctypes.byref(p), L.stream()), "fd_gemm")
+    return out
+
+
+def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C1=None, out=None, rowbias=None,
+            residual=None, act="none", out_dtype=None):
+    """Implicit-GEMM 3x3 conv on NHWC x [nimg*H*W, Cin] (or concat(x, x2) along C) with packed weight wp."""
+    Cout, K = wp.shape
+    Cin = K // 9
+    Hl, Wl = (2 * H, 2 * W) if upsample else (H, W)
+    Hout = (Hl + 2 * pad - 3) // stride + 1
+    Wout = (Wl + 2 * pad - 3) // stride + 1
+    if stride == 2 and pad == 0:  # VAE Downsample2D: F.pad (0,1,0,1) then conv(k3, s2, p0)
+        Hout, Wout = Hl // 2, Wl // 2
+    M = nimg * Hout * Wout
+    odt = out_dtype or x.dtype
+    if out is None:
+        out = torch.empty((M, Cout), dtype=odt, device=x.device)
+    p = L.GemmParams()
+    p.A, p.B, p.C = x.data_ptr(), wp.data_ptr(), out.data_ptr()
+    p.C1 = 0 if x2 is None else C1
+    p.lda = Cin if x2 is None else C1
+    p.ldb, p.ldc = K, out.stride(-2)
+    p.M, p.N, p.K, p.batch = M, Cout, K, 1
+    p.bias = bias.data_ptr() if bias is not None else None
+    if residual is not None:
+        p.residual, p.ldr = residual.data_ptr(), residual.stride(-2)
+    if rowbias is not None:
+        p.rowbias, p.rowbias_ld, p.rows_per_group = rowbias.data_ptr(), rowbias.stride(0), Hout * Wout
+    else:
+        p.rows_per_group = 1
+    p.alpha, p.act = 1.0, L.ACT[act]
+    p.dtype, p.out_dtype = L.dtype_code(x.dtype), L.dtype_code(odt)
+    p.conv, p.nimg, p.Hin, p.Win, p.Cin = 1, nimg, H, W, Cin
+    p.Hout, p.Wout, p.stride, p.pad, p.upsample = Hout, Wout, stride, pad, int(upsample)
+    p.A2 = x2.data_ptr() if x2 is not None else None
+    L.check(L.load().fd_gemm(ctypes.byref(p), L.stream()), "fd_gemm(conv)")
+    return out
+
+
+def conv_direct(x, w, bias, nimg, H, W, Cin, ksize=3, stride=1, pad=1, in_scale=1.0, out_dtype=None, out=None):
+    """Direct conv for Cin < 64: x NHWC, w fp32 [Cout, k, k, Cin]."""
+    Cout = w.shape[0]
+    Hout, Wout = (H + 2 * pad - ksize) // stride + 1, (W + 2 * pad - ksize) // stride + 1
+    odt = out_dtype or x.dtype
+    if out is None:
+        out = torch.empty((nimg * Hout * Wout, Cout), dtype=odt, device=x.device)
+    L.check(L.load().fd_conv2d_direct(L.ptr(x), L.ptr(w), L.ptr(bias), L.ptr(out), nimg, H, W, Cin, Cout, ksize,
+                                      stride, pad, in_scale, L.dtype_code(x.dtype), L.dtype_code(odt), L.stream()),
+            "fd_conv2d_direct")
+    return out
+
+
+# --------------------------------------------------------------------------------------- norms
+def group_norm(x, gamma, beta, nimg, HW, C, groups=32, eps=1e-5, silu=False, out=None):
+    if out is None:
+        out = torch.empty_like(x)
+    nb = L.load().fd_group_norm_ws_bytes(nimg, HW, C, groups)
+    ws = _gn_ws(nb, x.device)
+    L.check(L.load().fd_group_norm(L.ptr(x), L.ptr(out), L.ptr(gamma), L.ptr(beta), nimg, HW, C, groups, eps,
+                                   int(silu), L.dtype_code(x.dtype), L.ptr(ws), L.stream()), "fd_group_norm")
+    return out
+
+
+def layer_norm(x, gamma, beta, eps=1e-5, out=None, M=None, ldx=None):
+    C = gamma.shape[0]
+    M = x.numel() // x.shape[-1] if M is None else M
+    if out is None:
+        out = torch.empty((M, C), dtype=x.dtype, device=x.device)
+    L.check(L.load().fd_layer_norm(L.ptr(x), x.stride(-2) if ldx is None else ldx, L.ptr(out), out.stride(-2),
+                                   L.ptr(gamma), L.ptr(beta), M, C, eps, L.dtype_code(x.dtype), L.stream()),
+            "fd_layer_norm")
+    return out
+
+
+# --------------------------------------------------------------------------------------- attention
+def flash_attn(q, k, v, out, batch, heads, Lq, Lk, ldq, ldk, ldv, ldo, qbs, kbs, vbs, obs, kv_mod=0, scale=0.125):
+    L.check(L.load().fd_flash_attn(L.ptr(q), ldq, qbs, L.ptr(k), ldk, kbs, L.ptr(v), ldv, vbs, L.ptr(out), ldo, obs,
+                                   batch, heads, Lq, Lk, kv_mod, scale, L.dtype_code(q.dtype), L.stream()),
+            "fd_flash_attn")
+    return out
+
+
+def mha_seq_axis(qkv, out, L_, groups, N, E, heads):
+    L.check(L.load().fd_mha_seq_axis(L.ptr(qkv), L.ptr(out), L_, groups, N, E, heads, L.dtype_code(qkv.dtype),
+                                     L.stream()), "fd_mha_seq_axis")
+    return out
+
+
+def softmax_rows(s, out, R, C, scale):
+    L.check(L.load().fd_softmax_rows(L.ptr(s), L.ptr(out), R, C, scale, L.dtype_code(out.dtype), L.stream()),
+            "fd_softmax_rows")
+    return out
+
+
+# --------------------------------------------------------------------------------------- elementwise
+def concat_channels(a, C1, b, C2, out, M):
+    L.check(L.load().fd_concat_channels(L.ptr(a), C1, L.ptr(b), C2, L.ptr(out), M, L.dtype_code(a.dtype), L.stream()),
+            "fd_concat_channels")
+    return out
+
+
+def unary(x, out, act="none"):
+    L.check(L.load().fd_unary(L.ptr(x), L.ptr(out), x.numel(), L.ACT[act], L.dtype_code(x.dtype),
+                              L.dtype_code(out.dtype), L.stream()), "fd_unary")
+    return out
+
+
+def add_strided(x, ldx, a, lda, out, ldy, M, N):
+    L.check(L.load().fd_add_strided(L.ptr(x), ldx, L.ptr(a), lda, L.ptr(out), ldy, M, N, L.dtype_code(x.dtype),
+                                    L.dtype_code(out.dtype), L.stream()), "fd_add_strided")
+    return out
+
+
+def nchw_to_nhwc(x, out, nimg, C, HW, scale=1.0):
+    L.check(L.load().fd_nchw_to_nhwc(L.ptr(x), L.ptr(out), nimg, C, HW, scale, L.dtype_code(x.dtype),
+                                     L.dtype_code(out.dtype), L.stream()), "fd_nchw_to_nhwc")
+    return out
+
+
+def nhwc_to_nchw(x, out, nimg, C, HW, scale=1.0):
+    L.check(L.load().fd_nhwc_to_nchw(L.ptr(x), L.ptr(out), nimg, C, HW, scale, L.dtype_code(x.dtype),
+                                     L.dtype_code(out.dtype), L.stream()), "fd_nhwc_to_nchw")
+    return out
+
+
+def transpose(x, ldx, out, ldy, R, C, batch=1, sx=0, sy=0):
+    L.check(L.load().fd_transpose(L.ptr(x), ldx, L.ptr(out), ldy, R, C, batch, sx, sy, L.dtype_code(x.dtype),
+                                  L.stream()), "fd_transpose")
+    return out
+
+
+def time_features(t, time_ids, text_embeds, tfeat, afeat, batch):
+    L.check(L.load().fd_time_features(L.ptr(t), L.ptr(time_ids), L.ptr(text_embeds), L.ptr(tfeat), L.ptr(afeat), batch,
+                                      L.dtype_code(tfeat.dtype), L.stream()), "fd_time_features")
+
+
+# --------------------------------------------------------------------------------------- denoise loop
+def tlc_scale_input(canvas, row_org, col_org, H, W, kh, kw, tile_begin, ntiles, cfg, sigma, out):
+    L.check(L.load().fd_tlc_scale_input(L.ptr(canvas), L.ptr(row_org), row_org.numel(), L.ptr(col_org),
+                                        col_org.numel(), H, W, kh, kw, tile_begin, ntiles, cfg, sigma, L.ptr(out),
+                                        L.dtype_code(out.dtype), L.stream()), "fd_tlc_scale_input")
+    return out
+
+
+def tlc_cfg_euler_step(eps, canvas, row_org, col_org, H, W, kh, kw, tile_begin, ntiles, cfg, guidance, rescale, sigma,
+                       sigma_next, out_tiles):
+    L.check(L.load().fd_tlc_cfg_euler_step(L.ptr(eps), L.ptr(canvas), L.ptr(row_org), row_org.numel(), L.ptr(col_org),
+                                           col_org.numel(), H, W, kh, kw, tile_begin, ntiles, cfg, guidance, rescale,
+                                           sigma, sigma_next, L.ptr(out_tiles), L.dtype_code(eps.dtype), L.stream()),
+            "fd_tlc_cfg_euler_step")
+    return out_tiles
+
+
+def tlc_blend(tiles, weights, row_org, col_org, C, H, W, kh, kw, canvas):
+    L.check(L.load().fd_tlc_blend(L.ptr(tiles), L.ptr(weights), L.ptr(row_org), row_org.numel(), L.ptr(col_org),
+                                  col_org.numel(), C, H, W, kh, kw, L.ptr(canvas), L.stream()), "fd_tlc_blend")
+    return canvas
+
+
+def tlc_grids_nhwc(canvas, row_org, col_org, H, W, C, kh, kw, tile_begin, ntiles, cfg, out):
+    L.check(L.load().fd_tlc_grids_nhwc(L.ptr(canvas), L.ptr(row_org), row_org.numel(), L.ptr(col_org), col_org.numel(),
+                                       H, W, C, kh, kw, tile_begin, ntiles, cfg, L.ptr(out), L.dtype_code(canvas.dtype),
+                                       L.stream()), "fd_tlc_grids_nhwc")
+    return out
+
+
+def vae_sample_add_noise(moments, post_eps, noise, out, HW, scaling, init_sigma, a, b, start_lr):
+    L.check(L.load().fd_vae_sample_add_noise(L.ptr(moments), L.ptr(post_eps), L.ptr(noise), L.ptr(out), HW, scaling,
+                                             init_sigma, a, b, int(start_lr),
+                                             L.dtype_code(moments.dtype) if moments is not None else 0, L.stream()),
+            "fd_vae_sample_add_noise")
+    return out
+
+
+def postprocess_u8(x, out):
+    L.check(L.load().fd_postprocess_u8(L.ptr(x), L.ptr(out), x.numel(), L.dtype_code(x.dtype), L.stream()),
+            "fd_postprocess_u8")
+    return out

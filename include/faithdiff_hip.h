@@ -1,0 +1,194 @@
+/*
+ * faithdiff_hip.h -- C ABI of libfaithdiff_hip.so, the MI355X (gfx950) device path of the
+ * FaithDiff denoising hot path.
+ *
+ * The reference (tpetkovich/FaithDiff-dev) owns no native code: every op below replaces an
+ * *implicit* ATen kernel that diffusers 0.28 / torch 2.4 launch for it.  The
+ * reference call site each entry point replaces is cited next to it.
+ *
+ * Conventions
+ *   - Activations are NHWC ("[M, C]" row-major with M = batch*H*W); weights row-major [N][K].
+ *   - dtype codes: FD_BF16 (UNet), FD_F16 (VAE / denoise encoder), FD_F32.
+ *   - Every function returns 0 (FD_OK) or a negative fd_status; the Python layer raises
+ *     RuntimeError on non-zero.  No allocation and no host synchronisation happens inside an op,
+ *     so every op is capturable into a hipGraph.  Caller owns every buffer.
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).
+ */
+#ifndef FAITHDIFF_HIP_H
+#define FAITHDIFF_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  FD_OK = 0,
+  FD_ERR_SHAPE = -1,   /* unsupported / inconsistent shape */
+  FD_ERR_DTYPE = -2,   /* unsupported dtype combination */
+  FD_ERR_ARCH = -3,    /* device is not gfx950 */
+  FD_ERR_HIP = -4,     /* a HIP runtime call failed (launch error) */
+  FD_ERR_ARG = -5      /* null pointer / bad argument */
+} fd_status;
+
+enum { FD_BF16 = 0, FD_F16 = 1, FD_F32 = 2 };
+enum { FD_ACT_NONE = 0, FD_ACT_SILU = 1, FD_ACT_GELU = 2, FD_ACT_QUICKGELU = 3, FD_ACT_GEGLU = 4 };
+
+/* ---------------------------------------------------------------------------------------------
+ * GEMM / implicit-GEMM convolution on MFMA (v_mfma_f32_16x16x32_{bf16,f16}), LDS double-buffered
+ * via global_load_lds.  C[b][m][n] = epi( alpha * sum_k A[b][m][k] * B[b][n][k] ).
+ *   epi(v) = act(v + bias[n] + rowbias[(m / rows_per_group) * rowbias_ld + n]) + residual[m][n]
+ *   act == FD_ACT_GEGLU: B rows are packed in groups of 32 = [16 "hidden" | 16 "gate"]; the
+ *   output has N/2 columns: out = (h + b_h) * gelu(g + b_g)   (diffusers GEGLU).
+ * conv != 0 turns A into an implicit im2col gather from an NHWC image (K = 9*Cin, tap-major):
+ *   3x3 kernel, stride 1|2, symmetric pad `pad` (bottom/right zero-fill handles the VAE's
+ *   (0,1,0,1) pad with pad = 0), optional nearest x2 upsample folded into the gather
+ *   (Upsample2D), optional channel concat of two sources (A: C1 channels, A2: Cin-C1 channels).
+ * Replaces: cuBLAS addmm/mm behind every nn.Linear and cuDNN conv2d behind every nn.Conv2d of
+ *   ResnetBlock2D / Transformer2DModel / Down-/Upsample2D (diffusers; called from
+ *   unet_2d_condition_vae_extension.py:571-690 and pipeline_FaithDiff_tlc.py:970,1272,1438).
+ * Requires K % 64 == 0 (and Cin % 64 == 0, C1 % 64 == 0 for conv).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct fd_gemm_params {
+  const void* A;
+  const void* B;
+  void* C;
+  long long lda, ldb, ldc;
+  long long strideA, strideB, strideC;
+  int M, N, K, batch;
+  const float* bias;
+  const void* residual;
+  long long ldr, strideR;
+  const float* rowbias;
+  long long rowbias_ld;
+  int rows_per_group;
+  float alpha;
+  int act;
+  int dtype;
+  int out_dtype;
+  /* implicit-GEMM conv */
+  int conv;
+  int nimg, Hin, Win, Cin, Hout, Wout, stride, pad, upsample;
+  const void* A2;
+  int C1;
+} fd_gemm_params;
+
+int fd_gemm(const fd_gemm_params* p, void* stream);
+
+/* Direct convolution for the few convs with Cin < 64 (UNet conv_in 4->320, VAE conv_in 3->128,
+ * decoder conv_in 4->512, quant_conv / post_quant_conv 1x1).  x NHWC (dtype), w fp32
+ * [Cout][kh][kw][Cin], bias fp32, y NHWC (out_dtype).  in_scale multiplies x on load.
+ * Replaces: cuDNN conv2d of those layers (ext:571; diffusers Encoder/Decoder conv_in). */
+int fd_conv2d_direct(const void* x, const float* w, const float* bias, void* y, int nimg, int Hin, int Win,
+                     int Cin, int Cout, int ksize, int stride, int pad, float in_scale, int dtype, int out_dtype,
+                     void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * GroupNorm over NHWC x[nimg][HW][C] (32 groups typical), fp32 statistics, optional fused SiLU.
+ * Two launches (partial stats, then normalise); `ws` must hold fd_group_norm_ws_bytes() bytes.
+ * Replaces: torch native_group_norm (+ silu) in ResnetBlock2D.norm1/2, Transformer2DModel.norm,
+ *   conv_norm_out, ControlNetConditioningEmbedding.norm_in (ext:208,215), VAE attention group_norm.
+ * ------------------------------------------------------------------------------------------- */
+long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups);
+int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
+                  int groups, float eps, int silu, int dtype, void* ws, void* stream);
+
+/* LayerNorm over the last dim of x[M][C] (row stride ldx), fp32 stats; y[M][C] (ldy).
+ * Replaces: torch layer_norm in BasicTransformerBlock.norm1/2/3 and ResidualAttentionBlock.ln_1/2
+ *   (ext:243,248,258-259). */
+int fd_layer_norm(const void* x, long long ldx, void* y, long long ldy, const float* gamma, const float* beta,
+                  int M, int C, float eps, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Flash attention forward, head_dim 64, online softmax in fp32, MFMA for QK^T and PV.
+ * q/k/v/o are row-major token matrices; head h of batch b lives at
+ *   q + b*q_bstride + t*ldq + h*64 (same for o); k/v use batch index (kv_mod ? b % kv_mod : b), so
+ *   the cross-attention K/V of the [neg, pos] prompt pair serve every tile of a batched forward.
+ *   Lk may be any size (masked tail).
+ * Replaces: SDPA (flash / mem-efficient) behind diffusers AttnProcessor2_0 for attn1 (self,
+ *   T = 4096 / 1024 per tile) and attn2 (cross, Lk = 77) of all 70 BasicTransformerBlocks.
+ * ------------------------------------------------------------------------------------------- */
+int fd_flash_attn(const void* q, long long ldq, long long q_bstride, const void* k, long long ldk,
+                  long long k_bstride, const void* v, long long ldv, long long v_bstride, void* o, long long ldo,
+                  long long o_bstride, int batch, int heads, int Lq, int Lk, int kv_mod, float scale, int dtype,
+                  void* stream);
+
+/* The information transformer's nn.MultiheadAttention(640, 8) with batch_first=False fed
+ * (L=B, N=HW, E) (ext:242,251-254,576-577): for each pixel n, softmax attention over the L rows of
+ * each of `groups` consecutive row groups (one group = one tile's CFG pair when tiles are batched).
+ * qkv: [groups*L][N][3E] (in_proj output), o: [groups*L][N][E].  L <= 8; exact for distinct rows. */
+int fd_mha_seq_axis(const void* qkv, void* o, int L, int groups, int N, int E, int heads, int dtype, void* stream);
+
+/* Row softmax of fp32 scores s[R][C] (scaled by `scale`) into p (dtype).  With fd_gemm this forms
+ * the single-head d=512 VAE mid-block attention (diffusers Attention, 1 head, upcast softmax). */
+int fd_softmax_rows(const float* s, void* p, int R, int C, float scale, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Elementwise / layout helpers (all HBM-bound).
+ * ------------------------------------------------------------------------------------------- */
+/* y[m][0:C1] = a[m][0:C1], y[m][C1:C1+C2] = b[m][0:C2]  (up-block skip concat, diffusers
+ * CrossAttnUpBlock2D / UpBlock2D torch.cat) */
+int fd_concat_channels(const void* a, int C1, const void* b, int C2, void* y, long long M, int dtype, void* stream);
+/* y = act(x) elementwise, n elements; also casts dtype -> out_dtype (act 0 = copy/cast). */
+int fd_unary(const void* x, void* y, long long n, int act, int dtype, int out_dtype, void* stream);
+/* y[m][n] = x[m][n] (+ a[m][n] if a != NULL), general row strides; dtype cast allowed. */
+int fd_add_strided(const void* x, long long ldx, const void* a, long long lda, void* y, long long ldy, int M, int N,
+                   int dtype, int out_dtype, void* stream);
+/* NCHW <-> NHWC transposes (dtype in, out_dtype out; scale applied). */
+int fd_nchw_to_nhwc(const void* x, void* y, int nimg, int C, int HW, float scale, int dtype, int out_dtype,
+                    void* stream);
+int fd_nhwc_to_nchw(const void* x, void* y, int nimg, int C, int HW, float scale, int dtype, int out_dtype,
+                    void* stream);
+/* 2-D transpose y[C][R] = x[R][C] with batch (VAE attention V^T). */
+int fd_transpose(const void* x, long long ldx, void* y, long long ldy, int R, int C, int batch, long long sx,
+                 long long sy, int dtype, void* stream);
+
+/* SDXL time / micro-conditioning features (diffusers get_timestep_embedding, flip_sin_to_cos, shift 0;
+ * ext:543-561): tfeat[b][0:320] = sinusoid(t[b]); afeat[b] = [text_embeds[b] (1280) |
+ * sinusoid_256(time_ids[b][0..5])].  t, time_ids, text_embeds fp32 on device; outputs dtype. */
+int fd_time_features(const float* t, const float* time_ids, const float* text_embeds, void* tfeat, void* afeat,
+                     int batch, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Denoise-loop fusions (pipeline_FaithDiff_tlc.py:1271-1409).  The latent canvas is fp32 NCHW
+ * [4][H][W]; tile t of the TLC grid has origin (row_org[t / nc], col_org[t % nc]) -- the row-major
+ * Cartesian order LocalAttention.grids (:160-205) produces; tiles [tile_begin, tile_begin+ntiles)
+ * are this call's (a rank's shard when tiles are spread over GPUs).
+ * ------------------------------------------------------------------------------------------- */
+/* grids + CFG duplicate + EulerDiscreteScheduler.scale_model_input (:1326,1334-1336):
+ * out NHWC dtype [ntiles*cfg][kh*kw][4] = canvas tile / sqrt(sigma^2 + 1). */
+int fd_tlc_scale_input(const float* canvas, const int* row_org, int nr, const int* col_org, int nc, int H, int W,
+                       int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma, void* out, int dtype,
+                       void* stream);
+/* CFG combine (+ rescale_noise_cfg when guidance_rescale > 0, :286-305,1363-1369) and the Euler step
+ * (:1373; gamma = 0, fp32): eps NHWC [ntiles*cfg][kh*kw][4] (uncond row first), x = canvas tile,
+ * out_tiles fp32 NCHW [ntiles][4][kh][kw] = x + ((x - (x - sigma*e)) / sigma) * (sigma_next - sigma). */
+int fd_tlc_cfg_euler_step(const void* eps, const float* canvas, const int* row_org, int nr, const int* col_org, int nc,
+                          int H, int W, int kh, int kw, int tile_begin, int ntiles, int cfg, float guidance,
+                          float guidance_rescale, float sigma, float sigma_next, float* out_tiles, int dtype,
+                          void* stream);
+/* LocalAttention.grids_inverse (:230-252): canvas[c][y][x] = sum_t tile*w / sum_t w over the covering
+ * tiles in tile order, each product in fp64 rounded to fp32 per add exactly like the reference's
+ * fp32 canvas += tile * fp64 weight.  weights fp64 [kh][kw] (_gaussian_weights, :207-228). */
+int fd_tlc_blend(const float* tiles, const double* weights, const int* row_org, int nr, const int* col_org, int nc,
+                 int C, int H, int W, int kh, int kw, float* canvas, void* stream);
+/* LocalAttention.grids on the NHWC image-latent canvas [H][W][C] (:1257) + CFG duplicate (:1335):
+ * out [ntiles*cfg][kh][kw][C]. */
+int fd_tlc_grids_nhwc(const void* canvas, const int* row_org, int nr, const int* col_org, int nc, int H, int W, int C,
+                      int kh, int kw, int tile_begin, int ntiles, int cfg, void* out, int dtype, void* stream);
+/* prepare_latents + start_point 'lr' (:820-835, 1271-1276): moments NHWC [HW][8] (VAE quant_conv
+ * output), post_eps/noise fp32 NCHW [4][HW];  out = a * (mean + exp(0.5 clamp(logvar,-30,20)) *
+ * post_eps) * scaling + b * noise * init_sigma   (a, b = DDPM add_noise coefficients at t = 999);
+ * start_lr == 0: out = noise * init_sigma. */
+int fd_vae_sample_add_noise(const void* moments, const float* post_eps, const float* noise, float* out, int HW,
+                            float scaling, float init_sigma, float a, float b, int start_lr, int dtype, void* stream);
+/* VaeImageProcessor.postprocess (:1451): uint8 = round(clamp(x/2 + 0.5, 0, 1) * 255). */
+int fd_postprocess_u8(const void* x, void* y, long long n, int dtype, void* stream);
+
+/* library / device checks */
+int fd_device_check(void);
+const char* fd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,326 @@
+"""Per-kernel parity of the HIP library (via the C ABI) against plain fp32 references.
+
+Tolerances (stated per test) follow from bf16/fp16 storage: the kernels accumulate in fp32 and round
+once on store, so the relative L2 error vs an fp32 reference computed from the *same* rounded inputs
+is ~2^-9 (bf16) / 2^-12 (fp16) per stored value.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _dev():
+    from fdhip import lib
+    lib.require_device()
+    torch.manual_seed(0)
+
+
+def rel_l2(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def maxrel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+TOL = {torch.bfloat16: 6e-3, torch.float16: 1.5e-3}
+
+
+def rnd(*shape, dtype=torch.bfloat16, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(dtype)
+
+
+# ------------------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(8192, 640, 640), (2048, 1280, 1280), (2048, 3840, 1280), (77, 1280, 2048),
+                                   (2, 1280, 320), (300, 200, 128), (32768, 320, 640), (1000, 4, 2880)])
+def test_gemm_plain(dtype, M, N, K):
+    from fdhip import ops
+    a, w = rnd(M, K, dtype=dtype), rnd(N, K, dtype=dtype, scale=K ** -0.5)
+    b = torch.randn(N, device=DEV)
+    out = ops.gemm(a, w, bias=b)
+    ref = a.float() @ w.float().T + b
+    assert rel_l2(out, ref) < TOL[dtype], rel_l2(out, ref)
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu", "quickgelu"])
+def test_gemm_act_residual_rowbias(act):
+    from fdhip import ops
+    M, N, K = 1024, 640, 1280
+    a, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    bias = torch.randn(N, device=DEV)
+    res = rnd(M, N)
+    rowb = torch.randn(4, N, device=DEV)
+    out = ops.gemm(a, w, bias=bias, residual=res, rowbias=rowb, rows_per_group=M // 4, act=act)
+    v = a.float() @ w.float().T + bias + rowb.repeat_interleave(M // 4, 0)
+    v = {"silu": F.silu, "gelu": F.gelu, "quickgelu": lambda x: x * torch.sigmoid(1.702 * x)}[act](v)
+    ref = v + res.float()
+    assert rel_l2(out, ref) < 6e-3
+
+
+def test_gemm_geglu_packed():
+    from fdhip import ops
+    M, C, Fd = 2048, 640, 2560
+    x = rnd(M, C)
+    w = rnd(2 * Fd, C, scale=C ** -0.5)
+    b = torch.randn(2 * Fd, device=DEV) * 0.1
+    wp, bp = ops.pack_geglu(w, b)
+    out = ops.gemm(x, wp, bias=bp, act="geglu")
+    assert out.shape == (M, Fd)
+    h, g = (x.float() @ w.float().T + b).chunk(2, dim=-1)
+    ref = h * F.gelu(g)
+    assert rel_l2(out, ref) < 6e-3
+
+
+def test_gemm_batched_strided_f32_out():
+    from fdhip import ops
+    B, T, D = 2, 1000, 512
+    q, k = rnd(B, T, D, dtype=torch.float16), rnd(B, T, D, dtype=torch.float16)
+    s = ops.gemm(q, k, batch=B, M=T, N=T, K=D, stride_a=T * D, stride_w=T * D, stride_c=T * T, alpha=D ** -0.5,
+                 out_dtype=torch.float32)
+    ref = torch.einsum("btd,bsd->bts", q.float(), k.float()) * D ** -0.5
+    assert rel_l2(s, ref) < 1e-5 * 100
+
+
+# ------------------------------------------------------------------------------------------ conv
+def conv_ref(x_nhwc, w, b, nimg, H, W, stride, pad, upsample=False, vae_pad=False):
+    x = x_nhwc.float().reshape(nimg, H, W, -1).permute(0, 3, 1, 2)
+    if upsample:
+        x = F.interpolate(x, scale_factor=2.0, mode="nearest")
+    if vae_pad:
+        x = F.pad(x, (0, 1, 0, 1))
+    y = F.conv2d(x, w.float(), b, stride=stride, padding=pad)
+    return y.permute(0, 2, 3, 1).reshape(-1, w.shape[0])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nimg,H,W,Cin,Cout,stride,pad,up", [
+    (2, 128, 128, 320, 320, 1, 1, False), (2, 32, 32, 1280, 1280, 1, 1, False), (2, 64, 64, 640, 640, 2, 1, False),
+    (1, 33, 47, 128, 256, 1, 1, False), (1, 64, 64, 128, 128, 2, 0, False), (2, 32, 32, 1280, 1280, 1, 1, True),
+    (1, 40, 24, 256, 3, 1, 1, False), (2, 16, 16, 320, 4, 1, 1, False)])
+def test_conv3x3(dtype, nimg, H, W, Cin, Cout, stride, pad, up):
+    from fdhip import ops
+    x = rnd(nimg * H * W, Cin, dtype=dtype)
+    w = (torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)).to(dtype)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    out = ops.conv3x3(x, ops.pack_conv3x3(w), b, nimg, H, W, stride=stride, pad=pad, upsample=up)
+    ref = conv_ref(x, w, b, nimg, H, W, stride, pad, up, vae_pad=(stride == 2 and pad == 0))
+    assert out.shape == ref.shape
+    assert rel_l2(out, ref) < TOL[dtype], rel_l2(out, ref)
+
+
+def test_conv3x3_concat_temb_residual():
+    from fdhip import ops
+    nimg, H, W, C1, C2, Cout = 2, 32, 32, 1280, 640, 1280
+    x1, x2 = rnd(nimg * H * W, C1), rnd(nimg * H * W, C2)
+    w = (torch.randn(Cout, C1 + C2, 3, 3, device=DEV) / math.sqrt(9 * (C1 + C2))).to(torch.bfloat16)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    temb = torch.randn(nimg, Cout, device=DEV)
+    res = rnd(nimg * H * W, Cout)
+    out = ops.conv3x3(x1, ops.pack_conv3x3(w), b, nimg, H, W, x2=x2, C1=C1, rowbias=temb, residual=res)
+    ref = conv_ref(torch.cat([x1, x2], 1), w, b, nimg, H, W, 1, 1) + temb.repeat_interleave(H * W, 0) + res.float()
+    assert rel_l2(out, ref) < 6e-3
+
+
+@pytest.mark.parametrize("Cin,Cout,k", [(4, 320, 3), (3, 128, 3), (8, 8, 1), (4, 512, 3)])
+def test_conv_direct(Cin, Cout, k):
+    from fdhip import ops
+    nimg, H, W = 2, 37, 29
+    x = rnd(nimg * H * W, Cin, dtype=torch.float16)
+    w = torch.randn(Cout, Cin, k, k, device=DEV) / math.sqrt(k * k * Cin)
+    b = torch.randn(Cout, device=DEV)
+    out = ops.conv_direct(x, w.permute(0, 2, 3, 1).contiguous(), b, nimg, H, W, Cin, ksize=k, pad=k // 2,
+                          out_dtype=torch.float32)
+    ref = conv_ref(x, w, b, nimg, H, W, 1, k // 2)
+    assert rel_l2(out, ref) < 1e-5
+
+
+# ------------------------------------------------------------------------------------------ norms
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nimg,HW,C", [(2, 16384, 320), (2, 4096, 640), (2, 1024, 2560), (2, 1024, 1920),
+                                       (1, 65536, 128), (1, 16384, 512), (2, 4096, 960), (1, 100, 256)])
+@pytest.mark.parametrize("silu", [False, True])
+def test_group_norm(dtype, nimg, HW, C, silu):
+    from fdhip import ops
+    x = (torch.randn(nimg * HW, C, device=DEV) * 2 + 0.5).to(dtype)
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    out = ops.group_norm(x, g, b, nimg, HW, C, 32, 1e-5, silu)
+    xr = x.float().reshape(nimg, HW, C).permute(0, 2, 1)
+    ref = F.group_norm(xr, 32, g, b, 1e-5)
+    if silu:
+        ref = F.silu(ref)
+    ref = ref.permute(0, 2, 1).reshape(-1, C)
+    assert rel_l2(out, ref) < TOL[dtype]
+
+
+def test_group_norm_deterministic():
+    from fdhip import ops
+    x = rnd(2 * 4096, 640)
+    g, b = torch.ones(640, device=DEV), torch.zeros(640, device=DEV)
+    a1 = ops.group_norm(x, g, b, 2, 4096, 640)
+    a2 = ops.group_norm(x, g, b, 2, 4096, 640)
+    assert torch.equal(a1, a2)
+
+
+@pytest.mark.parametrize("C", [640, 1280])
+def test_layer_norm(C):
+    from fdhip import ops
+    x = rnd(4099, C)
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    out = ops.layer_norm(x, g, b, 1e-5)
+    ref = F.layer_norm(x.float(), (C,), g, b, 1e-5)
+    assert rel_l2(out, ref) < 6e-3
+
+
+# ------------------------------------------------------------------------------------------ attention
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,heads,Lq,Lk,kv_mod", [(2, 10, 4096, 4096, 0), (2, 20, 1024, 1024, 0), (4, 10, 4096, 77, 2),
+                                                  (1, 3, 200, 333, 0), (2, 20, 1024, 77, 2)])
+def test_flash_attn(dtype, B, heads, Lq, Lk, kv_mod):
+    from fdhip import ops
+    C = heads * 64
+    q = rnd(B, Lq, C, dtype=dtype)
+    nkv = kv_mod if kv_mod else B
+    kv = rnd(nkv, Lk, 2 * C, dtype=dtype)
+    k, v = kv[..., :C], kv[..., C:]
+    o = torch.empty(B, Lq, C, dtype=dtype, device=DEV)
+    ops.flash_attn(q, k, v, o, B, heads, Lq, Lk, C, 2 * C, 2 * C, C, Lq * C, Lk * 2 * C, Lk * 2 * C, Lq * C,
+                   kv_mod=kv_mod, scale=0.125)
+    idx = torch.arange(B, device=DEV) % nkv
+    qh = q.float().view(B, Lq, heads, 64).transpose(1, 2)
+    kh = k.float()[idx].reshape(B, Lk, heads, 64).transpose(1, 2)
+    vh = v.float()[idx].reshape(B, Lk, heads, 64).transpose(1, 2)
+    ref = F.scaled_dot_product_attention(qh, kh, vh).transpose(1, 2).reshape(B, Lq, C)
+    assert rel_l2(o, ref) < 1.5 * TOL[dtype], rel_l2(o, ref)
+
+
+@pytest.mark.parametrize("same", [True, False])
+def test_mha_seq_axis(same):
+    from fdhip import ops
+    G, Lx, N, E, H = 3, 2, 500, 640, 8
+    qkv = rnd(G * Lx, N, 3 * E)
+    if same:
+        qkv.view(G, Lx, N, 3 * E)[:, 1] = qkv.view(G, Lx, N, 3 * E)[:, 0]
+    o = torch.empty(G * Lx, N, E, dtype=torch.bfloat16, device=DEV)
+    ops.mha_seq_axis(qkv, o, Lx, G, N, E, H)
+    x = qkv.float().view(G, Lx, N, 3, H, E // H)
+    q, k, v = x[:, :, :, 0], x[:, :, :, 1], x[:, :, :, 2]  # G, L, N, H, d
+    s = torch.einsum("glnhd,gmnhd->gnhlm", q, k) / math.sqrt(E // H)
+    p = s.softmax(-1)
+    ref = torch.einsum("gnhlm,gmnhd->glnhd", p, v).reshape(G * Lx, N, E)
+    assert rel_l2(o, ref) < 6e-3
+    if same:
+        torch.testing.assert_close(o.float(), v[:, :1].expand(G, Lx, N, H, E // H).reshape(G * Lx, N, E),
+                                   rtol=1e-2, atol=2e-2)
+
+
+def test_softmax_rows():
+    from fdhip import ops
+    R, C = 333, 16384
+    s = torch.randn(R, C, device=DEV) * 3
+    p = torch.empty(R, C, dtype=torch.float16, device=DEV)
+    ops.softmax_rows(s, p, R, C, 0.5)
+    ref = (s * 0.5).softmax(-1)
+    assert rel_l2(p, ref) < 2e-3
+
+
+# ------------------------------------------------------------------------------------------ elementwise / loop
+def test_layouts_concat_time_features():
+    from fdhip import ops
+    from oracle.unet import timestep_embedding
+    x = torch.randn(2, 4, 37 * 29, device=DEV)
+    y = torch.empty(2, 37 * 29, 4, dtype=torch.bfloat16, device=DEV)
+    ops.nchw_to_nhwc(x, y, 2, 4, 37 * 29, 0.5)
+    assert torch.equal(y, (x * 0.5).transpose(1, 2).to(torch.bfloat16))
+    z = torch.empty(2, 4, 37 * 29, device=DEV)
+    ops.nhwc_to_nchw(y, z, 2, 4, 37 * 29, 2.0)
+    torch.testing.assert_close(z, (y.float() * 2).transpose(1, 2))
+    a, b = rnd(1000, 320), rnd(1000, 640)
+    c = torch.empty(1000, 960, dtype=torch.bfloat16, device=DEV)
+    ops.concat_channels(a, 320, b, 640, c, 1000)
+    assert torch.equal(c, torch.cat([a, b], 1))
+    t = torch.tensor([951.0, 951.0], device=DEV)
+    tid = torch.tensor([[1024, 1024, 0, 64, 1024, 1024]] * 2, dtype=torch.float32, device=DEV)
+    text = torch.randn(2, 1280, device=DEV)
+    tf = torch.empty(2, 320, device=DEV)
+    af = torch.empty(2, 2816, device=DEV)
+    ops.time_features(t, tid, text, tf, af, 2)
+    torch.testing.assert_close(tf.cpu(), timestep_embedding(t.cpu(), 320), rtol=1e-4, atol=2e-4)
+    ref_a = torch.cat([text.cpu(), timestep_embedding(tid.cpu().flatten(), 256).reshape(2, -1)], -1)
+    torch.testing.assert_close(af.cpu(), ref_a, rtol=1e-4, atol=2e-4)
+
+
+def test_tlc_blend_bitexact_vs_reference_golden(golden):
+    """fd_tlc_blend reproduces the reference's grids_inverse bit for bit (golden from the reference)."""
+    from fdhip import ops
+    from _det import det_tensor
+    from oracle import tlc
+    for h, w in [(64, 64), (128, 128), (128, 192), (200, 136)]:
+        idx, (k1, k2) = tlc.tile_origins(h, w, (128, 128), 0.5)
+        rows = sorted({i for i, _ in idx})
+        cols = sorted({j for _, j in idx})
+        assert idx == [(r, c) for r in rows for c in cols]
+        x = det_tensor((1, 4, h, w), 1000 + h * 7 + w)
+        tiles = torch.cat([x[:, :, i:i + k1, j:j + k2] for i, j in idx], 0)
+        outs = tiles * (1.0 + 0.01 * torch.arange(tiles.shape[0]).view(-1, 1, 1, 1)) + 0.05
+        wts = tlc.gaussian_weights(k2, k1)[0].contiguous()
+        canvas = torch.empty(4, h, w, device=DEV)
+        ops.tlc_blend(outs.to(DEV).contiguous(), wts.to(DEV), torch.tensor(rows, dtype=torch.int32, device=DEV),
+                      torch.tensor(cols, dtype=torch.int32, device=DEV), 4, h, w, k1, k2, canvas)
+        np.testing.assert_array_equal(canvas.cpu().numpy()[None], golden[f"tlc_{h}x{w}_inv"])
+
+
+def test_tlc_scale_input_and_euler_step():
+    from fdhip import ops
+    from oracle import schedulers as S
+    H, W, k = 200, 136, 128
+    canvas = torch.randn(4, H, W, device=DEV) * 5
+    rows = torch.tensor([0, 64, 72], dtype=torch.int32, device=DEV)
+    cols = torch.tensor([0, 8], dtype=torch.int32, device=DEV)
+    nt = 6
+    sig, sig_n, g = 11.02834, 10.1, 5.0
+    xin = torch.empty(nt * 2, k * k, 4, dtype=torch.bfloat16, device=DEV)
+    ops.tlc_scale_input(canvas, rows, cols, H, W, k, k, 0, nt, 2, sig, xin)
+    tiles = torch.stack([canvas[:, r:r + k, c:c + k] for r in rows.tolist() for c in cols.tolist()])
+    ref_in = S.euler_scale(tiles, sig).permute(0, 2, 3, 1).reshape(nt, k * k, 4)
+    torch.testing.assert_close(xin.view(nt, 2, k * k, 4)[:, 0].float(), ref_in.to(torch.bfloat16).float())
+    torch.testing.assert_close(xin.view(nt, 2, k * k, 4)[:, 1].float(), ref_in.to(torch.bfloat16).float())
+    eps = rnd(nt * 2, k * k, 4)
+    out = torch.empty(nt, 4, k, k, device=DEV)
+    ops.tlc_cfg_euler_step(eps, canvas, rows, cols, H, W, k, k, 0, nt, 2, g, 0.0, sig, sig_n, out)
+    e = eps.float().view(nt, 2, k, k, 4).permute(0, 1, 4, 2, 3)
+    ec = e[:, 0] + g * (e[:, 1] - e[:, 0])
+    ref = S.euler_step(ec, tiles, sig, sig_n)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+    # guidance_rescale > 0 path (rescale_noise_cfg)
+    from oracle.pipeline import rescale_noise_cfg
+    out2 = torch.empty_like(out)
+    ops.tlc_cfg_euler_step(eps, canvas, rows, cols, H, W, k, k, 0, nt, 2, g, 0.7, sig, sig_n, out2)
+    ref2 = torch.stack([S.euler_step(rescale_noise_cfg(ec[i:i + 1], e[i:i + 1, 1], 0.7)[0], tiles[i], sig, sig_n)
+                        for i in range(nt)])
+    torch.testing.assert_close(out2, ref2, rtol=1e-4, atol=1e-3)
+
+
+def test_tlc_grids_nhwc():
+    from fdhip import ops
+    H, W, C, k = 200, 136, 512, 128
+    canvas = rnd(H * W, C, dtype=torch.float16)
+    rows = torch.tensor([0, 64, 72], dtype=torch.int32, device=DEV)
+    cols = torch.tensor([0, 8], dtype=torch.int32, device=DEV)
+    out = torch.empty(2 * 2, k, k, C, dtype=torch.float16, device=DEV)
+    ops.tlc_grids_nhwc(canvas, rows, cols, H, W, C, k, k, 3, 2, 2, out)
+    cv = canvas.view(H, W, C)
+    for t, tid in enumerate([3, 4]):
+        r, c = rows[tid // 2].item(), cols[tid % 2].item()
+        assert torch.equal(out[2 * t], cv[r:r + k, c:c + k])
+        assert torch.equal(out[2 * t + 1], cv[r:r + k, c:c + k])
