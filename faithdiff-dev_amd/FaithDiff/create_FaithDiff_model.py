@@ -1,0 +1,42 @@
+"""Drop-in for FaithDiff/create_FaithDiff_model.py:11-37.
+
+``FaithDiff_pipeline(sdxl_path, VAE_FP16_path, FaithDiff_path, use_fp8=False)`` builds the same
+components the reference does (fp16 VAE, FaithDiff UNet with ``load_additional_layers``, optional fp8
+weight storage, DDPM scheduler for the 'lr' start point, Euler scheduler, the pipeline) on the HIP path.
+Paths that equal CKPT_PTH.RANDOM_INIT ('random-init') draw seeded random weights; otherwise local
+diffusers directories / a local ``FaithDiff.bin`` are loaded with safe loaders (no hub download, no
+pickle execution).  Extra keyword arguments (defaults keep the reference call working unchanged):
+``seed`` (random-init seed), ``unet_dtype`` (bf16 per the north star; fp16 also supported),
+``init_device`` ('cpu' for host-generated weights shared with the CPU oracle, 'cuda' for fast init).
+"""
+import torch
+
+from utils.system import quantize_8bit
+
+from .models.unet_2d_condition_vae_extension import RANDOM_INIT, AutoencoderKL, UNet2DConditionModel
+from .pipelines.pipeline_FaithDiff_tlc import FaithDiffStableDiffusionXLPipeline
+from .schedulers import DDPMScheduler
+
+
+def FaithDiff_pipeline(sdxl_path, VAE_FP16_path, FaithDiff_path, use_fp8=False, seed=0,
+                       unet_dtype=torch.bfloat16, init_device="cpu"):
+    dtype = torch.float16
+    vae = AutoencoderKL.from_pretrained(VAE_FP16_path, seed=seed, init_device=init_device).to(dtype=dtype)
+    unet = UNet2DConditionModel.from_pretrained(sdxl_path, subfolder="unet", variant="fp16", seed=seed,
+                                                init_device=init_device)
+    fd_path = FaithDiff_path
+    if fd_path != RANDOM_INIT and not str(fd_path).endswith((".bin", ".safetensors")):
+        fd_path = f"{fd_path}/FaithDiff.bin"
+    unet.load_additional_layers(weight_path=fd_path, dtype=dtype, init_device=init_device)
+    if use_fp8:
+        quantize_8bit(unet)
+    unet.to(dtype=unet_dtype)
+    pipe = FaithDiffStableDiffusionXLPipeline.from_pretrained(
+        sdxl_path, vae=vae, add_sample=True, denoise_encoder=unet.denoise_encoder, DDPM_scheduler=DDPMScheduler(),
+        add_watermarker=False, torch_dtype=dtype, variant="fp16", unet=unet)
+    pipe.unet = unet
+    return pipe
+
+
+def create_bsrnet(bsrnet_path):
+    raise NotImplementedError("BSRNet pre-pass is outside the denoising hot path (SURVEY 2.1: OUT)")

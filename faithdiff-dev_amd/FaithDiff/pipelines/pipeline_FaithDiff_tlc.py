@@ -1,0 +1,431 @@
+"""Drop-in for FaithDiff/pipelines/pipeline_FaithDiff_tlc.py on MI355X.
+
+``FaithDiffStableDiffusionXLPipeline.__call__`` keeps the reference signature (:1008-1042) and output
+(``.images``), and the same algorithm (:1187-1459): encode prompt (CFG always on, "" encoded, :1231-1243)
+-> preprocess (:1246) -> Euler timesteps (:1249) -> denoise encoder (:1250-1255) -> TLC grids of the
+image latents (:1257) -> noise * init sigma (:1261-1270) -> start_point 'lr': VAE posterior sample *
+0.13025, DDPM add_noise at t = 999 (:1271-1276) -> per step, per tile: CFG pair, scale_model_input,
+add_time_ids = [orig_h, orig_w, tile_i, tile_j, tgt_h, tgt_w] (latent-grid offsets), UNet, CFG (+
+rescale), Euler step, then the gaussian fp32 blend (:1324-1409) -> latents / 0.13025 -> fp16 VAE decode
+(:1411-1442) -> postprocess (:1451).
+
+What differs (MI355X-first, documented in DESIGN.md): the latent state stays fp32 between steps (the
+reference rounds it to fp16 at :1409); several tiles share one UNet forward (rows are independent
+except the extras' batch-axis MHA, which is grouped per tile); the per-element loop work is fused
+device kernels (fd_tlc_*); tiles can be sharded over ranks (tile_parallel.py); text encoders are a
+seeded synthetic stand-in unless embeddings are passed (CLIP weights are not available offline).
+"""
+import inspect
+import zlib
+from types import SimpleNamespace
+from typing import Any, Callable, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+import PIL.Image
+import torch
+import torch.distributed as dist
+
+from fdhip import ops
+
+from ..schedulers import DDPMScheduler, EulerDiscreteScheduler
+from .pipeline_output import FaithDiffStableDiffusionXLPipelineOutput
+from .tile_parallel import TileShard, run_tile_loop
+from .tlc import TileGrid
+
+
+class SyntheticTextEncoder:
+    """Seeded stand-in for CLIP-L + OpenCLIP-bigG: prompt -> (1, 77, 2048) hidden states
+    (``hidden_states[-2]`` concat) and (1, 1280) pooled embedding, deterministic in the prompt text.
+    The empty negative prompt is *encoded* like any other prompt, as in the reference (:622-675)."""
+
+    def __call__(self, prompt: str):
+        g = torch.Generator().manual_seed(zlib.crc32(prompt.encode("utf-8")) & 0x7FFFFFFF)
+        return torch.randn(1, 77, 2048, generator=g), torch.randn(1, 1280, generator=g)
+
+
+def randn_tensor(shape, generator=None, device=None, dtype=torch.float32):
+    """diffusers.utils.torch_utils.randn_tensor semantics: draw on the generator's device."""
+    if isinstance(generator, list):
+        generator = generator[0]
+    gdev = generator.device if generator is not None else torch.device(device)
+    return torch.randn(shape, generator=generator, device=gdev, dtype=dtype).to(device)
+
+
+def retrieve_timesteps(scheduler, num_inference_steps=None, device=None, timesteps=None, **kwargs):
+    """:331-372."""
+    if timesteps is not None:
+        if "timesteps" not in set(inspect.signature(scheduler.set_timesteps).parameters.keys()):
+            raise ValueError(f"The current scheduler class {scheduler.__class__}'s `set_timesteps` does not support "
+                             "custom timestep schedules.")
+        scheduler.set_timesteps(timesteps=timesteps, device=device, **kwargs)
+        return scheduler.timesteps, len(scheduler.timesteps)
+    scheduler.set_timesteps(num_inference_steps, device=device, **kwargs)
+    return scheduler.timesteps, num_inference_steps
+
+
+class FaithDiffStableDiffusionXLPipeline:
+    model_cpu_offload_seq = "text_encoder->text_encoder_2->denoise_encoder->unet->vae"
+    _optional_components = ["tokenizer", "tokenizer_2", "text_encoder", "text_encoder_2", "feature_extractor"]
+    _callback_tensor_inputs = ["latents", "prompt_embeds", "negative_prompt_embeds", "add_text_embeds",
+                               "add_time_ids", "negative_pooled_prompt_embeds", "negative_add_time_ids"]
+
+    def __init__(self, vae, denoise_encoder, text_encoder=None, text_encoder_2=None, tokenizer=None,
+                 tokenizer_2=None, unet=None, scheduler=None, DDPM_scheduler=None, force_zeros_for_empty_prompt=True,
+                 add_watermarker=None):
+        self.vae = vae
+        self.denoise_encoder = denoise_encoder
+        self.text_encoder = text_encoder or SyntheticTextEncoder()
+        self.text_encoder_2 = text_encoder_2
+        self.tokenizer, self.tokenizer_2 = tokenizer, tokenizer_2
+        self.unet = unet
+        self.scheduler = scheduler or EulerDiscreteScheduler()
+        self.DDPM_scheduler = DDPM_scheduler or DDPMScheduler()
+        self.config = SimpleNamespace(force_zeros_for_empty_prompt=force_zeros_for_empty_prompt)
+        self.vae_scale_factor = 2 ** (len(self.vae.config.block_out_channels) - 1)
+        self.default_sample_size = 128
+        self.watermark = None
+        self.device = torch.device("cpu")
+        self.tile_batch = 4          # TLC tiles per UNet forward (B = 2 * tile_batch rows)
+        self.process_group = None    # torch.distributed group for tile parallelism (None: single GPU)
+        self.last_timings = {}
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_pretrained(cls, sdxl_path, vae=None, denoise_encoder=None, DDPM_scheduler=None, add_sample=True,
+                        add_watermarker=False, torch_dtype=None, variant=None, unet=None, **kwargs):
+        return cls(vae=vae, denoise_encoder=denoise_encoder, unet=unet, scheduler=EulerDiscreteScheduler(),
+                   DDPM_scheduler=DDPM_scheduler or DDPMScheduler(), add_watermarker=add_watermarker)
+
+    def to(self, device=None, dtype=None):
+        dev = torch.device(device) if device is not None else self.device
+        if dev.type == "cuda" and dev.index is not None:
+            torch.cuda.set_device(dev)
+        self.device = dev
+        for m in (self.vae, self.denoise_encoder, self.unet):
+            if m is not None:
+                m.to(device=dev)
+        return self
+
+    @property
+    def _execution_device(self):
+        return self.device
+
+    def enable_model_cpu_offload(self, *a, **k):
+        """No-op: 288 GB of HBM3E hold the UNet, VAE and encoders (reference README:59-60 needs offload on
+        <12 GB parts)."""
+
+    def set_encoder_tile_settings(self, denoise_encoder_tile_sample_min_size=1024,
+                                  denoise_encoder_sample_overlap_factor=0.25, vae_sample_size=1024,
+                                  vae_tile_overlap_factor=0.25):
+        """:888-896 (note: does not recompute denoise_encoder.tile_latent_min_size, as in the reference)."""
+        self.denoise_encoder.tile_sample_min_size = denoise_encoder_tile_sample_min_size
+        self.denoise_encoder.tile_overlap_factor = denoise_encoder_sample_overlap_factor
+        self.vae.config.sample_size = vae_sample_size
+        self.vae.tile_overlap_factor = vae_tile_overlap_factor
+
+    def enable_vae_tiling(self):
+        self.vae.enable_tiling()
+        self.denoise_encoder.enable_tiling()
+
+    def disable_vae_tiling(self):
+        self.vae.disable_tiling()
+        self.denoise_encoder.disable_tiling()
+
+    def enable_tile_parallel(self, group=None):
+        """Shard TLC tiles over the ranks of `group` (default WORLD) with one all-gather per step."""
+        self.process_group = group if group is not None else dist.group.WORLD
+
+    # ------------------------------------------------------------------ properties (:915-948)
+    @property
+    def guidance_scale(self):
+        return self._guidance_scale
+
+    @property
+    def guidance_rescale(self):
+        return self._guidance_rescale
+
+    @property
+    def clip_skip(self):
+        return self._clip_skip
+
+    @property
+    def do_classifier_free_guidance(self):
+        return self._guidance_scale > 1 and self.unet.config.time_cond_proj_dim is None
+
+    @property
+    def cross_attention_kwargs(self):
+        return self._cross_attention_kwargs
+
+    @property
+    def denoising_end(self):
+        return self._denoising_end
+
+    @property
+    def num_timesteps(self):
+        return self._num_timesteps
+
+    @property
+    def interrupt(self):
+        return self._interrupt
+
+    # ------------------------------------------------------------------ inputs
+    def encode_prompt(self, prompt, prompt_2=None, device=None, num_images_per_prompt=1,
+                      do_classifier_free_guidance=True, negative_prompt=None, negative_prompt_2=None,
+                      prompt_embeds=None, negative_prompt_embeds=None, pooled_prompt_embeds=None,
+                      negative_pooled_prompt_embeds=None, lora_scale=None, clip_skip=None):
+        """:485-717 contract; text features from the synthetic encoder unless embeddings are passed."""
+        if prompt_embeds is None:
+            if isinstance(prompt, list):
+                prompt = prompt[0]
+            prompt_embeds, pooled_prompt_embeds = self.text_encoder(prompt)
+        zero_out = negative_prompt is None and self.config.force_zeros_for_empty_prompt
+        if do_classifier_free_guidance and negative_prompt_embeds is None and zero_out:
+            negative_prompt_embeds = torch.zeros_like(prompt_embeds)
+            negative_pooled_prompt_embeds = torch.zeros_like(pooled_prompt_embeds)
+        elif do_classifier_free_guidance and negative_prompt_embeds is None:
+            neg = negative_prompt or ""
+            if isinstance(neg, list):
+                neg = neg[0]
+            negative_prompt_embeds, negative_pooled_prompt_embeds = self.text_encoder(neg)
+        return prompt_embeds, negative_prompt_embeds, pooled_prompt_embeds, negative_pooled_prompt_embeds
+
+    def check_inputs(self, lr_img, prompt, prompt_2, height, width, callback_steps, negative_prompt=None,
+                     negative_prompt_2=None, prompt_embeds=None, negative_prompt_embeds=None,
+                     pooled_prompt_embeds=None, negative_pooled_prompt_embeds=None,
+                     callback_on_step_end_tensor_inputs=None):
+        """:738-817 (same ValueErrors)."""
+        if lr_img is None:
+            raise ValueError("`lr_image` must be provided!")
+        if height % 8 != 0 or width % 8 != 0:
+            raise ValueError(f"`height` and `width` have to be divisible by 8 but are {height} and {width}.")
+        if callback_steps is not None and (not isinstance(callback_steps, int) or callback_steps <= 0):
+            raise ValueError(f"`callback_steps` has to be a positive integer but is {callback_steps} of type "
+                             f"{type(callback_steps)}.")
+        if callback_on_step_end_tensor_inputs is not None and not all(
+                k in self._callback_tensor_inputs for k in callback_on_step_end_tensor_inputs):
+            raise ValueError(f"`callback_on_step_end_tensor_inputs` has to be in {self._callback_tensor_inputs}")
+        if prompt is not None and prompt_embeds is not None:
+            raise ValueError("Cannot forward both `prompt` and `prompt_embeds`. Please make sure to only forward one "
+                             "of the two.")
+        elif prompt_2 is not None and prompt_embeds is not None:
+            raise ValueError("Cannot forward both `prompt_2` and `prompt_embeds`.")
+        elif prompt is None and prompt_embeds is None:
+            raise ValueError("Provide either `prompt` or `prompt_embeds`. Cannot leave both `prompt` and "
+                             "`prompt_embeds` undefined.")
+        elif prompt is not None and not isinstance(prompt, (str, list)):
+            raise ValueError(f"`prompt` has to be of type `str` or `list` but is {type(prompt)}")
+        elif prompt_2 is not None and not isinstance(prompt_2, (str, list)):
+            raise ValueError(f"`prompt_2` has to be of type `str` or `list` but is {type(prompt_2)}")
+        if negative_prompt is not None and negative_prompt_embeds is not None:
+            raise ValueError("Cannot forward both `negative_prompt` and `negative_prompt_embeds`.")
+        elif negative_prompt_2 is not None and negative_prompt_embeds is not None:
+            raise ValueError("Cannot forward both `negative_prompt_2` and `negative_prompt_embeds`.")
+        if prompt_embeds is not None and negative_prompt_embeds is not None:
+            if prompt_embeds.shape != negative_prompt_embeds.shape:
+                raise ValueError("`prompt_embeds` and `negative_prompt_embeds` must have the same shape when passed "
+                                 f"directly, but got: {prompt_embeds.shape} != {negative_prompt_embeds.shape}.")
+        if prompt_embeds is not None and pooled_prompt_embeds is None:
+            raise ValueError("If `prompt_embeds` are provided, `pooled_prompt_embeds` also have to be passed.")
+        if negative_prompt_embeds is not None and negative_pooled_prompt_embeds is None:
+            raise ValueError("If `negative_prompt_embeds` are provided, `negative_pooled_prompt_embeds` also have to "
+                             "be passed.")
+
+    def _preprocess(self, img, height, width):
+        """VaeImageProcessor.preprocess (:1246): PIL (resized to (width, height) if needed, LANCZOS) ->
+        [-1, 1], laid out NHWC [H*W, 3] fp16 on the device (the host does only the uint8 -> float map)."""
+        if isinstance(img, list):
+            img = img[0]
+        if isinstance(img, torch.Tensor):
+            t = img.float()
+            if t.ndim == 4:
+                t = t[0]
+            if t.shape[0] == 3:
+                t = t.permute(1, 2, 0)
+            arr = t.cpu().numpy()
+        else:
+            if not isinstance(img, PIL.Image.Image):
+                raise ValueError(f"`image` has to be of type `torch.Tensor`, `PIL.Image.Image` or list but is "
+                                 f"{type(img)}")
+            if img.size != (width, height):
+                img = img.resize((width, height), resample=PIL.Image.LANCZOS)
+            arr = np.asarray(img.convert("RGB"), dtype=np.float32) / 255.0 * 2.0 - 1.0
+        x = torch.from_numpy(np.ascontiguousarray(arr)).reshape(-1, 3)
+        return x.to(self.device, torch.float16)
+
+    def prepare_latents(self, batch_size, num_channels_latents, height, width, dtype, device, generator,
+                        latents=None):
+        """:820-835 -- returns the *unscaled* noise; the init sigma is applied on device in the fused kernel."""
+        shape = (batch_size, num_channels_latents, height // self.vae_scale_factor, width // self.vae_scale_factor)
+        if isinstance(generator, list) and len(generator) != batch_size:
+            raise ValueError(f"You have passed a list of generators of length {len(generator)}, but requested an "
+                             f"effective batch size of {batch_size}.")
+        if latents is None:
+            return randn_tensor(shape, generator=generator, device=device, dtype=torch.float32)
+        return latents.to(device=device, dtype=torch.float32)
+
+    # ------------------------------------------------------------------ the call
+    @torch.no_grad()
+    def __call__(self, lr_img=None, prompt: Union[str, List[str]] = None, prompt_2=None, height: Optional[int] = None,
+                 width: Optional[int] = None, num_inference_steps: int = 50, start_point: Optional[str] = "noise",
+                 timesteps: List[int] = None, denoising_end: Optional[float] = None, overlap: float = 0.5,
+                 guidance_scale: float = 5.0, negative_prompt=None, negative_prompt_2=None,
+                 num_images_per_prompt: Optional[int] = 1, eta: float = 0.0, generator=None,
+                 latents: Optional[torch.Tensor] = None, prompt_embeds=None, negative_prompt_embeds=None,
+                 pooled_prompt_embeds=None, negative_pooled_prompt_embeds=None, output_type: Optional[str] = "pil",
+                 return_dict: bool = True, cross_attention_kwargs: Optional[Dict[str, Any]] = None,
+                 guidance_rescale: float = 0.0, original_size: Optional[Tuple[int, int]] = None,
+                 target_size: Optional[Tuple[int, int]] = None, clip_skip: Optional[int] = None,
+                 callback_on_step_end: Optional[Callable[[int, int, Dict], None]] = None,
+                 callback_on_step_end_tensor_inputs: List[str] = ["latents"], add_sample: bool = True, **kwargs):
+        callback = kwargs.pop("callback", None)
+        callback_steps = kwargs.pop("callback_steps", None)
+        posterior_noise = kwargs.pop("posterior_noise", None)  # explicit VAE posterior draw (parity tests)
+        timer = kwargs.pop("timer", None)
+
+        height = height or self.default_sample_size * self.vae_scale_factor
+        width = width or self.default_sample_size * self.vae_scale_factor
+        original_size = original_size or (height, width)
+        target_size = target_size or (height, width)
+        self.check_inputs(lr_img, prompt, prompt_2, height, width, callback_steps, negative_prompt, negative_prompt_2,
+                          prompt_embeds, negative_prompt_embeds, pooled_prompt_embeds, negative_pooled_prompt_embeds,
+                          callback_on_step_end_tensor_inputs)
+        self._guidance_scale = guidance_scale
+        self._guidance_rescale = guidance_rescale
+        self._clip_skip = clip_skip
+        self._cross_attention_kwargs = cross_attention_kwargs
+        self._denoising_end = denoising_end
+        self._interrupt = False
+        dev = self.device
+        if dev.type != "cuda":
+            raise RuntimeError("FaithDiff on MI355X: call pipe.to('cuda') (there is no CPU execution path)")
+        unet = self.unet.hip()
+
+        # 3. prompts (CFG always requested from encode_prompt, :1240)
+        pe, npe, ppe, nppe = self.encode_prompt(prompt, do_classifier_free_guidance=True,
+                                                negative_prompt=negative_prompt, prompt_embeds=prompt_embeds,
+                                                negative_prompt_embeds=negative_prompt_embeds,
+                                                pooled_prompt_embeds=pooled_prompt_embeds,
+                                                negative_pooled_prompt_embeds=negative_pooled_prompt_embeds)
+        cfg = 2 if self.do_classifier_free_guidance else 1
+        if cfg == 2:
+            ctx = torch.cat([npe.float(), pe.float()], 0)
+            text = torch.cat([nppe.float(), ppe.float()], 0)
+        else:
+            ctx, text = pe.float(), ppe.float()
+
+        # 4. image + timesteps
+        x_img = self._preprocess(lr_img, height, width)
+        ts, num_inference_steps = retrieve_timesteps(self.scheduler, num_inference_steps, dev, timesteps)
+        if denoising_end is not None and isinstance(denoising_end, float) and 0 < denoising_end < 1:
+            cutoff = int(round(self.scheduler.config.num_train_timesteps
+                               - denoising_end * self.scheduler.config.num_train_timesteps))
+            num_inference_steps = len([t for t in ts if t >= cutoff])
+        sig = self.scheduler.sigmas
+        self._num_timesteps = num_inference_steps
+        h, w = height // 8, width // 8
+
+        # 5. denoise-encoder image latents (:1250-1255) -> TLC tiles (:1257)
+        grid = TileGrid(h, w, (target_size[0] // 8, target_size[1] // 8), overlap)
+        kh, kw, N = grid.kh, grid.kw, grid.ntiles
+        shard = TileShard(N, self.process_group)
+        img_lat = self.denoise_encoder.encode_nhwc(x_img, height, width)  # [h*w, 512] fp16
+        rows_t = torch.tensor(grid.rows, dtype=torch.int32, device=dev)
+        cols_t = torch.tensor(grid.cols, dtype=torch.int32, device=dev)
+        cond_dt = unet.dtype
+        img_lat_c = torch.empty_like(img_lat, dtype=cond_dt)
+        ops.unary(img_lat, img_lat_c)
+        cond_tiles = None
+        if shard.count:
+            cond_tiles = torch.empty((shard.count * cfg, kh * kw, 512), dtype=cond_dt, device=dev)
+            ops.tlc_grids_nhwc(img_lat_c, rows_t, cols_t, h, w, 512, kh, kw, shard.begin, shard.count, cfg,
+                               cond_tiles)
+        del img_lat_c
+
+        # 6. initial latent canvas (:1261-1278): noise * init_sigma [+ DDPM(add_noise) of the VAE sample]
+        noise = self.prepare_latents(1, 4, height, width, torch.float32, dev, generator, latents)
+        canvas = torch.empty((4, h, w), dtype=torch.float32, device=dev)
+        init_sigma = float(self.scheduler.init_noise_sigma)
+        if start_point == "lr":
+            moments = self.vae.encode_moments_nhwc(x_img, height, width)
+            eps_post = (posterior_noise.to(dev, torch.float32) if posterior_noise is not None
+                        else torch.randn((1, 4, h, w), device=dev, dtype=torch.float32))
+            a, b = self.DDPM_scheduler.add_noise_coefficients(999)
+            ops.vae_sample_add_noise(moments, eps_post.contiguous(), noise.contiguous(), canvas, h * w,
+                                     self.vae.config.scaling_factor, init_sigma, a, b, True)
+        else:
+            ops.vae_sample_add_noise(None, None, noise.contiguous(), canvas, h * w, 1.0, init_sigma, 0.0, 1.0, False)
+        if shard.world > 1:
+            dist.broadcast(canvas, src=dist.get_global_rank(self.process_group, 0), group=self.process_group)
+
+        # 7. per-row conditioning, computed once per image
+        unet.set_context(ctx.to(dev))
+        tb = max(1, min(self.tile_batch, shard.count or 1))
+        B = tb * cfg
+        text_rows = text.to(dev).repeat(tb, 1).contiguous()  # [B, 1280]
+        tids_all = torch.tensor([[original_size[0], original_size[1], i, j, target_size[0], target_size[1]]
+                                 for (i, j) in [grid.origin(t) for t in range(N)]], dtype=torch.float32)
+        tids_all = tids_all.repeat_interleave(cfg, 0).to(dev)  # [N*cfg, 6]
+        t_rows = torch.tensor(np.repeat(ts[:num_inference_steps], B), dtype=torch.float32, device=dev).view(-1, B)
+        weights = torch.tensor(grid.weights(), dtype=torch.float64, device=dev)
+        xin = torch.empty((B * kh * kw, 4), dtype=cond_dt, device=dev)
+        canvas_next = torch.empty_like(canvas)
+        state = {"canvas": canvas, "next": canvas_next}
+
+        def compute(i, begin, count, out):
+            s, s_next = float(sig[i]), float(sig[i + 1])
+            for c0 in range(0, count, tb):
+                n = min(tb, count - c0)
+                rows = n * cfg
+                ops.tlc_scale_input(state["canvas"], rows_t, cols_t, h, w, kh, kw, begin + c0, n, cfg, s, xin)
+                cond = cond_tiles[c0 * cfg:(c0 + n) * cfg].reshape(rows * kh * kw, 512)
+                tid = tids_all[(begin + c0) * cfg:(begin + c0 + n) * cfg]
+                eps = unet.forward(xin[:rows * kh * kw], t_rows[i, :rows], tid, text_rows[:rows], cond, rows, kh, kw,
+                                   add_sample=add_sample)
+                ops.tlc_cfg_euler_step(eps, state["canvas"], rows_t, cols_t, h, w, kh, kw, begin + c0, n, cfg,
+                                       guidance_scale, guidance_rescale, s, s_next, out[c0:c0 + n])
+
+        def blend(tiles):
+            ops.tlc_blend(tiles.contiguous(), weights, rows_t, cols_t, 4, h, w, kh, kw, state["next"])
+            state["canvas"], state["next"] = state["next"], state["canvas"]
+            return state["canvas"]
+
+        def on_step(i, cv):
+            if timer is not None:
+                timer("step", i)
+            if callback_on_step_end is not None:
+                cb = {k: (cv.view(1, 4, h, w) if k == "latents" else None) for k in callback_on_step_end_tensor_inputs}
+                out = callback_on_step_end(self, i, ts[i], cb)
+                if out is not None and out.get("latents") is not None:
+                    state["canvas"].copy_(out["latents"].reshape(4, h, w))
+            if callback is not None and callback_steps and i % callback_steps == 0:
+                callback(i, ts[i], cv.view(1, 4, h, w))
+
+        final = run_tile_loop(num_inference_steps, shard, (4, kh, kw), compute, blend, dev, on_step=on_step)
+        if final is None:
+            final = canvas
+        lat = final.view(1, 4, h, w)
+        if output_type == "latent":
+            image = lat.clone()
+        else:
+            z = torch.empty((h * w, 4), dtype=self.vae.dtype, device=dev)
+            ops.nchw_to_nhwc(final, z, 1, 4, h * w, 1.0 / self.vae.config.scaling_factor)
+            y = self.vae.decode_nhwc(z, h, w)  # NHWC [H*W, 3] fp16
+            if timer is not None:
+                timer("decode", 0)
+            image = self._postprocess(y, height, width, output_type)
+        if not return_dict:
+            return (image,)
+        return FaithDiffStableDiffusionXLPipelineOutput(images=image)
+
+    def _postprocess(self, y, H, W, output_type):
+        """VaeImageProcessor.postprocess (:1451)."""
+        if output_type == "pt":
+            out = torch.empty((1, 3, H, W), dtype=y.dtype, device=y.device)
+            ops.nhwc_to_nchw(y, out, 1, 3, H * W)
+            return (out.float() / 2 + 0.5).clamp(0, 1)
+        u8 = torch.empty((H * W, 3), dtype=torch.uint8, device=y.device)
+        ops.postprocess_u8(y, u8)
+        arr = u8.view(H, W, 3).cpu().numpy()
+        if output_type == "np":
+            return arr[None].astype(np.float32) / 255.0
+        return [PIL.Image.fromarray(arr)]

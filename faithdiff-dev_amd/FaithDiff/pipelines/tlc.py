@@ -1,0 +1,51 @@
+"""Host side of the TLC latent-tile loop: tile origins and gaussian blend weights.
+
+Semantics of LocalAttention (FaithDiff/pipelines/pipeline_FaithDiff_tlc.py:101-252): kernel clamped to
+the latent (h, w); step ceil(k * overlap) (k when a single row/column); the last tile snapped to the
+edge; tiles in row-major order over a Cartesian grid of row and column origins.  Weights
+(:207-228): fp64, x midpoint (W-1)/2 but y midpoint H/2 (asymmetric), var 0.01.  The per-element
+split / blend run on the device (fd_tlc_* kernels); only these O(#tiles) index lists are host work.
+"""
+import math
+
+import numpy as np
+
+
+def axis_origins(n, k, overlap):
+    """Origins along one axis (the inner loop of LocalAttention.grids)."""
+    k = min(k, n)
+    num = (n - 1) // k + 1
+    step = k if num == 1 else math.ceil(k * overlap)
+    out, pos, last = [], 0, False
+    while pos < n and not last:
+        if pos + k >= n:
+            pos = n - k
+            last = True
+        out.append(pos)
+        pos += step
+    return out, k
+
+
+class TileGrid:
+    def __init__(self, h, w, kernel_size, overlap=0.5):
+        self.h, self.w = h, w
+        self.rows, self.kh = axis_origins(h, kernel_size[0], overlap)
+        self.cols, self.kw = axis_origins(w, kernel_size[1], overlap)
+        self.idxes = [{"i": i, "j": j} for i in self.rows for j in self.cols]
+
+    @property
+    def ntiles(self):
+        return len(self.rows) * len(self.cols)
+
+    def origin(self, t):
+        return self.rows[t // len(self.cols)], self.cols[t % len(self.cols)]
+
+    def weights(self):
+        """(kh, kw) float64, identical for each of the 4 latent channels."""
+        var = 0.01
+        W, H = self.kw, self.kh
+        mid = (W - 1) / 2
+        xp = [np.exp(-(x - mid) * (x - mid) / (W * W) / (2 * var)) / np.sqrt(2 * np.pi * var) for x in range(W)]
+        mid = H / 2
+        yp = [np.exp(-(y - mid) * (y - mid) / (H * H) / (2 * var)) / np.sqrt(2 * np.pi * var) for y in range(H)]
+        return np.outer(yp, xp)

@@ -270,11 +270,11 @@ extern "C" int fd_mha_seq_axis(const void* qkv, void* o, int L, int groups, int 
 // fp32 row softmax: p[r][c] = exp(scale*s - max) / sum  (one 256-thread block per row)
 template <typename TO>
 __global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ s, TO* __restrict__ p, int C,
-                                                           float scale) {
+                                                           long long ldp, float scale) {
   __shared__ float red[8];
   const long long r = blockIdx.x;
   const float* row = s + r * C;
-  TO* out = p + r * C;
+  TO* out = p + r * ldp;
   float mx = -INFINITY;
   for (int c = threadIdx.x; c < C; c += 256) mx = fmaxf(mx, row[c] * scale);
   mx = wave_max(mx);
@@ -291,11 +291,12 @@ __global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restri
   for (int c = threadIdx.x; c < C; c += 256) out[c] = (TO)(__expf(row[c] * scale - mx) * inv);
 }
 
-extern "C" int fd_softmax_rows(const float* s, void* p, int R, int C, float scale, int dtype, void* stream) {
+extern "C" int fd_softmax_rows(const float* s, void* p, int R, int C, long long ldp, float scale, int dtype,
+                               void* stream) {
   if (!s || !p) return FD_ERR_ARG;
-  if (R <= 0 || C <= 0) return FD_ERR_SHAPE;
+  if (R <= 0 || C <= 0 || ldp < C) return FD_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  FD_DISPATCH_O(dtype, hipLaunchKernelGGL(softmax_rows_kernel<TO>, dim3(R), dim3(256), 0, st, s, (TO*)p, C, scale));
+  FD_DISPATCH_O(dtype, hipLaunchKernelGGL(softmax_rows_kernel<TO>, dim3(R), dim3(256), 0, st, s, (TO*)p, C, ldp, scale));
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

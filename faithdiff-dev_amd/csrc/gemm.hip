@@ -71,7 +71,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p) {
     const int n = n0 + row;
     b_row[i] = Bw + (long long)(n < N ? n : N - 1) * p.ldb + (slot ^ ((row >> 1) & 7)) * 8;
   }
-  const int Hl = p.upsample ? 2 * p.Hin : p.Hin, Wl = p.upsample ? 2 * p.Win : p.Win;
+  // upsample: the conv runs on a nearest-resized (Hout x Wout) image; exact x2 or diffusers' upsample_size
+  const int Hl = p.upsample ? p.Hout : p.Hin, Wl = p.upsample ? p.Wout : p.Win;
   const int C1 = p.C1 > 0 ? p.C1 : p.Cin;
   const T* __restrict__ A2 = (const T*)p.A2;
 
@@ -87,7 +88,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p) {
       for (int i = 0; i < A_INSTR; ++i) {
         const int iy = a_iy0[i] + ky, ix = a_ix0[i] + kx;
         const bool ok = a_ok[i] && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
-        const int py = p.upsample ? (iy >> 1) : iy, px = p.upsample ? (ix >> 1) : ix;
+        const int py = p.upsample ? (iy * p.Hin) / Hl : iy, px = p.upsample ? (ix * p.Win) / Wl : ix;
         const long long pix = a_pix[i] + (long long)py * p.Win + px;
         const T* src = second ? (A2 + pix * (p.Cin - C1) + (c0 - C1) + a_chunk[i] * 8)
                               : (A + pix * p.lda + c0 + a_chunk[i] * 8);
@@ -227,6 +228,7 @@ extern "C" int fd_gemm(const fd_gemm_params* p, void* stream) {
     if (p->Cin % 64 || (p->C1 > 0 && (p->C1 % 64 || !p->A2)) || p->K != 9 * p->Cin) return FD_ERR_SHAPE;
     if (p->M != p->nimg * p->Hout * p->Wout) return FD_ERR_SHAPE;
     if (p->stride != 1 && p->stride != 2) return FD_ERR_SHAPE;
+    if (p->upsample && (p->stride != 1 || p->pad != 1 || p->Hout < p->Hin || p->Wout < p->Win)) return FD_ERR_SHAPE;
   }
   hipStream_t s = (hipStream_t)stream;
   FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, return dispatch_tiles<T, TO>(p, s)));

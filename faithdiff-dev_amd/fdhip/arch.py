@@ -171,11 +171,6 @@ def vae_param_shapes():
     return d
 
 
-def _is_norm(name):
-    leaf = name.rsplit(".", 2)
-    return any(t in name for t in ("norm", "ln_")) and not name.endswith("weight") is False
-
-
 def random_init(shapes, seed=0, device="cpu", dtype=torch.float32, gain=1.0):
     """Seeded per-key init: weights U(-1,1)*gain/sqrt(fan_in); biases U(-1,1)*0.05;
     norm weights 1 + 0.1*U(-1,1); norm biases 0.05*U(-1,1)."""
@@ -207,3 +202,89 @@ def count(shapes):
             k *= x
         n += k
     return n
+
+
+def unet_flops(h, w, B=2, with_extras=True, Lk=77):
+    """Algorithmic FLOPs (2 per MAC) of one UNet forward on B rows of an h x w latent: every conv / Linear
+    GEMM plus attention QK^T and PV (4*Lq*Lk*d per head); norms/elementwise are bytes, not FLOPs
+    (SURVEY 8(d)).  C2 (B=2, 128x128) = 14.217 TFLOP."""
+    C, Lr, Hd = UNET_CH, UNET_LAYERS, UNET_HEADS
+    f = 0.0
+
+    def conv(M, ci, co, k=3):
+        return 2.0 * M * co * k * k * ci
+
+    def lin(M, k, n):
+        return 2.0 * M * k * n
+
+    def resnet(M, ci, co):
+        x = conv(M, ci, co) + conv(M, co, co)
+        if ci != co:
+            x += lin(M, ci, co)
+        return x
+
+    def t2d(M, T, c, layers):
+        x = 2 * lin(M, c, c)
+        for _ in range(layers):
+            x += lin(M, c, 3 * c) + lin(M, c, c) + 4.0 * B * T * T * c        # attn1
+            x += lin(M, c, c) + lin(B * Lk, 2048, 2 * c) + lin(M, c, c) + 4.0 * B * T * Lk * c  # attn2
+            x += lin(M, c, 8 * c) + lin(M, 4 * c, c)                          # GEGLU FF
+        return x
+
+    sizes = [(h, w)]
+    for _ in range(2):
+        sizes.append(((sizes[-1][0] + 1) // 2, (sizes[-1][1] + 1) // 2))
+    M = [B * a * b for a, b in sizes]
+    T = [a * b for a, b in sizes]
+    f += conv(M[0], 4, C[0])
+    if with_extras:
+        f += conv(M[0], 512, 512) + conv(M[0], 512, 320)
+        f += 2 * (lin(M[0], 640, 1920) + lin(M[0], 640, 640) + 4.0 * M[0] * B * 640 + lin(M[0], 640, 1280)
+                  + lin(M[0], 1280, 640))
+        f += lin(M[0], 640, 320)
+    prev = C[0]
+    for i in range(3):
+        for j in range(2):
+            f += resnet(M[i], prev if j == 0 else C[i], C[i])
+            if Lr[i]:
+                f += t2d(M[i], T[i], C[i], Lr[i])
+        if i < 2:
+            f += conv(M[i + 1], C[i], C[i])
+        prev = C[i]
+    f += 2 * resnet(M[2], C[2], C[2]) + t2d(M[2], T[2], C[2], Lr[2])
+    skips = up_skip_channels()
+    prev = C[2]
+    for i in range(3):
+        lvl = 2 - i
+        for j in range(3):
+            f += resnet(M[lvl], (prev if j == 0 else C[lvl]) + skips[i][j], C[lvl])
+            if Lr[lvl]:
+                f += t2d(M[lvl], T[lvl], C[lvl], Lr[lvl])
+        if i < 2:
+            f += conv(M[lvl - 1], C[lvl], C[lvl])
+        prev = C[lvl]
+    f += conv(M[0], C[0], 4)
+    return f
+
+
+def vae_decode_flops(h, w):
+    """AutoencoderKL.decode on an h x w latent (10.47 TFLOP at 128x128)."""
+    rch = tuple(reversed(VAE_CH))
+    f = 2.0 * h * w * 4 * 4 + 2.0 * h * w * rch[0] * 9 * 4
+
+    def resnet(M, ci, co):
+        x = 2.0 * M * co * 9 * ci + 2.0 * M * co * 9 * co
+        return x + (2.0 * M * ci * co if ci != co else 0.0)
+
+    T = h * w
+    f += 2 * resnet(T, 512, 512) + 4 * 2.0 * T * 512 * 512 + 4.0 * T * T * 512
+    hh, ww, prev = h, w, rch[0]
+    for i, c in enumerate(rch):
+        for j in range(3):
+            f += resnet(hh * ww, prev if j == 0 else c, c)
+        if i < 3:
+            hh, ww = hh * 2, ww * 2
+            f += 2.0 * hh * ww * c * 9 * c
+        prev = c
+    f += 2.0 * hh * ww * 3 * 9 * rch[-1]
+    return f

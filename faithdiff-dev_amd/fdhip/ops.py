@@ -81,11 +81,12 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
 
 
 def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C1=None, out=None, rowbias=None,
-            residual=None, act="none", out_dtype=None):
-    """Implicit-GEMM 3x3 conv on NHWC x [nimg*H*W, Cin] (or concat(x, x2) along C) with packed weight wp."""
+            residual=None, act="none", out_dtype=None, upsample_size=None):
+    """Implicit-GEMM 3x3 conv on NHWC x [nimg*H*W, Cin] (or concat(x, x2) along C) with packed weight wp.
+    upsample=True: nearest-resize to upsample_size (default 2H x 2W) folded into the gather."""
     Cout, K = wp.shape
     Cin = K // 9
-    Hl, Wl = (2 * H, 2 * W) if upsample else (H, W)
+    Hl, Wl = ((2 * H, 2 * W) if upsample_size is None else tuple(upsample_size)) if upsample else (H, W)
     Hout = (Hl + 2 * pad - 3) // stride + 1
     Wout = (Wl + 2 * pad - 3) // stride + 1
     if stride == 2 and pad == 0:  # VAE Downsample2D: F.pad (0,1,0,1) then conv(k3, s2, p0)
@@ -165,8 +166,9 @@ def mha_seq_axis(qkv, out, L_, groups, N, E, heads):
     return out
 
 
-def softmax_rows(s, out, R, C, scale):
-    L.check(L.load().fd_softmax_rows(L.ptr(s), L.ptr(out), R, C, scale, L.dtype_code(out.dtype), L.stream()),
+def softmax_rows(s, out, R, C, scale, ldp=None):
+    L.check(L.load().fd_softmax_rows(L.ptr(s), L.ptr(out), R, C, C if ldp is None else ldp, scale,
+                                     L.dtype_code(out.dtype), L.stream()),
             "fd_softmax_rows")
     return out
 

@@ -1,0 +1,282 @@
+"""SDXL UNet + FaithDiff conditioning extras on the HIP kernel library (bf16, NHWC).
+
+Forward order follows FaithDiff/models/unet_2d_condition_vae_extension.py:480-697:
+time/aug embedding (:543-561) -> conv_in (:571) -> condition_embedding + information transformer +
+spatial_ch_projs (:572-579) -> down blocks (:611-630) -> mid (:641-655) -> up blocks (:660-684) ->
+GN + SiLU + conv_out (:686-690).  The diffusers blocks follow SURVEY Appendix B.1.
+
+MI355X-specific structure (not a translation of the reference's module graph):
+  * activations stay NHWC bf16 [M = B*H*W, C]; every Linear and 3x3/1x1 conv is one fd_gemm launch with
+    its bias / time-embedding add / residual / GEGLU fused into the MFMA epilogue;
+  * the 22 ResnetBlock2D time_emb_proj Linears are one GEMM (SiLU(emb) x [sum C_out, 1280]^T);
+  * attn1 uses one fused QKV projection; attn2's K/V projections of the (constant) prompt embeddings
+    are computed once per image (``set_context``) for all 70 transformer blocks, and one K/V pair
+    [neg, pos] serves every tile of a batched forward (kv_mod = CFG width);
+  * the up-block skip concat is folded into the conv1 gather (two-source implicit GEMM) after the
+    GroupNorm reads the materialised concat.
+Rows are [tile0 uncond, tile0 cond, tile1 uncond, ...]: several TLC tiles can share one forward.
+"""
+import torch
+
+from . import arch
+from . import lib as L
+from . import ops
+
+
+def _dev(t, device, dtype):
+    return t.to(device=device, dtype=dtype).contiguous()
+
+
+class HipUNet:
+    def __init__(self, sd, device="cuda", dtype=torch.bfloat16):
+        L.require_device()
+        self.device, self.dtype = torch.device(device), dtype
+        f32 = torch.float32
+        W = lambda k: _dev(sd[k], self.device, dtype)  # noqa: E731
+        Fp = lambda k: _dev(sd[k], self.device, f32)  # noqa: E731
+        self.W, self.Fp = W, Fp
+
+        # time / add embeddings
+        self.te = [(W("time_embedding.linear_1.weight"), Fp("time_embedding.linear_1.bias")),
+                   (W("time_embedding.linear_2.weight"), Fp("time_embedding.linear_2.bias"))]
+        self.ae = [(W("add_embedding.linear_1.weight"), Fp("add_embedding.linear_1.bias")),
+                   (W("add_embedding.linear_2.weight"), Fp("add_embedding.linear_2.bias"))]
+        self.conv_in = (Fp("conv_in.weight").permute(0, 2, 3, 1).contiguous(), Fp("conv_in.bias"))
+
+        # all resnet time_emb_proj in one matrix
+        temb_w, temb_b = [], []
+        self._temb_off = 0
+
+        def resnet(p, cin, cout):
+            r = dict(cin=cin, cout=cout,
+                     n1=(Fp(p + ".norm1.weight"), Fp(p + ".norm1.bias")),
+                     c1=(_dev(ops.pack_conv3x3(sd[p + ".conv1.weight"]), self.device, dtype), Fp(p + ".conv1.bias")),
+                     n2=(Fp(p + ".norm2.weight"), Fp(p + ".norm2.bias")),
+                     c2=(_dev(ops.pack_conv3x3(sd[p + ".conv2.weight"]), self.device, dtype), Fp(p + ".conv2.bias")),
+                     toff=self._temb_off)
+            temb_w.append(sd[p + ".time_emb_proj.weight"])
+            temb_b.append(sd[p + ".time_emb_proj.bias"])
+            self._temb_off += cout
+            if cin != cout:
+                r["sc"] = (_dev(sd[p + ".conv_shortcut.weight"].reshape(cout, cin), self.device, dtype),
+                           Fp(p + ".conv_shortcut.bias"))
+            return r
+
+        def t2d(p, c, layers):
+            blocks = []
+            for i in range(layers):
+                b = f"{p}.transformer_blocks.{i}"
+                ffw, ffb = ops.pack_geglu(sd[b + ".ff.net.0.proj.weight"], sd[b + ".ff.net.0.proj.bias"])
+                blocks.append(dict(
+                    n1=(Fp(b + ".norm1.weight"), Fp(b + ".norm1.bias")),
+                    qkv=_dev(torch.cat([sd[f"{b}.attn1.to_{n}.weight"] for n in "qkv"], 0), self.device, dtype),
+                    o1=(W(b + ".attn1.to_out.0.weight"), Fp(b + ".attn1.to_out.0.bias")),
+                    n2=(Fp(b + ".norm2.weight"), Fp(b + ".norm2.bias")),
+                    q2=W(b + ".attn2.to_q.weight"),
+                    kv2=_dev(torch.cat([sd[b + ".attn2.to_k.weight"], sd[b + ".attn2.to_v.weight"]], 0), self.device,
+                             dtype),
+                    o2=(W(b + ".attn2.to_out.0.weight"), Fp(b + ".attn2.to_out.0.bias")),
+                    n3=(Fp(b + ".norm3.weight"), Fp(b + ".norm3.bias")),
+                    ff1=(_dev(ffw, self.device, dtype), _dev(ffb, self.device, f32)),
+                    ff2=(W(b + ".ff.net.2.weight"), Fp(b + ".ff.net.2.bias")),
+                ))
+            return dict(c=c, heads=c // 64, norm=(Fp(p + ".norm.weight"), Fp(p + ".norm.bias")),
+                        pin=(W(p + ".proj_in.weight"), Fp(p + ".proj_in.bias")),
+                        pout=(W(p + ".proj_out.weight"), Fp(p + ".proj_out.bias")), blocks=blocks)
+
+        C, Lr = arch.UNET_CH, arch.UNET_LAYERS
+        self.down = []
+        prev = C[0]
+        for i in range(3):
+            blk = dict(resnets=[], attns=[], ds=None)
+            for j in range(2):
+                blk["resnets"].append(resnet(f"down_blocks.{i}.resnets.{j}", prev if j == 0 else C[i], C[i]))
+                if Lr[i]:
+                    blk["attns"].append(t2d(f"down_blocks.{i}.attentions.{j}", C[i], Lr[i]))
+            if i < 2:
+                p = f"down_blocks.{i}.downsamplers.0.conv"
+                blk["ds"] = (_dev(ops.pack_conv3x3(sd[p + ".weight"]), self.device, dtype), Fp(p + ".bias"))
+            self.down.append(blk)
+            prev = C[i]
+        self.mid = dict(r0=resnet("mid_block.resnets.0", C[2], C[2]), attn=t2d("mid_block.attentions.0", C[2], Lr[2]),
+                        r1=resnet("mid_block.resnets.1", C[2], C[2]))
+        skips = arch.up_skip_channels()
+        self.up = []
+        prev = C[2]
+        for i in range(3):
+            lvl = 2 - i
+            co = C[lvl]
+            blk = dict(resnets=[], attns=[], us=None)
+            for j in range(3):
+                blk["resnets"].append(resnet(f"up_blocks.{i}.resnets.{j}", (prev if j == 0 else co) + skips[i][j], co))
+                if Lr[lvl]:
+                    blk["attns"].append(t2d(f"up_blocks.{i}.attentions.{j}", co, Lr[lvl]))
+            if i < 2:
+                p = f"up_blocks.{i}.upsamplers.0.conv"
+                blk["us"] = (_dev(ops.pack_conv3x3(sd[p + ".weight"]), self.device, dtype), Fp(p + ".bias"))
+            self.up.append(blk)
+            prev = co
+        self.norm_out = (Fp("conv_norm_out.weight"), Fp("conv_norm_out.bias"))
+        self.conv_out = (_dev(ops.pack_conv3x3(sd["conv_out.weight"]), self.device, dtype), Fp("conv_out.bias"))
+        self.temb_w = _dev(torch.cat(temb_w, 0), self.device, dtype)
+        self.temb_b = _dev(torch.cat(temb_b, 0), self.device, f32)
+        self.temb_total = self._temb_off
+
+        # FaithDiff extras
+        self.has_extras = "spatial_ch_projs.weight" in sd
+        if self.has_extras:
+            self.cne = dict(norm=(Fp("condition_embedding.norm_in.weight"), Fp("condition_embedding.norm_in.bias")),
+                            cin=(_dev(ops.pack_conv3x3(sd["condition_embedding.conv_in.weight"]), self.device, dtype),
+                                 Fp("condition_embedding.conv_in.bias")),
+                            cout=(_dev(ops.pack_conv3x3(sd["condition_embedding.conv_out.weight"]), self.device,
+                                       dtype), Fp("condition_embedding.conv_out.bias")))
+            self.itl = []
+            for i in range(2):
+                p = f"information_transformer_layes.{i}"
+                self.itl.append(dict(
+                    ln1=(Fp(p + ".ln_1.weight"), Fp(p + ".ln_1.bias")),
+                    inp=(W(p + ".attn.in_proj_weight"), Fp(p + ".attn.in_proj_bias")),
+                    outp=(W(p + ".attn.out_proj.weight"), Fp(p + ".attn.out_proj.bias")),
+                    ln2=(Fp(p + ".ln_2.weight"), Fp(p + ".ln_2.bias")),
+                    fc=(W(p + ".mlp.c_fc.weight"), Fp(p + ".mlp.c_fc.bias")),
+                    proj=(W(p + ".mlp.c_proj.weight"), Fp(p + ".mlp.c_proj.bias"))))
+            self.scp = (W("spatial_ch_projs.weight"), Fp("spatial_ch_projs.bias"))
+        self.ctx_kv = None
+        self.ncfg = None
+
+    # ------------------------------------------------------------------------------------------ context
+    def _all_t2d(self):
+        for blk in self.down:
+            yield from blk["attns"]
+        yield self.mid["attn"]
+        for blk in self.up:
+            yield from blk["attns"]
+
+    def set_context(self, ctx):
+        """ctx: [ncfg, 77, 2048] prompt embeddings ([neg, pos] under CFG).  Computes every attn2 K/V once."""
+        ctx = ctx.to(device=self.device, dtype=self.dtype).contiguous()
+        self.ncfg, self.Lk = ctx.shape[0], ctx.shape[1]
+        flat = ctx.reshape(-1, ctx.shape[-1])
+        kvs = []
+        for t in self._all_t2d():
+            for b in t["blocks"]:
+                kv = ops.gemm(flat, b["kv2"])  # [ncfg*77, 2C]
+                b["kv"] = kv
+                kvs.append(kv)
+        self.ctx_kv = kvs
+
+    # ------------------------------------------------------------------------------------------ blocks
+    def _resnet(self, r, x, B, H, Wd, temb, x2=None, C1=None):
+        """x: [M, cin] (or concat(x [M,C1], x2) when x2 is given)."""
+        HW = H * Wd
+        if x2 is not None:
+            cat = torch.empty((B * HW, r["cin"]), dtype=self.dtype, device=self.device)
+            ops.concat_channels(x, C1, x2, r["cin"] - C1, cat, B * HW)
+            x = cat
+        h = ops.group_norm(x, *r["n1"], B, HW, r["cin"], 32, 1e-5, silu=True)
+        h = ops.conv3x3(h, r["c1"][0], r["c1"][1], B, H, Wd,
+                        rowbias=temb[:, r["toff"]:r["toff"] + r["cout"]])
+        h2 = ops.group_norm(h, *r["n2"], B, HW, r["cout"], 32, 1e-5, silu=True, out=h)
+        sc = ops.gemm(x, r["sc"][0], bias=r["sc"][1]) if "sc" in r else x
+        return ops.conv3x3(h2, r["c2"][0], r["c2"][1], B, H, Wd, residual=sc)
+
+    def _t2d(self, t, x, B, H, Wd):
+        C, heads, HW = t["c"], t["heads"], H * Wd
+        M = B * HW
+        h = ops.group_norm(x, *t["norm"], B, HW, C, 32, 1e-6, silu=False)
+        h = ops.gemm(h, t["pin"][0], bias=t["pin"][1])
+        qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
+        att = torch.empty((M, C), dtype=self.dtype, device=self.device)
+        n = torch.empty((M, C), dtype=self.dtype, device=self.device)
+        for b in t["blocks"]:
+            ops.layer_norm(h, *b["n1"], 1e-5, out=n)
+            ops.gemm(n, b["qkv"], out=qkv)
+            ops.flash_attn(qkv, qkv[:, C:], qkv[:, 2 * C:], att, B, heads, HW, HW, 3 * C, 3 * C, 3 * C, C,
+                           HW * 3 * C, HW * 3 * C, HW * 3 * C, HW * C, kv_mod=0, scale=0.125)
+            ops.gemm(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
+            ops.layer_norm(h, *b["n2"], 1e-5, out=n)
+            q = ops.gemm(n, b["q2"], out=qkv[:, :C], ldc=3 * C)
+            kv = b["kv"]
+            Lk = self.Lk
+            ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, 2 * C, 2 * C, C,
+                           HW * 3 * C, Lk * 2 * C, Lk * 2 * C, HW * C, kv_mod=self.ncfg, scale=0.125)
+            ops.gemm(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
+            ops.layer_norm(h, *b["n3"], 1e-5, out=n)
+            ff = ops.gemm(n, b["ff1"][0], bias=b["ff1"][1], act="geglu")
+            ops.gemm(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
+        return ops.gemm(h, t["pout"][0], bias=t["pout"][1], residual=x)
+
+    def _extras(self, x0, cond, B, H, Wd):
+        HW = H * Wd
+        M = B * HW
+        c = ops.group_norm(cond, *self.cne["norm"], B, HW, 512, 32, 1e-6, silu=False)
+        c = ops.conv3x3(c, *self.cne["cin"], B, H, Wd, act="silu")
+        ie = ops.conv3x3(c, *self.cne["cout"], B, H, Wd)
+        feat = torch.empty((M, 640), dtype=self.dtype, device=self.device)
+        ops.concat_channels(x0, 320, ie, 320, feat, M)
+        n = torch.empty_like(feat)
+        att = torch.empty_like(feat)
+        for lay in self.itl:
+            ops.layer_norm(feat, *lay["ln1"], 1e-5, out=n)
+            qkv = ops.gemm(n, lay["inp"][0], bias=lay["inp"][1])
+            ops.mha_seq_axis(qkv, att, self.ncfg, B // self.ncfg, HW, 640, 8)
+            ops.gemm(att, lay["outp"][0], bias=lay["outp"][1], residual=feat, out=feat)
+            ops.layer_norm(feat, *lay["ln2"], 1e-5, out=n)
+            m = ops.gemm(n, lay["fc"][0], bias=lay["fc"][1], act="quickgelu")
+            ops.gemm(m, lay["proj"][0], bias=lay["proj"][1], residual=feat, out=feat)
+        return feat
+
+    # ------------------------------------------------------------------------------------------ forward
+    def embeddings(self, t, time_ids, text_embeds, B):
+        tf = torch.empty((B, 320), dtype=self.dtype, device=self.device)
+        af = torch.empty((B, 2816), dtype=self.dtype, device=self.device)
+        ops.time_features(t, time_ids, text_embeds, tf, af, B)
+        h = ops.gemm(tf, self.te[0][0], bias=self.te[0][1], act="silu")
+        emb = ops.gemm(h, self.te[1][0], bias=self.te[1][1], out_dtype=torch.float32)
+        h = ops.gemm(af, self.ae[0][0], bias=self.ae[0][1], act="silu")
+        emb = ops.gemm(h, self.ae[1][0], bias=self.ae[1][1], residual=emb, out_dtype=torch.float32)
+        semb = torch.empty((B, 1280), dtype=self.dtype, device=self.device)
+        ops.unary(emb, semb, "silu")
+        return ops.gemm(semb, self.temb_w, bias=self.temb_b, out_dtype=torch.float32)  # [B, sum C_out]
+
+    def forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True):
+        """x: NHWC [B*H*W, 4] (dtype); t: fp32 [B]; time_ids fp32 [B, 6]; text_embeds fp32 [B, 1280];
+        cond: NHWC [B*H*W, 512] image latents (dtype) or None.  Returns eps NHWC [B*H*W, 4] (dtype)."""
+        assert self.ctx_kv is not None, "call set_context(prompt_embeds) first"
+        assert B % self.ncfg == 0
+        temb = self.embeddings(t, time_ids, text_embeds, B)
+        x0 = ops.conv_direct(x, *self.conv_in, B, H, Wd, 4, 3, 1, 1, out_dtype=self.dtype)
+        if cond is not None and self.has_extras:
+            feat = self._extras(x0, cond, B, H, Wd)
+            if add_sample:
+                x0 = ops.gemm(feat, self.scp[0], bias=self.scp[1], residual=x0)
+            else:
+                x0 = ops.gemm(feat, self.scp[0], bias=self.scp[1])
+        skips = [(x0, 320, H, Wd)]
+        h, hh, ww = x0, H, Wd
+        for i, blk in enumerate(self.down):
+            for j, r in enumerate(blk["resnets"]):
+                h = self._resnet(r, h, B, hh, ww, temb)
+                if blk["attns"]:
+                    h = self._t2d(blk["attns"][j], h, B, hh, ww)
+                skips.append((h, r["cout"], hh, ww))
+            if blk["ds"] is not None:
+                h = ops.conv3x3(h, *blk["ds"], B, hh, ww, stride=2, pad=1)
+                hh, ww = (hh + 1) // 2, (ww + 1) // 2
+                skips.append((h, r["cout"], hh, ww))
+        h = self._resnet(self.mid["r0"], h, B, hh, ww, temb)
+        h = self._t2d(self.mid["attn"], h, B, hh, ww)
+        h = self._resnet(self.mid["r1"], h, B, hh, ww, temb)
+        for i, blk in enumerate(self.up):
+            for j, r in enumerate(blk["resnets"]):
+                s, cs, _, _ = skips.pop()
+                h = self._resnet(r, h, B, hh, ww, temb, x2=s, C1=r["cin"] - cs)
+                if blk["attns"]:
+                    h = self._t2d(blk["attns"][j], h, B, hh, ww)
+            if blk["us"] is not None:
+                # Upsample2D to the next skip's size (x2, or diffusers' forward_upsample_size path, ext:665-666)
+                th, tw = skips[-1][2], skips[-1][3]
+                h = ops.conv3x3(h, *blk["us"], B, hh, ww, upsample=True, upsample_size=(th, tw))
+                hh, ww = th, tw
+        h = ops.group_norm(h, *self.norm_out, B, hh * ww, 320, 32, 1e-5, silu=True)
+        return ops.conv3x3(h, *self.conv_out, B, hh, ww)

@@ -1,0 +1,175 @@
+"""fp16 AutoencoderKL (sdxl-vae-fp16-fix) encoder/decoder and the FaithDiff denoise encoder on HIP, NHWC.
+
+Semantics per SURVEY Appendix B.2 and FaithDiff/models/unet_2d_condition_vae_extension.py:39-196:
+resnets without temb (GN eps 1e-6), VAE Downsample2D = zero pad (0,1,0,1) + conv s2 p0 (folded into the
+implicit-GEMM gather as pad=0 with a bottom/right zero fringe), Upsample2D = nearest x2 folded into the
+next conv's gather, mid-block single-head d=512 attention with residual.
+
+The d=512 attention runs as GEMM (S = QK^T/sqrt(512), fp32) -> fp32 row softmax -> GEMM (P V) on the MFMA
+GEMM kernel: a [T, T] fp32 score matrix is 1 GiB at T = 16384, which 288 GB of HBM3E holds without
+tiling; the two GEMMs carry the 0.55 TFLOP of the 1024^2 decode's attention.
+"""
+import torch
+
+from . import arch
+from . import lib as L
+from . import ops
+
+
+def _dev(t, device, dtype):
+    return t.to(device=device, dtype=dtype).contiguous()
+
+
+class _Trunk:
+    """Shared resnet / attention helpers (weights keyed by diffusers names under `prefix`)."""
+
+    def __init__(self, sd, prefix, device, dtype):
+        self.sd, self.prefix, self.device, self.dtype = sd, prefix, torch.device(device), dtype
+
+    def f32(self, k):
+        return _dev(self.sd[self.prefix + k], self.device, torch.float32)
+
+    def w(self, k):
+        return _dev(self.sd[self.prefix + k], self.device, self.dtype)
+
+    def conv(self, k):
+        return (_dev(ops.pack_conv3x3(self.sd[self.prefix + k + ".weight"]), self.device, self.dtype),
+                self.f32(k + ".bias"))
+
+    def direct(self, k):
+        return (self.f32(k + ".weight").permute(0, 2, 3, 1).contiguous(), self.f32(k + ".bias"))
+
+    def resnet(self, p, cin, cout):
+        r = dict(cin=cin, cout=cout, n1=(self.f32(p + ".norm1.weight"), self.f32(p + ".norm1.bias")),
+                 c1=self.conv(p + ".conv1"), n2=(self.f32(p + ".norm2.weight"), self.f32(p + ".norm2.bias")),
+                 c2=self.conv(p + ".conv2"))
+        if cin != cout:
+            r["sc"] = (self.w(p + ".conv_shortcut.weight").reshape(cout, cin).contiguous(),
+                       self.f32(p + ".conv_shortcut.bias"))
+        return r
+
+    def attn(self, p):
+        wq = torch.cat([self.sd[self.prefix + f"{p}.to_{n}.weight"] for n in "qkv"], 0)
+        bq = torch.cat([self.sd[self.prefix + f"{p}.to_{n}.bias"] for n in "qkv"], 0)
+        return dict(gn=(self.f32(p + ".group_norm.weight"), self.f32(p + ".group_norm.bias")),
+                    qkv=(_dev(wq, self.device, self.dtype), _dev(bq, self.device, torch.float32)),
+                    out=(self.w(p + ".to_out.0.weight"), self.f32(p + ".to_out.0.bias")))
+
+
+def run_resnet(r, x, n, H, W, dtype, device):
+    HW = H * W
+    h = ops.group_norm(x, *r["n1"], n, HW, r["cin"], 32, 1e-6, silu=True)
+    h = ops.conv3x3(h, *r["c1"], n, H, W)
+    ops.group_norm(h, *r["n2"], n, HW, r["cout"], 32, 1e-6, silu=True, out=h)
+    sc = ops.gemm(x, r["sc"][0], bias=r["sc"][1]) if "sc" in r else x
+    return ops.conv3x3(h, *r["c2"], n, H, W, residual=sc)
+
+
+def run_attn(a, x, n, H, W):
+    """Single-head d=C attention with residual (diffusers Attention, AttnProcessor2_0)."""
+    C = a["out"][0].shape[0]
+    T = H * W
+    h = ops.group_norm(x, *a["gn"], n, T, C, 32, 1e-6, silu=False)
+    qkv = ops.gemm(h, a["qkv"][0], bias=a["qkv"][1])  # [n*T, 3C]
+    out = torch.empty((n * T, C), dtype=x.dtype, device=x.device)
+    Tp = (T + 63) // 64 * 64  # the P.V GEMM contracts over T: pad K to the kernel's 64 granule with zeros
+    S = torch.empty((T, T), dtype=torch.float32, device=x.device)
+    P = torch.zeros((T, Tp), dtype=x.dtype, device=x.device)
+    Vt = torch.zeros((C, Tp), dtype=x.dtype, device=x.device)
+    for i in range(n):  # per image (the VAE runs batch 1)
+        q = qkv[i * T:(i + 1) * T]
+        ops.gemm(q, q[:, C:], out=S, M=T, N=T, K=C, lda=3 * C, ldw=3 * C, alpha=C ** -0.5, out_dtype=torch.float32)
+        ops.softmax_rows(S, P, T, T, 1.0, ldp=Tp)
+        ops.transpose(q[:, 2 * C:], 3 * C, Vt, Tp, T, C)
+        ops.gemm(P, Vt, out=out[i * T:(i + 1) * T], K=Tp)
+    return ops.gemm(out, a["out"][0], bias=a["out"][1], residual=x)
+
+
+class HipEncoder:
+    """VAE encoder trunk (with_out=True: + conv_norm_out/conv_out/quant_conv -> moments [HW, 8]) or the
+    FaithDiff denoise encoder (with_out=False -> mid-block features [HW, 512], ext:145-148)."""
+
+    def __init__(self, sd, prefix="", with_out=True, device="cuda", dtype=torch.float16, quant_sd=None):
+        L.require_device()
+        t = _Trunk(sd, prefix, device, dtype)
+        self.device, self.dtype = t.device, dtype
+        ch = arch.VAE_CH
+        self.conv_in = t.direct("conv_in")
+        self.blocks = []
+        prev = ch[0]
+        for i, c in enumerate(ch):
+            rs = [t.resnet(f"down_blocks.{i}.resnets.{j}", prev if j == 0 else c, c) for j in range(2)]
+            ds = t.conv(f"down_blocks.{i}.downsamplers.0.conv") if i < 3 else None
+            self.blocks.append((rs, ds))
+            prev = c
+        self.mid = (t.resnet("mid_block.resnets.0", 512, 512), t.attn("mid_block.attentions.0"),
+                    t.resnet("mid_block.resnets.1", 512, 512))
+        self.with_out = with_out
+        if with_out:
+            self.norm_out = (t.f32("conv_norm_out.weight"), t.f32("conv_norm_out.bias"))
+            self.conv_out = t.conv("conv_out")
+            q = quant_sd
+            self.quant = (_dev(q["quant_conv.weight"], self.device, torch.float32).permute(0, 2, 3, 1).contiguous(),
+                          _dev(q["quant_conv.bias"], self.device, torch.float32))
+        # FaithDiff Encoder tiling knobs (ext:70-73); set via set_encoder_tile_settings / enable_tiling
+        self.tile_sample_min_size = 1024
+        self.tile_latent_min_size = int(self.tile_sample_min_size / 8)
+        self.tile_overlap_factor = 0.25
+        self.use_tiling = False
+
+    def encode(self, x, n, H, W):
+        """x: NHWC [n*H*W, 3] (dtype) in [-1, 1].  Returns NHWC [n*(H/8)*(W/8), 8 or 512]."""
+        h = ops.conv_direct(x, *self.conv_in, n, H, W, 3, 3, 1, 1, out_dtype=self.dtype)
+        hh, ww = H, W
+        for rs, ds in self.blocks:
+            for r in rs:
+                h = run_resnet(r, h, n, hh, ww, self.dtype, self.device)
+            if ds is not None:
+                h = ops.conv3x3(h, *ds, n, hh, ww, stride=2, pad=0)
+                hh, ww = hh // 2, ww // 2
+        h = run_resnet(self.mid[0], h, n, hh, ww, self.dtype, self.device)
+        h = run_attn(self.mid[1], h, n, hh, ww)
+        h = run_resnet(self.mid[2], h, n, hh, ww, self.dtype, self.device)
+        if self.with_out:
+            h = ops.group_norm(h, *self.norm_out, n, hh * ww, 512, 32, 1e-6, silu=True)
+            h = ops.conv3x3(h, *self.conv_out, n, hh, ww)
+            h = ops.conv_direct(h, *self.quant, n, hh, ww, 8, 1, 1, 0, out_dtype=self.dtype)
+        return h
+
+
+class HipDecoder:
+    def __init__(self, sd, device="cuda", dtype=torch.float16):
+        L.require_device()
+        t = _Trunk(sd, "", device, dtype)
+        self.device, self.dtype = t.device, dtype
+        self.post_quant = t.direct("post_quant_conv")
+        self.conv_in = t.direct("decoder.conv_in")
+        self.mid = (t.resnet("decoder.mid_block.resnets.0", 512, 512), t.attn("decoder.mid_block.attentions.0"),
+                    t.resnet("decoder.mid_block.resnets.1", 512, 512))
+        rch = tuple(reversed(arch.VAE_CH))
+        self.blocks = []
+        prev = rch[0]
+        for i, c in enumerate(rch):
+            rs = [t.resnet(f"decoder.up_blocks.{i}.resnets.{j}", prev if j == 0 else c, c) for j in range(3)]
+            us = t.conv(f"decoder.up_blocks.{i}.upsamplers.0.conv") if i < 3 else None
+            self.blocks.append((rs, us))
+            prev = c
+        self.norm_out = (t.f32("decoder.conv_norm_out.weight"), t.f32("decoder.conv_norm_out.bias"))
+        self.conv_out = t.conv("decoder.conv_out")
+
+    def decode(self, z, n, h, w):
+        """z: NHWC [n*h*w, 4] (already divided by scaling_factor).  Returns NHWC [n*8h*8w, 3] (dtype)."""
+        x = ops.conv_direct(z, *self.post_quant, n, h, w, 4, 1, 1, 0, out_dtype=self.dtype)
+        x = ops.conv_direct(x, *self.conv_in, n, h, w, 4, 3, 1, 1, out_dtype=self.dtype)
+        x = run_resnet(self.mid[0], x, n, h, w, self.dtype, self.device)
+        x = run_attn(self.mid[1], x, n, h, w)
+        x = run_resnet(self.mid[2], x, n, h, w, self.dtype, self.device)
+        hh, ww = h, w
+        for rs, us in self.blocks:
+            for r in rs:
+                x = run_resnet(r, x, n, hh, ww, self.dtype, self.device)
+            if us is not None:
+                x = ops.conv3x3(x, *us, n, hh, ww, upsample=True)
+                hh, ww = hh * 2, ww * 2
+        x = ops.group_norm(x, *self.norm_out, n, hh * ww, 128, 32, 1e-6, silu=True)
+        return ops.conv3x3(x, *self.conv_out, n, hh, ww)

@@ -1,0 +1,17 @@
+"""Host pre-processing (mirror of utils/image_process.py:7-21).
+
+check_image_size pads bottom/right to a multiple of 8 by edge replication; the reference calls
+cv2.copyMakeBorder(BORDER_REPLICATE), which is np.pad(mode='edge') (cv2 is not needed here).
+"""
+import numpy as np
+from PIL import Image
+
+
+def check_image_size(x, padder_size=8):
+    width, height = x.size
+    mod_pad_h = (padder_size - height % padder_size) % padder_size
+    mod_pad_w = (padder_size - width % padder_size) % padder_size
+    x_np = np.array(x)
+    pad = ((0, mod_pad_h), (0, mod_pad_w)) + ((0, 0),) * (x_np.ndim - 2)
+    x = Image.fromarray(np.pad(x_np, pad, mode="edge"))
+    return x, width, height, width + mod_pad_w, height + mod_pad_h

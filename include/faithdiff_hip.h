@@ -41,8 +41,9 @@ enum { FD_ACT_NONE = 0, FD_ACT_SILU = 1, FD_ACT_GELU = 2, FD_ACT_QUICKGELU = 3, 
  *   output has N/2 columns: out = (h + b_h) * gelu(g + b_g)   (diffusers GEGLU).
  * conv != 0 turns A into an implicit im2col gather from an NHWC image (K = 9*Cin, tap-major):
  *   3x3 kernel, stride 1|2, symmetric pad `pad` (bottom/right zero-fill handles the VAE's
- *   (0,1,0,1) pad with pad = 0), optional nearest x2 upsample folded into the gather
- *   (Upsample2D), optional channel concat of two sources (A: C1 channels, A2: Cin-C1 channels).
+ *   (0,1,0,1) pad with pad = 0), optional nearest upsample folded into the gather (Upsample2D:
+ *   upsample=1 resizes Hin x Win -> Hout x Wout with src = dst*in/out, i.e. x2 or diffusers'
+ *   upsample_size for latents that are not multiples of 4; needs stride 1, pad 1), optional channel concat of two sources (A: C1 channels, A2: Cin-C1 channels).
  * Replaces: cuBLAS addmm/mm behind every nn.Linear and cuDNN conv2d behind every nn.Conv2d of
  *   ResnetBlock2D / Transformer2DModel / Down-/Upsample2D (diffusers; called from
  *   unet_2d_condition_vae_extension.py:571-690 and pipeline_FaithDiff_tlc.py:970,1272,1438).
@@ -118,9 +119,9 @@ int fd_flash_attn(const void* q, long long ldq, long long q_bstride, const void*
  * qkv: [groups*L][N][3E] (in_proj output), o: [groups*L][N][E].  L <= 8; exact for distinct rows. */
 int fd_mha_seq_axis(const void* qkv, void* o, int L, int groups, int N, int E, int heads, int dtype, void* stream);
 
-/* Row softmax of fp32 scores s[R][C] (scaled by `scale`) into p (dtype).  With fd_gemm this forms
+/* Row softmax of fp32 scores s[R][C] (scaled by `scale`) into p[R][ldp] (dtype).  With fd_gemm this forms
  * the single-head d=512 VAE mid-block attention (diffusers Attention, 1 head, upcast softmax). */
-int fd_softmax_rows(const float* s, void* p, int R, int C, float scale, int dtype, void* stream);
+int fd_softmax_rows(const float* s, void* p, int R, int C, long long ldp, float scale, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Elementwise / layout helpers (all HBM-bound).

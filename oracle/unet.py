@@ -166,8 +166,12 @@ class Upsample2D(nn.Module):
         super().__init__()
         self.conv = nn.Conv2d(ch, ch, 3, padding=1)
 
-    def forward(self, x):
-        return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
+    def forward(self, x, size=None):
+        # diffusers Upsample2D: x2, or `upsample_size` (the next skip's size) when the latent is not a
+        # multiple of 4 (forward_upsample_size, ext:522-529,665-666)
+        if size is None:
+            return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
+        return self.conv(F.interpolate(x, size=size, mode="nearest"))
 
 
 # ----------------------------------------------------------------------------- UNet blocks
@@ -215,7 +219,8 @@ class UpBlock(nn.Module):
             if self.attentions is not None:
                 x = self.attentions[i](x, ctx)
         if self.upsamplers is not None:
-            x = self.upsamplers[0](x)
+            fwd_size = any(d % 4 for d in self._latent_hw) if hasattr(self, "_latent_hw") else False
+            x = self.upsamplers[0](x, skips[-1].shape[2:] if (skips and fwd_size) else None)
         return x
 
 
@@ -344,6 +349,7 @@ class UNet2DConditionModel(nn.Module):
             skips.extend(outs)
         x = self.mid_block(x, emb, ctx)
         for blk in self.up_blocks:
+            blk._latent_hw = tuple(sample.shape[-2:])
             x = blk(x, skips, emb, ctx)
         x = F.silu(self.conv_norm_out(x))
         return self.conv_out(x)
