@@ -212,56 +212,107 @@ extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const 
 // ------------------------------------------------------------------------------------------------
 // MultiheadAttention over the sequence axis L (the CFG pair) for every pixel n, grouped: rows
 // [g*L, (g+1)*L) of the batch form one attention problem.  qkv [Btot][N][3E] -> o [Btot][N][E].
-// One thread per (group, n, head, l_query); hd = E / heads.
-template <typename T>
-__global__ void mha_seq_axis_kernel(const T* __restrict__ qkv, T* __restrict__ o, int L, int groups, int N, int E,
-                                    int heads) {
+// One thread per (group, pixel, head) computes all L query rows; the heads of a pixel are adjacent
+// threads, so a wave reads whole contiguous q/k/v rows with 16-B loads.  HBM-bound (reads qkv once).
+template <typename T, int HD, int LMAX>
+__global__ void __launch_bounds__(256) mha_seq_axis_kernel(const T* __restrict__ qkv, T* __restrict__ o, int L,
+                                                           int groups, int N, int E, int heads) {
+  typedef typename VecT<T>::v8 V8;
+  constexpr int NV = HD / 8;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)groups * N * heads * L;
+  const long long total = (long long)groups * N * heads;
   if (idx >= total) return;
-  const int l1 = idx % L;
-  long long r = idx / L;
-  const int h = r % heads;
-  r /= heads;
+  const int h = idx % heads;
+  const long long r = idx / heads;
   const int n = r % N;
   const int g = r / N;
-  const int hd = E / heads;
-  const float scale = rsqrtf((float)hd);
+  const float scale = rsqrtf((float)HD);
   const long long E3 = 3LL * E;
-  const T* qrow = qkv + ((long long)(g * L + l1) * N + n) * E3 + h * hd;
-  float s[8];
-  float mx = -INFINITY;
-  for (int l2 = 0; l2 < L; ++l2) {
-    const T* krow = qkv + ((long long)(g * L + l2) * N + n) * E3 + E + h * hd;
-    float acc = 0.f;
-    for (int d = 0; d < hd; ++d) acc += (float)qrow[d] * (float)krow[d];
-    s[l2] = acc * scale;
-    mx = fmaxf(mx, s[l2]);
+  float q[LMAX][HD];
+  float s[LMAX][LMAX];
+#pragma unroll
+  for (int l = 0; l < LMAX; ++l) {
+    if (l >= L) break;
+    const T* row = qkv + ((long long)(g * L + l) * N + n) * E3 + h * HD;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const V8 x = *(const V8*)(row + v * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) q[l][v * 8 + i] = (float)x[i];
+    }
   }
-  float den = 0.f;
-  for (int l2 = 0; l2 < L; ++l2) {
-    s[l2] = __expf(s[l2] - mx);
-    den += s[l2];
+#pragma unroll
+  for (int l2 = 0; l2 < LMAX; ++l2) {
+    if (l2 >= L) break;
+    const T* krow = qkv + ((long long)(g * L + l2) * N + n) * E3 + E + h * HD;
+    float acc[LMAX];
+#pragma unroll
+    for (int l1 = 0; l1 < LMAX; ++l1) acc[l1] = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const V8 x = *(const V8*)(krow + v * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int l1 = 0; l1 < LMAX; ++l1) acc[l1] += q[l1][v * 8 + i] * (float)x[i];
+    }
+#pragma unroll
+    for (int l1 = 0; l1 < LMAX; ++l1) s[l1][l2] = acc[l1] * scale;
   }
-  const float inv = 1.f / den;
-  T* orow = o + ((long long)(g * L + l1) * N + n) * E + h * hd;
-  for (int d = 0; d < hd; ++d) {
-    float acc = 0.f;
-    for (int l2 = 0; l2 < L; ++l2)
-      acc += s[l2] * (float)qkv[((long long)(g * L + l2) * N + n) * E3 + 2 * E + h * hd + d];
-    orow[d] = (T)(acc * inv);
+#pragma unroll
+  for (int l1 = 0; l1 < LMAX; ++l1) {
+    if (l1 >= L) break;
+    float mx = -INFINITY;
+    for (int l2 = 0; l2 < L; ++l2) mx = fmaxf(mx, s[l1][l2]);
+    float den = 0.f;
+    for (int l2 = 0; l2 < L; ++l2) {
+      s[l1][l2] = __expf(s[l1][l2] - mx);
+      den += s[l1][l2];
+    }
+    const float inv = 1.f / den;
+    for (int l2 = 0; l2 < L; ++l2) s[l1][l2] *= inv;
+  }
+  // o[l1] = sum_l2 p[l1][l2] v[l2]   (q registers reused as the accumulator)
+#pragma unroll
+  for (int l1 = 0; l1 < LMAX; ++l1)
+#pragma unroll
+    for (int d = 0; d < HD; ++d) q[l1][d] = 0.f;
+#pragma unroll
+  for (int l2 = 0; l2 < LMAX; ++l2) {
+    if (l2 >= L) break;
+    const T* vrow = qkv + ((long long)(g * L + l2) * N + n) * E3 + 2 * E + h * HD;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const V8 x = *(const V8*)(vrow + v * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int l1 = 0; l1 < LMAX; ++l1) q[l1][v * 8 + i] += s[l1][l2] * (float)x[i];
+    }
+  }
+#pragma unroll
+  for (int l1 = 0; l1 < LMAX; ++l1) {
+    if (l1 >= L) break;
+    T* orow = o + ((long long)(g * L + l1) * N + n) * E + h * HD;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      V8 y;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) y[i] = (T)q[l1][v * 8 + i];
+      *(V8*)(orow + v * 8) = y;
+    }
   }
 }
 
-extern "C" int fd_mha_seq_axis(const void* qkv, void* o, int L, int groups, int N, int E, int heads,
-                                       int dtype, void* stream) {
+extern "C" int fd_mha_seq_axis(const void* qkv, void* o, int L, int groups, int N, int E, int heads, int dtype,
+                               void* stream) {
   if (!qkv || !o) return FD_ERR_ARG;
-  if (L <= 0 || L > 8 || groups <= 0 || N <= 0 || E % heads) return FD_ERR_SHAPE;
-  const long long total = (long long)groups * N * heads * L;
+  if (L <= 0 || L > 2 || groups <= 0 || N <= 0 || heads <= 0 || E % heads || E / heads != 80) return FD_ERR_SHAPE;
+  const long long total = (long long)groups * N * heads;
   dim3 grid((unsigned)((total + 255) / 256)), block(256);
   hipStream_t s = (hipStream_t)stream;
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(mha_seq_axis_kernel<T>, grid, block, 0, s, (const T*)qkv, (T*)o, L, groups,
-                                          N, E, heads));
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((mha_seq_axis_kernel<T, 80, 2>), grid, block, 0, s, (const T*)qkv, (T*)o, L,
+                                          groups, N, E, heads));
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

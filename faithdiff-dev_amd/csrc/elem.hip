@@ -181,33 +181,41 @@ extern "C" int fd_transpose(const void* x, long long ldx, void* y, long long ldy
 }
 
 // ------------------------------------------------------------------------------------------------
-// Direct conv for Cin < 64.  One thread per (pixel, cout); consecutive threads = consecutive cout.
-template <typename TI, typename TO>
-__global__ void conv_direct_kernel(const TI* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
-                                   TO* __restrict__ y, int nimg, int Hin, int Win, int Cin, int Cout, int Hout,
-                                   int Wout, int ks, int stride, int pad, float in_scale) {
-  const long long total = (long long)nimg * Hout * Wout * Cout;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
-    const int co = e % Cout;
-    long long pix = e / Cout;
-    const int ox = pix % Wout;
-    pix /= Wout;
-    const int oy = pix % Hout;
-    const int img = pix / Hout;
-    float acc = bias ? bias[co] : 0.f;
-    const float* wr = w + (long long)co * ks * ks * Cin;
-    for (int ky = 0; ky < ks; ++ky) {
-      const int iy = oy * stride - pad + ky;
-      if (iy < 0 || iy >= Hin) continue;
-      for (int kx = 0; kx < ks; ++kx) {
-        const int ix = ox * stride - pad + kx;
-        if (ix < 0 || ix >= Win) continue;
-        const TI* xp = x + (((long long)img * Hin + iy) * Win + ix) * Cin;
-        const float* wp = wr + (ky * ks + kx) * Cin;
-        for (int c = 0; c < Cin; ++c) acc += (float)xp[c] * in_scale * wp[c];
+// Direct conv for Cin < 64 (K = k*k*Cin <= 72).  Block = 8 consecutive output pixels x all Cout
+// (threads stride over Cout); each thread keeps its output channel's K weights in registers and
+// reuses them for the 8 pixels; input taps are wave-uniform (broadcast) loads; stores are coalesced.
+template <typename TI, typename TO, int KK>
+__global__ void __launch_bounds__(256) conv_direct_kernel(const TI* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, TO* __restrict__ y, int nimg,
+                                                          int Hin, int Win, int Cin, int Cout, int Hout, int Wout,
+                                                          int ks, int stride, int pad, float in_scale) {
+  constexpr int P = 8;
+  const long long npix = (long long)nimg * Hout * Wout;
+  const long long p0 = (long long)blockIdx.x * P;
+  constexpr int K = KK;  // exact k*k*Cin (compile-time: the weights live in registers)
+  for (int co = threadIdx.x; co < Cout; co += blockDim.x) {
+    float wr[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) wr[k] = w[(long long)co * K + k];
+    const float b = bias ? bias[co] : 0.f;
+    for (int pi = 0; pi < P; ++pi) {
+      const long long pix = p0 + pi;
+      if (pix >= npix) break;
+      const int ox = pix % Wout;
+      const long long t = pix / Wout;
+      const int oy = t % Hout;
+      const int img = t / Hout;
+      float acc = b;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int c = k % Cin, tap = k / Cin;
+        const int ky = tap / ks, kx = tap % ks;
+        const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+        if (iy >= 0 && iy < Hin && ix >= 0 && ix < Win)
+          acc += (float)x[(((long long)img * Hin + iy) * Win + ix) * Cin + c] * in_scale * wr[k];
       }
+      y[pix * Cout + co] = (TO)acc;
     }
-    y[e] = (TO)acc;
   }
 }
 
@@ -216,13 +224,24 @@ extern "C" int fd_conv2d_direct(const void* x, const float* w, const float* bias
                                 int out_dtype, void* stream) {
   if (!x || !w || !y) return FD_ERR_ARG;
   if (nimg <= 0 || Hin <= 0 || Win <= 0 || Cin <= 0 || Cout <= 0 || ksize <= 0 || stride <= 0) return FD_ERR_SHAPE;
+  const int K = ksize * ksize * Cin;
   const int Hout = (Hin + 2 * pad - ksize) / stride + 1, Wout = (Win + 2 * pad - ksize) / stride + 1;
-  const long long total = (long long)nimg * Hout * Wout * Cout;
+  const long long npix = (long long)nimg * Hout * Wout;
+  dim3 grid((unsigned)((npix + 7) / 8)), block(Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64);
   hipStream_t s = (hipStream_t)stream;
-  FD_DISPATCH_I(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv_direct_kernel<TI, TO>), grid1d(total),
-                                                                   dim3(256), 0, s, (const TI*)x, w, bias, (TO*)y, nimg,
-                                                                   Hin, Win, Cin, Cout, Hout, Wout, ksize, stride, pad,
-                                                                   in_scale)));
+#define FD_CONV_DIRECT(KK)                                                                                    \
+  FD_DISPATCH_I(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv_direct_kernel<TI, TO, KK>), grid, block, 0, \
+                                                                   s, (const TI*)x, w, bias, (TO*)y, nimg, Hin, Win,  \
+                                                                   Cin, Cout, Hout, Wout, ksize, stride, pad,         \
+                                                                   in_scale)))
+  switch (K) {  // the FaithDiff convs with Cin < 64: 3x3x4, 3x3x3, 1x1x8, 1x1x4
+    case 36: FD_CONV_DIRECT(36); break;
+    case 27: FD_CONV_DIRECT(27); break;
+    case 8: FD_CONV_DIRECT(8); break;
+    case 4: FD_CONV_DIRECT(4); break;
+    default: return FD_ERR_SHAPE;
+  }
+#undef FD_CONV_DIRECT
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

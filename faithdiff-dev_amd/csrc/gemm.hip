@@ -10,26 +10,59 @@
 // ds_read_b128 fragment address.  The conv variant gathers its A rows straight from the NHWC
 // image (im2col never materialised): out-of-image taps point at a zero page, the nearest x2
 // Upsample2D and the up-block skip concat are folded into that gather.
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "fd_common.h"
 
 __device__ __attribute__((aligned(256))) unsigned char g_zero_page[256];
 
-template <typename T, int BM, int BN, int WM, int WN, bool CONV, bool GEGLU, typename TO>
-__global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p) {
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Tile order.  Workgroups are dealt round-robin to the 8 XCDs (blocks b and b+8 share one; each XCD has
+// its own 4 MiB L2).  swz = 1: give each XCD a contiguous chunk of the tile space (bijective remap,
+// cdna_hip_programming.md section 5 "XCD swizzle must be bijective"), and walk that chunk in groups of
+// GROUP_M tile rows so the ~32 tiles an XCD runs at once share A row-panels and B column-panels in L2.
+__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int swz, int& tm, int& tn) {
+  if (!swz) {
+    tm = bid / tiles_n;
+    tn = bid % tiles_n;
+    return;
+  }
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  constexpr int GROUP_M = 4;
+  const int group = pid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_group = pid - group * (GROUP_M * tiles_n);
+  tm = first_m + in_group % gsz;
+  tn = in_group / gsz;
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int NS, bool CONV, bool GEGLU, typename TO>
+__global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int swz) {
   typedef typename VecT<T>::v8 V8;
   constexpr int WAVES_N = BN / WN;
   constexpr int MT = WM / 16, NT = WN / 16;
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int A_INSTR = BM / 32, B_INSTR = BN / 32;
+  constexpr int PER = A_INSTR + B_INSTR;  // global_load_lds per lane per pipeline stage
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STAGE];
+  static_assert(NS >= 2 && NS <= 4 && (NS - 2) * PER < 64, "pipeline depth");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int tiles_n = (p.N + BN - 1) / BN;
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  int tm, tn;
+  tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, swz, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const long long bz = blockIdx.z;
   const T* __restrict__ A = (const T*)p.A + bz * p.strideA;
@@ -112,16 +145,22 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  // NS-deep LDS ring: stages kt+1 .. kt+NS-2 stay in flight (counted vmcnt) while stage kt is
+  // consumed; one raw s_barrier per K-step (guide section 5, "Pipelining across barriers").
   const int nk = K / 64;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < nk) stage(s0, s0);
 
   const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
-    const unsigned char* sa = smem + buf * STAGE;
+    const int ahead = min(NS - 2, nk - 1 - kt);  // stages issued after kt that may still be in flight
+    if (NS >= 4 && ahead >= 2) wait_vmcnt<(NS >= 4 ? 2 * PER : 0)>();
+    else if (NS >= 3 && ahead >= 1) wait_vmcnt<(NS >= 3 ? PER : 0)>();
+    else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + NS - 1 < nk) stage(kt + NS - 1, (kt + NS - 1) % NS);
+    const unsigned char* sa = smem + (kt % NS) * STAGE;
     const unsigned char* sb = sa + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -142,8 +181,6 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p) {
 #pragma unroll
         for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = mfma16x16x32(af[mi], bfr[ni], acc[mi][ni]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
   // ---- epilogue: acc[mi][ni][j] = C[m0 + wm*WM + mi*16 + 4*fg + j][n0 + wn*WN + ni*16 + fr]
@@ -194,29 +231,79 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p) {
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, typename TO>
-static int launch_cfg(const fd_gemm_params* p, hipStream_t s) {
+template <typename T, int BM, int BN, int WM, int WN, int NS, typename TO>
+static int launch_cfg(const fd_gemm_params* p, hipStream_t s, int swz) {
   const int tiles = ((p->M + BM - 1) / BM) * ((p->N + BN - 1) / BN);
   dim3 grid(tiles, 1, p->batch > 0 ? p->batch : 1), block(256);
   if (p->conv) {
     if (p->act == FD_ACT_GEGLU) return FD_ERR_ARG;
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, true, false, TO>), grid, block, 0, s, *p);
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, true, false, TO>), grid, block, 0, s, *p, swz);
   } else if (p->act == FD_ACT_GEGLU) {
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, false, true, TO>), grid, block, 0, s, *p);
+    if constexpr (WN % 32 == 0)
+      hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, true, TO>), grid, block, 0, s, *p, swz);
+    else
+      return FD_ERR_ARG;
   } else {
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, false, false, TO>), grid, block, 0, s, *p);
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, false, TO>), grid, block, 0, s, *p, swz);
   }
   FD_LAUNCH_CHECK();
   return FD_OK;
 }
 
+// Tile choice: cost ~ ceil(tiles / (256 CUs x resident WGs per CU)) x per-tile time; a smaller tile is
+// worth it only when it removes a partial wave.  Relative per-tile efficiencies are estimates.
+enum { CFG_128x128, CFG_64x160, CFG_128x64, CFG_64x64, CFG_COUNT };
+static const int CFG_BM[] = {128, 64, 128, 64}, CFG_BN[] = {128, 160, 64, 64};
+
+static int pick_cfg(const fd_gemm_params* p) {
+  const long long b = p->batch > 0 ? p->batch : 1;
+  const double eff[] = {1.00, 0.92, 0.85, 0.60};
+  int best = CFG_128x128;
+  double bestc = 1e30;
+  for (int c = 0; c < CFG_COUNT; ++c) {
+    if (p->act == FD_ACT_GEGLU && c == CFG_64x160) continue;
+    const long long tiles = b * ((p->M + CFG_BM[c] - 1) / CFG_BM[c]) * ((p->N + CFG_BN[c] - 1) / CFG_BN[c]);
+    const long long waves = (tiles + 255) / 256;
+    const double cost = waves * (double)(CFG_BM[c] * CFG_BN[c]) / eff[c];
+    if (cost < bestc - 1e-9) { bestc = cost; best = c; }
+  }
+  return best;
+}
+
+// Tuning overrides (benchmarks only): FD_GEMM_CFG=<0..3> forces the tile, FD_GEMM_NS=<2|3|4> the ring
+// depth, FD_GEMM_SWZ=<0|1> the tile order.  Read once.
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+static int g_cfg = -2, g_ns = -1, g_swz = -1;
+
+template <typename T, typename TO, int BM, int BN, int WM, int WN>
+static int dispatch_ns(const fd_gemm_params* p, hipStream_t s, int ns, int swz) {
+  if constexpr (std::is_same<T, TO>::value) {
+    if (ns == 2) return launch_cfg<T, BM, BN, WM, WN, 2, TO>(p, s, swz);
+    if (ns == 3) return launch_cfg<T, BM, BN, WM, WN, 3, TO>(p, s, swz);
+    return launch_cfg<T, BM, BN, WM, WN, 4, TO>(p, s, swz);
+  } else {
+    return launch_cfg<T, BM, BN, WM, WN, 2, TO>(p, s, swz);
+  }
+}
+
 template <typename T, typename TO>
 static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
-  const long long t128 = (long long)((p->M + 127) / 128) * ((p->N + 127) / 128) * (p->batch > 0 ? p->batch : 1);
-  const long long t12864 = (long long)((p->M + 127) / 128) * ((p->N + 63) / 64) * (p->batch > 0 ? p->batch : 1);
-  if (p->N > 64 && t128 >= 256) return launch_cfg<T, 128, 128, 64, 64, TO>(p, s);
-  if (t12864 >= 256 || p->N <= 64) return launch_cfg<T, 128, 64, 64, 32, TO>(p, s);
-  return launch_cfg<T, 64, 64, 32, 32, TO>(p, s);
+  if (g_cfg == -2) {
+    g_cfg = env_int("FD_GEMM_CFG", -1);
+    g_ns = env_int("FD_GEMM_NS", 2);
+    g_swz = env_int("FD_GEMM_SWZ", 1);
+  }
+  int cfg = g_cfg >= 0 && g_cfg < CFG_COUNT ? g_cfg : pick_cfg(p);
+  if (p->act == FD_ACT_GEGLU && cfg == CFG_64x160) cfg = CFG_128x128;
+  switch (cfg) {
+    case CFG_128x128: return dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, g_ns, g_swz);
+    case CFG_64x160: return dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, g_ns, g_swz);
+    case CFG_128x64: return dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, g_ns, g_swz);
+    default: return dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, g_ns, g_swz);
+  }
 }
 
 extern "C" int fd_gemm(const fd_gemm_params* p, void* stream) {

@@ -75,7 +75,7 @@ typedef struct fd_gemm_params {
 
 int fd_gemm(const fd_gemm_params* p, void* stream);
 
-/* Direct convolution for the few convs with Cin < 64 (UNet conv_in 4->320, VAE conv_in 3->128,
+/* Direct convolution for the few convs with Cin < 64 (k*k*Cin in {36, 27, 8, 4}) (UNet conv_in 4->320, VAE conv_in 3->128,
  * decoder conv_in 4->512, quant_conv / post_quant_conv 1x1).  x NHWC (dtype), w fp32
  * [Cout][kh][kw][Cin], bias fp32, y NHWC (out_dtype).  in_scale multiplies x on load.
  * Replaces: cuDNN conv2d of those layers (ext:571; diffusers Encoder/Decoder conv_in). */
@@ -116,7 +116,8 @@ int fd_flash_attn(const void* q, long long ldq, long long q_bstride, const void*
 /* The information transformer's nn.MultiheadAttention(640, 8) with batch_first=False fed
  * (L=B, N=HW, E) (ext:242,251-254,576-577): for each pixel n, softmax attention over the L rows of
  * each of `groups` consecutive row groups (one group = one tile's CFG pair when tiles are batched).
- * qkv: [groups*L][N][3E] (in_proj output), o: [groups*L][N][E].  L <= 8; exact for distinct rows. */
+ * qkv: [groups*L][N][3E] (in_proj output), o: [groups*L][N][E].  L <= 2 (the CFG pair), head dim 80
+ * (FaithDiff's 640 / 8); exact for distinct rows. */
 int fd_mha_seq_axis(const void* qkv, void* o, int L, int groups, int N, int E, int heads, int dtype, void* stream);
 
 /* Row softmax of fp32 scores s[R][C] (scaled by `scale`) into p[R][ldp] (dtype).  With fd_gemm this forms
