@@ -192,6 +192,24 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(const TI* __restrict__
   constexpr int P = 8;
   const long long npix = (long long)nimg * Hout * Wout;
   const long long p0 = (long long)blockIdx.x * P;
+  // im2col of the block's 8 output pixels (8 x K values) staged once in LDS, read as broadcasts
+  __shared__ float patch[P][KK];
+  for (int e = threadIdx.x; e < P * KK; e += blockDim.x) {
+    const int pi = e / KK, k = e % KK;
+    const long long pix = p0 + pi;
+    float v = 0.f;
+    if (pix < npix) {
+      const int ox = pix % Wout;
+      const long long t = pix / Wout;
+      const int oy = t % Hout;
+      const int img = t / Hout;
+      const int c = k % Cin, tap = k / Cin;
+      const int iy = oy * stride - pad + tap / ks, ix = ox * stride - pad + tap % ks;
+      if (iy >= 0 && iy < Hin && ix >= 0 && ix < Win) v = (float)x[(((long long)img * Hin + iy) * Win + ix) * Cin + c];
+    }
+    patch[pi][k] = v * in_scale;
+  }
+  __syncthreads();
   constexpr int K = KK;  // exact k*k*Cin (compile-time: the weights live in registers)
   for (int co = threadIdx.x; co < Cout; co += blockDim.x) {
     float wr[K];
@@ -201,19 +219,9 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(const TI* __restrict__
     for (int pi = 0; pi < P; ++pi) {
       const long long pix = p0 + pi;
       if (pix >= npix) break;
-      const int ox = pix % Wout;
-      const long long t = pix / Wout;
-      const int oy = t % Hout;
-      const int img = t / Hout;
       float acc = b;
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int c = k % Cin, tap = k / Cin;
-        const int ky = tap / ks, kx = tap % ks;
-        const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
-        if (iy >= 0 && iy < Hin && ix >= 0 && ix < Win)
-          acc += (float)x[(((long long)img * Hin + iy) * Win + ix) * Cin + c] * in_scale * wr[k];
-      }
+      for (int k = 0; k < K; ++k) acc += patch[pi][k] * wr[k];
       y[pix * Cout + co] = (TO)acc;
     }
   }

@@ -55,7 +55,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
   constexpr int PER = A_INSTR + B_INSTR;  // global_load_lds per lane per pipeline stage
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
   static_assert(NS >= 2 && NS <= 4 && (NS - 2) * PER < 64, "pipeline depth");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * STAGE];
+  constexpr int BNO = GEGLU ? BN / 2 : BN;   // output columns of the tile
+  constexpr int LDE = BNO + 4;               // fp32 epilogue staging row stride (16-B aligned rows)
+  constexpr int SMEM = (NS * STAGE > BM * LDE * 4) ? NS * STAGE : BM * LDE * 4;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -183,30 +186,25 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
     }
   }
 
-  // ---- epilogue: acc[mi][ni][j] = C[m0 + wm*WM + mi*16 + 4*fg + j][n0 + wn*WN + ni*16 + fr]
-  TO* __restrict__ C = (TO*)p.C + bz * p.strideC;
-  const TO* __restrict__ R = p.residual ? (const TO*)p.residual + bz * p.strideR : nullptr;
+  // ---- epilogue, phase 1: acc[mi][ni][j] = C[wm*WM + mi*16 + 4*fg + j][wn*WN + ni*16 + fr] (tile-local)
+  // -> alpha, bias, per-row-group bias, activation / GEGLU in fp32 -> LDS tile [BM][LDE] (fp32)
+  __syncthreads();  // every wave is done reading the operand ring
+  float* ep = (float*)smem;
   const float alpha = p.alpha;
   if (GEGLU) {
-    const int Nout = N / 2;
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
       for (int ni = 0; ni < NT; ni += 2) {
-        const int np = n0 + wn * WN + ni * 16 + fr;      // packed "hidden" column
-        const int no = (n0 + wn * WN) / 2 + (ni / 2) * 16 + fr;
-        if (np >= N) continue;
-        const float bh = p.bias ? p.bias[np] : 0.f, bg = p.bias ? p.bias[np + 16] : 0.f;
+        const int np = n0 + wn * WN + ni * 16 + fr;  // packed "hidden" column; gate at np + 16
+        const int col = (wn * WN) / 2 + (ni / 2) * 16 + fr;
+        const float bh = (p.bias && np < N) ? p.bias[np] : 0.f, bg = (p.bias && np < N) ? p.bias[np + 16] : 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int m = m0 + wm * WM + mi * 16 + fg * 4 + j;
-          if (m >= M) continue;
+          const int row = wm * WM + mi * 16 + fg * 4 + j;
           const float h = acc[mi][ni][j] * alpha + bh;
           const float g = acc[mi][ni + 1][j] * alpha + bg;
-          float v = h * gelu_f(g);
-          if (R) v += (float)R[(long long)m * p.ldr + no];
-          C[(long long)m * p.ldc + no] = (TO)v;
-          (void)Nout;
+          ep[row * LDE + col] = h * gelu_f(g);
         }
       }
   } else {
@@ -214,20 +212,56 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
     for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni) {
-        const int n = n0 + wn * WN + ni * 16 + fr;
-        if (n >= N) continue;
-        const float b = p.bias ? p.bias[n] : 0.f;
+        const int col = wn * WN + ni * 16 + fr;
+        const int n = n0 + col;
+        const float b = (p.bias && n < N) ? p.bias[n] : 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int m = m0 + wm * WM + mi * 16 + fg * 4 + j;
-          if (m >= M) continue;
+          const int row = wm * WM + mi * 16 + fg * 4 + j;
+          const int m = m0 + row;
           float v = acc[mi][ni][j] * alpha + b;
-          if (p.rowbias) v += p.rowbias[(long long)(m / p.rows_per_group) * p.rowbias_ld + n];
-          v = act_f(v, p.act);
-          if (R) v += (float)R[(long long)m * p.ldr + n];
-          C[(long long)m * p.ldc + n] = (TO)v;
+          if (p.rowbias && m < M && n < N) v += p.rowbias[(long long)(m / p.rows_per_group) * p.rowbias_ld + n];
+          ep[row * LDE + col] = act_f(v, p.act);
         }
       }
+  }
+  __syncthreads();
+
+  // ---- phase 2: whole-row 16-B vector residual loads and stores (8 outputs per thread per step)
+  TO* __restrict__ C = (TO*)p.C + bz * p.strideC;
+  const TO* __restrict__ R = p.residual ? (const TO*)p.residual + bz * p.strideR : nullptr;
+  const int Nout = GEGLU ? N / 2 : N;
+  const int n0o = GEGLU ? n0 / 2 : n0;
+  const bool vec = (Nout % 8 == 0) && (p.ldc % 8 == 0) && ((((unsigned long long)C) & 15) == 0) &&
+                   (!R || ((p.ldr % 8 == 0) && ((((unsigned long long)R) & 15) == 0)));
+  constexpr int VPR = BNO / 8;
+  for (int e = tid; e < BM * VPR; e += 256) {
+    const int r = e / VPR, cv = e - (e / VPR) * VPR;
+    const int m = m0 + r, n = n0o + cv * 8;
+    if (m >= M || n >= Nout) continue;
+    const float* src = ep + r * LDE + cv * 8;
+    float v[8];
+    *(f32x4*)&v[0] = *(const f32x4*)src;
+    *(f32x4*)&v[4] = *(const f32x4*)(src + 4);
+    if (vec && n + 8 <= Nout) {
+      if (R) {
+        typedef __attribute__((ext_vector_type(8))) TO TO8;
+        const TO8 rv = *(const TO8*)(R + (long long)m * p.ldr + n);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += (float)rv[i];
+      }
+      typedef __attribute__((ext_vector_type(8))) TO TO8;
+      TO8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (TO)v[i];
+      *(TO8*)(C + (long long)m * p.ldc + n) = o;
+    } else {
+      for (int i = 0; i < 8 && n + i < Nout; ++i) {
+        float x = v[i];
+        if (R) x += (float)R[(long long)m * p.ldr + n + i];
+        C[(long long)m * p.ldc + n + i] = (TO)x;
+      }
+    }
   }
 }
 
@@ -293,16 +327,18 @@ template <typename T, typename TO>
 static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
   if (g_cfg == -2) {
     g_cfg = env_int("FD_GEMM_CFG", -1);
-    g_ns = env_int("FD_GEMM_NS", 2);
+    g_ns = env_int("FD_GEMM_NS", 0);
     g_swz = env_int("FD_GEMM_SWZ", 1);
   }
   int cfg = g_cfg >= 0 && g_cfg < CFG_COUNT ? g_cfg : pick_cfg(p);
+  // ring depth: 4 stages (1 WG/CU) pays only on long K; 2 stages (2-3 WGs/CU) otherwise (gemm_sweep)
+  const int ns = g_ns ? g_ns : (p->K >= 4096 ? 4 : 2);
   if (p->act == FD_ACT_GEGLU && cfg == CFG_64x160) cfg = CFG_128x128;
   switch (cfg) {
-    case CFG_128x128: return dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, g_ns, g_swz);
-    case CFG_64x160: return dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, g_ns, g_swz);
-    case CFG_128x64: return dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, g_ns, g_swz);
-    default: return dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, g_ns, g_swz);
+    case CFG_128x128: return dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, g_swz);
+    case CFG_64x160: return dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, g_swz);
+    case CFG_128x64: return dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, g_swz);
+    default: return dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, g_swz);
   }
 }
 

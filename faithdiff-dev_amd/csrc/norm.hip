@@ -9,10 +9,10 @@
 
 #define GN_MAXC 2560
 
-static inline int gn_rows_per_chunk(int HW) {
-  // ~64 rows per chunk, at most 256 chunks per image
-  int r = 64;
-  while ((HW + r - 1) / r > 256) r *= 2;
+static inline int gn_rows_per_chunk(int nimg, int HW) {
+  // ~512 partial blocks in total (fills the chip even at the 32x32 level), at most 512 chunks per image
+  int r = 1;
+  while ((long long)nimg * ((HW + r - 1) / r) > 512 || (HW + r - 1) / r > 512) r *= 2;
   return r;
 }
 
@@ -88,20 +88,32 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
   const int img = blockIdx.y;
   const int t = threadIdx.x;
   const int cpg = C / groups;
-  if (t < groups) {
+  // fold the per-chunk partials: SUB = 256/groups threads per group, each a strided share of the chunks
+  // (fixed order -> bitwise reproducible), then a shuffle tree in fp64
+  {
+    const int SUB = 256 / groups;  // groups <= 64 -> SUB >= 4 (power of two for groups in {32, 64})
+    const int g = t / SUB, j = t % SUB;
     double s = 0.0, q = 0.0;
-    const float2* p = part + (long long)img * nchunks * groups + t;
-    for (int c = 0; c < nchunks; ++c) {
-      const float2 v = p[(long long)c * groups];
-      s += v.x;
-      q += v.y;
+    if (g < groups) {
+      const float2* p = part + (long long)img * nchunks * groups + g;
+      for (int c = j; c < nchunks; c += SUB) {
+        const float2 v = p[(long long)c * groups];
+        s += v.x;
+        q += v.y;
+      }
     }
-    const double n = (double)HW * cpg;
-    const double mean = s / n;
-    double var = q / n - mean * mean;
-    if (var < 0) var = 0;
-    mean_s[t] = (float)mean;
-    rstd_s[t] = (float)(1.0 / sqrt(var + (double)eps));
+    for (int o = SUB / 2; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o, 64);
+      q += __shfl_xor(q, o, 64);
+    }
+    if (g < groups && j == 0) {
+      const double n = (double)HW * cpg;
+      const double mean = s / n;
+      double var = q / n - mean * mean;
+      if (var < 0) var = 0;
+      mean_s[g] = (float)mean;
+      rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
+    }
   }
   __syncthreads();
   for (int c = t; c < C; c += 256) {
@@ -132,7 +144,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
 }
 
 extern "C" long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups) {
-  const int rpc = gn_rows_per_chunk(HW);
+  const int rpc = gn_rows_per_chunk(nimg, HW);
   const int nch = (HW + rpc - 1) / rpc;
   return (long long)nimg * nch * groups * sizeof(float2);
 }
@@ -140,15 +152,17 @@ extern "C" long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups)
 extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
                              int groups, float eps, int silu, int dtype, void* ws, void* stream) {
   if (!x || !y || !ws) return FD_ERR_ARG;
-  if (nimg <= 0 || HW <= 0 || C <= 0 || groups <= 0 || groups > 64 || C % groups || C % 8 || C > GN_MAXC)
+  if (nimg <= 0 || HW <= 0 || C <= 0 || groups <= 0 || groups > 64 || (groups & (groups - 1)) || C % groups ||
+      C % 8 || C > GN_MAXC)
     return FD_ERR_SHAPE;
-  const int rpc = gn_rows_per_chunk(HW);
+  const int rpc = gn_rows_per_chunk(nimg, HW);
   const int nch = (HW + rpc - 1) / rpc;
   hipStream_t s = (hipStream_t)stream;
   const int NV = (C / 8 > 256) ? 2 : 1;
   if (NV == 2 && (C % 16)) return FD_ERR_SHAPE;
-  // apply: ~32 rows per block
-  const int rpb = 32;
+  // apply: ~1024 blocks in total, each a run of whole rows
+  int rpb = 1;
+  while ((long long)nimg * ((HW + rpb - 1) / rpb) > 1024) rpb *= 2;
   const int nblk = (HW + rpb - 1) / rpb;
   if (NV == 1) {
     FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_partial_kernel<T, 1>), dim3(nch, nimg), dim3(256), 0, s, (const T*)x,
