@@ -282,6 +282,10 @@ class AutoencoderKL:
         self._enc = self._dec = None
         self.use_tiling = False
         self.tile_overlap_factor = 0.25
+        # diffusers sets these from config.sample_size at construction; later config changes (as
+        # set_encoder_tile_settings makes, pipeline:895) do not move them -- reproduced.
+        self.tile_sample_min_size = self.config.sample_size
+        self.tile_latent_min_size = int(self.config.sample_size / 8)
 
     @classmethod
     def from_pretrained(cls, path, subfolder=None, seed=0, init_device="cpu", **kwargs):
@@ -330,13 +334,13 @@ class AutoencoderKL:
         return self._dec
 
     def encode_moments_nhwc(self, x, H, W):
-        if self.use_tiling and (H > self.config.sample_size or W > self.config.sample_size):
+        if self.use_tiling and (H > self.tile_sample_min_size or W > self.tile_sample_min_size):
             from fdhip.tiling import tiled_vae_encode
             return tiled_vae_encode(self, x, H, W)
         return self.encoder_hip().encode(x, 1, H, W)
 
     def decode_nhwc(self, z, h, w):
-        tl = self.config.sample_size // 8
+        tl = self.tile_latent_min_size
         if self.use_tiling and (h > tl or w > tl):
             from fdhip.tiling import tiled_vae_decode
             return tiled_vae_decode(self, z, h, w)

@@ -568,6 +568,60 @@ extern "C" int fd_postprocess_u8(const void* x, void* y, long long n, int dtype,
 }
 
 // ------------------------------------------------------------------------------------------------
+// Tiled VAE / encoder seam blending (diffusers AutoencoderKL.blend_v / blend_h, FaithDiff
+// Encoder.blend_v / blend_h ext:150-162), in place on tile b (NHWC [Hb][Wb][C]):
+//   vertical:   b[y][x] = a[Ha - e + y][x] * (1 - y/e) + b[y][x] * (y/e)   for y < e
+//   horizontal: b[y][x] = a[y][Wa - e + x] * (1 - x/e) + b[y][x] * (x/e)   for x < e
+// e = min(extent, Ha|Wa, Hb|Wb) as in the reference.  Tiles are blended in the reference's order
+// (row by row, vertical then horizontal), each call reading the already-blended neighbour.
+template <typename T>
+__global__ void blend_edge_kernel(const T* __restrict__ a, T* __restrict__ b, int Ha, int Wa, int Hb, int Wb, int C,
+                                  int e, int vertical) {
+  const long long total = vertical ? (long long)e * Wb * C : (long long)Hb * e * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = i % C;
+    const long long r = i / C;
+    int y, x;
+    float w;
+    long long ai;
+    if (vertical) {
+      x = r % Wb;
+      y = r / Wb;
+      w = (float)y / (float)e;
+      ai = ((long long)(Ha - e + y) * Wa + x) * C + c;
+    } else {
+      x = r % e;
+      y = r / e;
+      w = (float)x / (float)e;
+      ai = ((long long)y * Wa + (Wa - e + x)) * C + c;
+    }
+    const long long bi = ((long long)y * Wb + x) * C + c;
+    b[bi] = (T)((float)a[ai] * (1.f - w) + (float)b[bi] * w);
+  }
+}
+
+extern "C" int fd_blend_edge(const void* a, void* b, int Ha, int Wa, int Hb, int Wb, int C, int extent, int vertical,
+                             int dtype, void* stream) {
+  if (!a || !b) return FD_ERR_ARG;
+  if (C <= 0 || Ha <= 0 || Wa <= 0 || Hb <= 0 || Wb <= 0) return FD_ERR_SHAPE;
+  int e = extent;
+  if (vertical) {
+    e = min(e, min(Ha, Hb));
+    if (Wa != Wb) return FD_ERR_SHAPE;
+  } else {
+    e = min(e, min(Wa, Wb));
+    if (Ha != Hb) return FD_ERR_SHAPE;
+  }
+  if (e <= 0) return FD_OK;
+  const long long total = vertical ? (long long)e * Wb * C : (long long)Hb * e * C;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_I(dtype, hipLaunchKernelGGL(blend_edge_kernel<TI>, grid1d(total), dim3(256), 0, s, (const TI*)a, (TI*)b,
+                                          Ha, Wa, Hb, Wb, C, e, vertical));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
 extern "C" int fd_device_check(void) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return FD_ERR_HIP;

@@ -331,8 +331,11 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
     g_swz = env_int("FD_GEMM_SWZ", 1);
   }
   int cfg = g_cfg >= 0 && g_cfg < CFG_COUNT ? g_cfg : pick_cfg(p);
-  // ring depth: 4 stages (1 WG/CU) pays only on long K; 2 stages (2-3 WGs/CU) otherwise (gemm_sweep)
-  const int ns = g_ns ? g_ns : (p->K >= 4096 ? 4 : 2);
+  // ring depth: 4 stages (1 WG/CU) pays only on long K when one wave of tiles covers the launch; 2 stages
+  // (2-3 co-resident WGs/CU) otherwise (scripts/gemm_sweep.py + in-situ traces)
+  const long long tiles = (long long)(p->batch > 0 ? p->batch : 1) * ((p->M + CFG_BM[cfg] - 1) / CFG_BM[cfg]) *
+                          ((p->N + CFG_BN[cfg] - 1) / CFG_BN[cfg]);
+  const int ns = g_ns ? g_ns : ((p->K >= 4096 && tiles <= 256) ? 4 : 2);
   if (p->act == FD_ACT_GEGLU && cfg == CFG_64x160) cfg = CFG_128x128;
   switch (cfg) {
     case CFG_128x128: return dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, g_swz);

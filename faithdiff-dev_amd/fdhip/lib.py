@@ -63,6 +63,7 @@ _SIGS = {
                                   c_int, c_vp, c_int, c_vp]),
     "fd_vae_sample_add_noise": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f, c_f, c_f, c_int, c_int, c_vp]),
     "fd_postprocess_u8": (c_int, [c_vp, c_vp, c_ll, c_int, c_vp]),
+    "fd_blend_edge": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "fd_device_check": (c_int, []),
     "fd_version": (c_char_p, []),
 }

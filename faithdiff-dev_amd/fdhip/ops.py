@@ -257,3 +257,16 @@ def postprocess_u8(x, out):
     L.check(L.load().fd_postprocess_u8(L.ptr(x), L.ptr(out), x.numel(), L.dtype_code(x.dtype), L.stream()),
             "fd_postprocess_u8")
     return out
+
+
+def blend_edge(a, b, Ha, Wa, Hb, Wb, C, extent, vertical):
+    L.check(L.load().fd_blend_edge(L.ptr(a), L.ptr(b), Ha, Wa, Hb, Wb, C, extent, int(vertical),
+                                   L.dtype_code(b.dtype), L.stream()), "fd_blend_edge")
+    return b
+
+
+def copy_2d(src, src_ld, dst, dst_ld, rows, cols):
+    """dst[r][0:cols] = src[r][0:cols] (element row strides src_ld / dst_ld)."""
+    L.check(L.load().fd_add_strided(L.ptr(src), src_ld, None, 0, L.ptr(dst), dst_ld, rows, cols,
+                                    L.dtype_code(src.dtype), L.dtype_code(dst.dtype), L.stream()), "fd_add_strided")
+    return dst

@@ -9,8 +9,8 @@ MI355X-specific structure (not a translation of the reference's module graph):
   * activations stay NHWC bf16 [M = B*H*W, C]; every Linear and 3x3/1x1 conv is one fd_gemm launch with
     its bias / time-embedding add / residual / GEGLU fused into the MFMA epilogue;
   * the 22 ResnetBlock2D time_emb_proj Linears are one GEMM (SiLU(emb) x [sum C_out, 1280]^T);
-  * attn1 uses one fused QKV projection; attn2's K/V projections of the (constant) prompt embeddings
-    are computed once per image (``set_context``) for all 70 transformer blocks, and one K/V pair
+  * attn1 uses one fused QKV projection; attn2's K/V projections of the prompt embeddings for all 70
+    transformer blocks are ONE GEMM per forward ([ncfg*77, 2048] x [166400, 2048]^T), and one K/V pair
     [neg, pos] serves every tile of a batched forward (kv_mod = CFG width);
   * the up-block skip concat is folded into the conv1 gather (two-source implicit GEMM) after the
     GroupNorm reads the materialised concat.
@@ -141,7 +141,16 @@ class HipUNet:
                     fc=(W(p + ".mlp.c_fc.weight"), Fp(p + ".mlp.c_fc.bias")),
                     proj=(W(p + ".mlp.c_proj.weight"), Fp(p + ".mlp.c_proj.bias"))))
             self.scp = (W("spatial_ch_projs.weight"), Fp("spatial_ch_projs.bias"))
-        self.ctx_kv = None
+        # all 70 attn2 K/V projections of the prompt as ONE [sum 2C, 2048] weight: one GEMM per forward
+        kv_ws, off = [], 0
+        for t in self._all_t2d():
+            for b in t["blocks"]:
+                b["kv_off"] = off
+                off += b["kv2"].shape[0]
+                kv_ws.append(b.pop("kv2"))
+        self.kv_w = torch.cat(kv_ws, 0).contiguous()
+        self.kv_total = off
+        self.ctx = None
         self.ncfg = None
 
     # ------------------------------------------------------------------------------------------ context
@@ -153,17 +162,10 @@ class HipUNet:
             yield from blk["attns"]
 
     def set_context(self, ctx):
-        """ctx: [ncfg, 77, 2048] prompt embeddings ([neg, pos] under CFG).  Computes every attn2 K/V once."""
-        ctx = ctx.to(device=self.device, dtype=self.dtype).contiguous()
+        """ctx: [ncfg, 77, 2048] prompt embeddings ([neg, pos] under CFG).  Stored on device; every forward
+        projects it through all 70 attn2 to_k/to_v at once (one K/V pair serves every tile of the batch)."""
+        self.ctx = ctx.to(device=self.device, dtype=self.dtype).contiguous().reshape(-1, ctx.shape[-1])
         self.ncfg, self.Lk = ctx.shape[0], ctx.shape[1]
-        flat = ctx.reshape(-1, ctx.shape[-1])
-        kvs = []
-        for t in self._all_t2d():
-            for b in t["blocks"]:
-                kv = ops.gemm(flat, b["kv2"])  # [ncfg*77, 2C]
-                b["kv"] = kv
-                kvs.append(kv)
-        self.ctx_kv = kvs
 
     # ------------------------------------------------------------------------------------------ blocks
     def _resnet(self, r, x, B, H, Wd, temb, x2=None, C1=None):
@@ -196,10 +198,10 @@ class HipUNet:
             ops.gemm(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
             ops.layer_norm(h, *b["n2"], 1e-5, out=n)
             q = ops.gemm(n, b["q2"], out=qkv[:, :C], ldc=3 * C)
-            kv = b["kv"]
-            Lk = self.Lk
-            ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, 2 * C, 2 * C, C,
-                           HW * 3 * C, Lk * 2 * C, Lk * 2 * C, HW * C, kv_mod=self.ncfg, scale=0.125)
+            kv = self._kv[:, b["kv_off"]:]  # [ncfg*77, ...] view; K at +0, V at +C, row stride kv_total
+            Lk, ldkv = self.Lk, self.kv_total
+            ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, ldkv, ldkv, C,
+                           HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self.ncfg, scale=0.125)
             ops.gemm(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
             ops.layer_norm(h, *b["n3"], 1e-5, out=n)
             ff = ops.gemm(n, b["ff1"][0], bias=b["ff1"][1], act="geglu")
@@ -242,9 +244,10 @@ class HipUNet:
     def forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True):
         """x: NHWC [B*H*W, 4] (dtype); t: fp32 [B]; time_ids fp32 [B, 6]; text_embeds fp32 [B, 1280];
         cond: NHWC [B*H*W, 512] image latents (dtype) or None.  Returns eps NHWC [B*H*W, 4] (dtype)."""
-        assert self.ctx_kv is not None, "call set_context(prompt_embeds) first"
+        assert self.ctx is not None, "call set_context(prompt_embeds) first"
         assert B % self.ncfg == 0
         temb = self.embeddings(t, time_ids, text_embeds, B)
+        self._kv = ops.gemm(self.ctx, self.kv_w)  # [ncfg*77, sum 2C]: every attn2 K/V of this forward
         x0 = ops.conv_direct(x, *self.conv_in, B, H, Wd, 4, 3, 1, 1, out_dtype=self.dtype)
         if cond is not None and self.has_extras:
             feat = self._extras(x0, cond, B, H, Wd)

@@ -186,6 +186,12 @@ int fd_vae_sample_add_noise(const void* moments, const float* post_eps, const fl
 /* VaeImageProcessor.postprocess (:1451): uint8 = round(clamp(x/2 + 0.5, 0, 1) * 255). */
 int fd_postprocess_u8(const void* x, void* y, long long n, int dtype, void* stream);
 
+/* Tiled VAE / denoise-encoder seam blend (diffusers AutoencoderKL.blend_v/blend_h; FaithDiff
+ * Encoder.blend_v/blend_h, ext:150-162), in place on NHWC tile b from neighbour a (vertical: a above
+ * b; horizontal: a left of b); e = min(extent, overlapping dims). */
+int fd_blend_edge(const void* a, void* b, int Ha, int Wa, int Hb, int Wb, int C, int extent, int vertical, int dtype,
+                  void* stream);
+
 /* library / device checks */
 int fd_device_check(void);
 const char* fd_version(void);

@@ -125,7 +125,42 @@ class Decoder(nn.Module):
         return self.conv_out(F.silu(self.conv_norm_out(x)))
 
 
+def _blend_v(a, b, e):
+    e = min(a.shape[2], b.shape[2], e)
+    for y in range(e):
+        b[:, :, y, :] = a[:, :, -e + y, :] * (1 - y / e) + b[:, :, y, :] * (y / e)
+    return b
+
+
+def _blend_h(a, b, e):
+    e = min(a.shape[3], b.shape[3], e)
+    for x in range(e):
+        b[:, :, :, x] = a[:, :, :, -e + x] * (1 - x / e) + b[:, :, :, x] * (x / e)
+    return b
+
+
+def _tiled(x, fn, step, size, blend, limit):
+    """diffusers tiled_encode / tiled_decode skeleton (0.28): tiles every `step`, in-place blends in
+    row-major order, crop to `limit`."""
+    rows = []
+    for i in range(0, x.shape[2], step):
+        rows.append([fn(x[:, :, i:i + size, j:j + size]) for j in range(0, x.shape[3], step)])
+    out_rows = []
+    for i, row in enumerate(rows):
+        out = []
+        for j, tile in enumerate(row):
+            if i > 0:
+                tile = _blend_v(rows[i - 1][j], tile, blend)
+            if j > 0:
+                tile = _blend_h(row[j - 1], tile, blend)
+            out.append(tile[:, :, :limit, :limit])
+        out_rows.append(torch.cat(out, dim=3))
+    return torch.cat(out_rows, dim=2)
+
+
 class AutoencoderKL(nn.Module):
+    """diffusers AutoencoderKL (sdxl-vae-fp16-fix config); use_tiling -> tiled_encode / tiled_decode with
+    tile_sample_min_size = sample_size (1024), tile_latent_min_size = 128, overlap 0.25."""
     scaling_factor = 0.13025
 
     def __init__(self):
@@ -134,8 +169,16 @@ class AutoencoderKL(nn.Module):
         self.decoder = Decoder()
         self.quant_conv = nn.Conv2d(8, 8, 1)
         self.post_quant_conv = nn.Conv2d(4, 4, 1)
+        self.use_tiling = False
+        self.tile_sample_min_size = 1024
+        self.tile_latent_min_size = 128
+        self.tile_overlap_factor = 0.25
 
     def encode_moments(self, x):
+        if self.use_tiling and (x.shape[-1] > self.tile_sample_min_size or x.shape[-2] > self.tile_sample_min_size):
+            ts, tl, f = self.tile_sample_min_size, self.tile_latent_min_size, self.tile_overlap_factor
+            return _tiled(x, lambda t: self.quant_conv(self.encoder.encode(t)), int(ts * (1 - f)), ts, int(tl * f),
+                          tl - int(tl * f))
         return self.quant_conv(self.encoder.encode(x))
 
     def encode_sample(self, x, eps):
@@ -146,6 +189,10 @@ class AutoencoderKL(nn.Module):
         return mean + torch.exp(0.5 * logvar) * eps
 
     def decode(self, z):
+        if self.use_tiling and (z.shape[-1] > self.tile_latent_min_size or z.shape[-2] > self.tile_latent_min_size):
+            ts, tl, f = self.tile_sample_min_size, self.tile_latent_min_size, self.tile_overlap_factor
+            return _tiled(z, lambda t: self.decoder(self.post_quant_conv(t)), int(tl * (1 - f)), tl, int(ts * f),
+                          ts - int(ts * f))
         return self.decoder(self.post_quant_conv(z))
 
 
