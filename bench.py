@@ -12,9 +12,14 @@ images, no data-path collective), so `scaling` is "weak" and value = total steps
 with a barrier + synchronize on both sides, max over ranks).  The tile-sharded path for one large image
 (C3/C4, one all-gather per step) is FaithDiff/pipelines/tile_parallel.py, exercised by the tests.
 
-roofline: the unit is one denoise step captured as ONE hipGraph launch (UNet forward) plus three fused
-loop kernels; achieved = 14.217 TFLOP (analytic, fdhip.arch.unet_flops) / step time measured with HIP
-events on the launch stream; peak = 2500 TFLOP/s dense bf16 MFMA (MI355X_MICROARCH.md).
+roofline: the dominant kernel is the MFMA GEMM (gemm_kernel: every projection, FF and implicit-GEMM 3x3
+conv of the UNet, ~76% of a step).  achieved = its algorithmic FLOPs (2*M*N*K per launch, summed over the
+launches of one UNet forward) / the summed launch durations, each launch bracketed by HIP events on its
+launch stream in an instrumented (eager) forward after the timed region; peak = 2500 TFLOP/s dense bf16
+MFMA (MI355X_MICROARCH.md).  traffic = HBM bytes of the same launches from the committed rocprofv3 PMC
+pass (profiles/r01_gemm_traffic.json: 2*FETCH_SIZE + WRITE_SIZE, gfx950 correction), else null.
+"step_roofline" is the same ratio for the whole graph-replayed step (14.217 TFLOP analytic);
+"attention" and "vae_norm" report flash-attention MFMA TFLOP/s and VAE GroupNorm HBM GB/s the same way.
 cpu_baseline: the fp32 CPU oracle (the repo's restatement of the reference path) timed on this host for
 a bounded sample (1 denoise step of the same C2 tile).
 """
@@ -32,6 +37,54 @@ import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_HBM_GBS = 8000.0
+
+
+def event_pair_overhead_ms(n=64):
+    """Median elapsed time of an event pair with nothing between them, on a busy-then-idle stream: the
+    per-launch bias the probe subtracts (rocprofv3 --kernel-trace of the same run cross-checks it)."""
+    x = torch.empty(1 << 20, device="cuda")
+    ts = []
+    for _ in range(n):
+        x.mul_(1.0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        e1.record()
+        ts.append((e0, e1))
+    torch.cuda.synchronize()
+    v = sorted(a.elapsed_time(b) for a, b in ts)
+    return v[len(v) // 2]
+
+
+def probe(fn, reps=3):
+    """Run fn() `reps` times with the per-launch event probe on; per kind: (launches, FLOPs, bytes, ms),
+    averaged per call of fn, each launch's event time less the empty event-pair time."""
+    from fdhip import ops
+    bias = event_pair_overhead_ms()
+    rec = []
+    ops.set_probe(rec)
+    try:
+        for _ in range(reps):
+            fn()
+    finally:
+        ops.set_probe(None)
+    torch.cuda.synchronize()
+    agg = {}
+    for kind, fl, nb, e0, e1, *_ in rec:
+        a = agg.setdefault(kind, [0, 0.0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += fl
+        a[2] += nb
+        a[3] += max(e0.elapsed_time(e1) - bias, 1e-4)
+    return {k: (v[0] // reps, v[1] / reps, v[2] / reps, v[3] / reps) for k, v in agg.items()}
+
+
+def load_traffic():
+    path = os.path.join(ROOT, "profiles", "r01_gemm_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 
 
 def parse():
@@ -194,9 +247,11 @@ def main():
     for i in range(args.profile_steps):
         step(i)
     torch.cuda.synchronize()
+    # instrumented eager forwards (outside the timed region): per-kernel-family durations
+    kstats = probe(unet_fwd)
 
     # ---- VAE decode at the same size (ms), separately timed
-    vae_ms = None
+    vae_ms, vstats = None, {}
     if not args.no_vae:
         from fdhip.vae import HipDecoder
         vsd = arch.random_init(arch.vae_param_shapes(), seed=3, device=dev)
@@ -216,6 +271,7 @@ def main():
             torch.cuda.synchronize()
             times.append(e0.elapsed_time(e1))
         vae_ms = sorted(times)[1]
+        vstats = probe(lambda: dec.decode(z, 1, h, w), reps=2)
 
     steps_total = args.steps * world
     value = steps_total / t_max
@@ -223,6 +279,20 @@ def main():
     flops = arch.unet_flops(k, k, B)
     step_s = ev_ms / 1e3 / args.steps
     achieved = flops / step_s / 1e12
+    n_g, fl_g, _, ms_g = kstats["gemm"]
+    gemm_tf = fl_g / (ms_g / 1e3) / 1e12
+    tr = load_traffic()
+    traffic = None
+    if tr and tr.get("workload") == f"C2 {args.size}":
+        traffic = tr["hbm_bytes_per_forward"]
+    n_a, fl_a, _, ms_a = kstats["flash_attn"]
+    attn_tf = fl_a / (ms_a / 1e3) / 1e12
+    vae_norm = None
+    if "group_norm" in vstats:
+        n_n, _, nb_n, ms_n = vstats["group_norm"]
+        vae_norm = {"bound": "hbm", "achieved": round(nb_n / (ms_n / 1e3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": round(nb_n / (ms_n / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+                    "launches": n_n, "ms": round(ms_n, 3), "algorithmic_bytes": nb_n}
     result = {
         "metric": "denoise steps/sec @1024px 20-step + VAE decode ms",
         "value": round(value, 4), "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -234,10 +304,20 @@ def main():
                    "latent": [h, w], "parallelism": f"replicas x{world}"},
         "vae_decode_ms": None if vae_ms is None else round(vae_ms, 2),
         "vae_decode_tflops": None if vae_ms is None else round(arch.vae_decode_flops(h, w) / (vae_ms / 1e3) / 1e12, 1),
-        "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                     "kernel": "one denoise step (hipGraph UNet forward + 3 loop kernels)",
-                     "algorithmic_flops_per_step": flops, "event_ms_per_step": round(step_s * 1e3, 3)},
+        "roofline": {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(gemm_tf / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                     "kernel": "gemm_kernel (all MFMA GEMM + implicit-GEMM conv launches of one UNet forward)",
+                     "launches": n_g, "algorithmic_flops": fl_g, "kernel_ms_per_forward": round(ms_g, 3),
+                     "avg_launch_us": round(ms_g / n_g * 1e3, 2),
+                     "traffic_note": "HBM bytes per forward of these launches (PMC pass)" if traffic else
+                                     "no PMC pass committed for this workload"},
+        "step_roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
+                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                          "algorithmic_flops_per_step": flops, "event_ms_per_step": round(step_s * 1e3, 3)},
+        "attention": {"bound": "mfma", "achieved": round(attn_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                      "frac": round(attn_tf / PEAK_BF16_TFLOPS, 4), "launches": n_a, "ms": round(ms_a, 3)},
+        "vae_norm": vae_norm,
+        "kernel_ms_per_forward": {k: round(v[3], 3) for k, v in kstats.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

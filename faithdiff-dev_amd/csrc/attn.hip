@@ -17,17 +17,22 @@ template <typename T>
 __global__ void __launch_bounds__(256) flash_attn_d64_kernel(
     const T* __restrict__ Q, long long ldq, long long qbs, const T* __restrict__ K, long long ldk, long long kbs,
     const T* __restrict__ V, long long ldv, long long vbs, T* __restrict__ O, long long ldo, long long obs,
-    int Lq, int Lk, int kv_mod, float scale_log2) {
+    int Lq, int Lk, int kv_mod, float scale_log2, int heads, int swz) {
   typedef typename VecT<T>::v8 V8;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = blockIdx.y, b = blockIdx.z;
+  // 1-D grid; the q-blocks of one (batch, head) are contiguous after the XCD remap, so the head's K/V
+  // stream is fetched into one L2 instead of all eight.
+  const int nq = (Lq + 127) / 128;
+  const int pid = swz ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int qblk = pid % nq, bh = pid / nq;
+  const int h = bh % heads, b = bh / heads;
   const int kvb = kv_mod > 0 ? (b % kv_mod) : b;
   const T* Qb = Q + (long long)b * qbs + h * 64;
   const T* Kb = K + (long long)kvb * kbs + h * 64;
   const T* Vb = V + (long long)kvb * vbs + h * 64;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q0 = qblk * 128 + wave * 32;
   const int fr = lane & 15, fg = lane >> 4;
 
   // Q fragments (B operand): lane holds Q[q0 + qb*16 + fr][ds*32 + 8*fg .. +7]
@@ -199,12 +204,19 @@ extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const 
   if (!q || !k || !v || !o) return FD_ERR_ARG;
   if (batch <= 0 || heads <= 0 || Lq <= 0 || Lk <= 0 || kv_mod < 0) return FD_ERR_SHAPE;
   if ((ldq | ldk | ldv | ldo) & 7) return FD_ERR_SHAPE;
-  dim3 grid((Lq + 127) / 128, heads, batch), block(256);
+  static int swz = -1;
+  if (swz < 0) {
+    const char* e = getenv("FD_FLASH_SWZ");
+    swz = e ? atoi(e) : 1;
+  }
+  const long long nblk = (long long)((Lq + 127) / 128) * heads * batch;
+  if (nblk > 0x7fffffff) return FD_ERR_SHAPE;
+  dim3 grid((unsigned)nblk), block(256);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   FD_DISPATCH_T(dtype, hipLaunchKernelGGL(flash_attn_d64_kernel<T>, grid, block, 0, s, (const T*)q, ldq, qbs,
                                           (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk,
-                                          kv_mod, sl2));
+                                          kv_mod, sl2, heads, swz));
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

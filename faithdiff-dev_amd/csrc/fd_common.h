@@ -38,6 +38,14 @@ template <typename T> __device__ __forceinline__ void stf(void* p, long long i, 
   ((T*)p)[i] = (T)v;
 }
 
+// Workgroups are dealt round-robin to the 8 XCDs (b and b+8 share one; each XCD has its own 4 MiB L2).
+// Bijective remap giving XCD x the contiguous logical range [x*q + min(x, r), ...) of the nwg blocks, so
+// neighbouring logical blocks (same weight panel, same attention head) share an L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float quickgelu_f(float x) { return x / (1.0f + __expf(-1.702f * x)); }

@@ -33,8 +33,7 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int t
     tn = bid % tiles_n;
     return;
   }
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int pid = xcd_remap(bid, nwg);
   constexpr int GROUP_M = 4;
   const int group = pid / (GROUP_M * tiles_n);
   const int first_m = group * GROUP_M;

@@ -10,9 +10,12 @@
 #define GN_MAXC 2560
 
 static inline int gn_rows_per_chunk(int nimg, int HW) {
-  // ~512 partial blocks in total (fills the chip even at the 32x32 level), at most 512 chunks per image
+  // 256 chunks per image at most, chosen from HW alone: the per-(image, group) reduction order -- and so
+  // every bit of the result -- does not depend on how many images share the launch (tile batching, CFG
+  // rows, tile-parallel sharding all give identical outputs).  512+ blocks at the UNet's B >= 2.
+  (void)nimg;
   int r = 1;
-  while ((long long)nimg * ((HW + r - 1) / r) > 512 || (HW + r - 1) / r > 512) r *= 2;
+  while ((HW + r - 1) / r > 256) r *= 2;
   return r;
 }
 

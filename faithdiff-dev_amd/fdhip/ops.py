@@ -45,6 +45,39 @@ def pack_geglu(w, b):
 
 
 # --------------------------------------------------------------------------------------- GEMM / conv
+_probe = None
+
+
+def set_probe(records):
+    """Measurement hook (bench.py's roofline leg, never on in timed steps): while ``records`` is a list,
+    every GEMM / conv (fd_gemm), flash-attention, GroupNorm and LayerNorm launch appends
+    (kind, algorithmic FLOPs, algorithmic HBM bytes, start event, end event) recorded on the launch stream.
+    None turns it off."""
+    global _probe
+    _probe = records
+
+
+def _timed(kind, flops, nbytes, launch, label=None):
+    if _probe is None:
+        launch()
+        return
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    launch()
+    e1.record()
+    _probe.append((kind, float(flops), float(nbytes), e0, e1) + ((label,) if label else ()))
+
+
+def _launch_gemm(p, what):
+    flops = 2.0 * p.M * p.N * p.K * max(p.batch, 1)
+    label = None
+    if _probe is not None:
+        act = {v: k for k, v in L.ACT.items()}[p.act]
+        label = (f"{'conv' if p.conv else 'gemm'} M={p.M} N={p.N} K={p.K} b={p.batch} {act}"
+                 f"{' up' if p.upsample else ''}{' cat' if p.A2 else ''}{' res' if p.residual else ''}")
+    _timed("gemm", flops, 0.0, lambda: L.check(L.load().fd_gemm(ctypes.byref(p), L.stream()), what), label)
+
+
 def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=1, alpha=1.0, act="none",
          out_dtype=None, batch=1, M=None, N=None, K=None, lda=None, ldw=None, ldc=None, ldr=None,
          stride_a=0, stride_w=0, stride_c=0, stride_r=0):
@@ -76,7 +109,7 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
     p.act = L.ACT[act]
     p.dtype = L.dtype_code(a.dtype)
     p.out_dtype = L.dtype_code(odt)
-    L.check(L.load().fd_gemm(ctypes.byref(p), L.stream()), "fd_gemm")
+    _launch_gemm(p, "fd_gemm")
     return out
 
 
@@ -113,7 +146,7 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
     p.conv, p.nimg, p.Hin, p.Win, p.Cin = 1, nimg, H, W, Cin
     p.Hout, p.Wout, p.stride, p.pad, p.upsample = Hout, Wout, stride, pad, int(upsample)
     p.A2 = x2.data_ptr() if x2 is not None else None
-    L.check(L.load().fd_gemm(ctypes.byref(p), L.stream()), "fd_gemm(conv)")
+    _launch_gemm(p, "fd_gemm(conv)")
     return out
 
 
@@ -136,8 +169,9 @@ def group_norm(x, gamma, beta, nimg, HW, C, groups=32, eps=1e-5, silu=False, out
         out = torch.empty_like(x)
     nb = L.load().fd_group_norm_ws_bytes(nimg, HW, C, groups)
     ws = _gn_ws(nb, x.device)
-    L.check(L.load().fd_group_norm(L.ptr(x), L.ptr(out), L.ptr(gamma), L.ptr(beta), nimg, HW, C, groups, eps,
-                                   int(silu), L.dtype_code(x.dtype), L.ptr(ws), L.stream()), "fd_group_norm")
+    _timed("group_norm", 0, 2.0 * nimg * HW * C * x.element_size(), lambda: L.check(
+        L.load().fd_group_norm(L.ptr(x), L.ptr(out), L.ptr(gamma), L.ptr(beta), nimg, HW, C, groups, eps, int(silu),
+                               L.dtype_code(x.dtype), L.ptr(ws), L.stream()), "fd_group_norm"))
     return out
 
 
@@ -146,17 +180,20 @@ def layer_norm(x, gamma, beta, eps=1e-5, out=None, M=None, ldx=None):
     M = x.numel() // x.shape[-1] if M is None else M
     if out is None:
         out = torch.empty((M, C), dtype=x.dtype, device=x.device)
-    L.check(L.load().fd_layer_norm(L.ptr(x), x.stride(-2) if ldx is None else ldx, L.ptr(out), out.stride(-2),
-                                   L.ptr(gamma), L.ptr(beta), M, C, eps, L.dtype_code(x.dtype), L.stream()),
-            "fd_layer_norm")
+    _timed("layer_norm", 0, 2.0 * M * C * x.element_size(), lambda: L.check(
+        L.load().fd_layer_norm(L.ptr(x), x.stride(-2) if ldx is None else ldx, L.ptr(out), out.stride(-2),
+                               L.ptr(gamma), L.ptr(beta), M, C, eps, L.dtype_code(x.dtype), L.stream()),
+        "fd_layer_norm"))
     return out
 
 
 # --------------------------------------------------------------------------------------- attention
 def flash_attn(q, k, v, out, batch, heads, Lq, Lk, ldq, ldk, ldv, ldo, qbs, kbs, vbs, obs, kv_mod=0, scale=0.125):
-    L.check(L.load().fd_flash_attn(L.ptr(q), ldq, qbs, L.ptr(k), ldk, kbs, L.ptr(v), ldv, vbs, L.ptr(out), ldo, obs,
-                                   batch, heads, Lq, Lk, kv_mod, scale, L.dtype_code(q.dtype), L.stream()),
-            "fd_flash_attn")
+    _timed("flash_attn", 4.0 * batch * heads * Lq * Lk * 64, 0, label=f"flash b={batch} h={heads} Lq={Lq} Lk={Lk}",
+           launch=lambda: L.check(
+        L.load().fd_flash_attn(L.ptr(q), ldq, qbs, L.ptr(k), ldk, kbs, L.ptr(v), ldv, vbs, L.ptr(out), ldo, obs,
+                               batch, heads, Lq, Lk, kv_mod, scale, L.dtype_code(q.dtype), L.stream()),
+        "fd_flash_attn"))
     return out
 
 

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Parse the two PMC passes of scripts/pmc.sh into profiles/r01_gemm_traffic.json.
+
+Windows are found with the fd_postprocess_u8 marker kernels: [m1, m2) holds the 1 GiB calibration copy,
+[m2, m3) the measured UNet forward.  Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE on gfx950 reports
+half the bytes of a 16-B/lane streaming read (x2 correction); WRITE_SIZE is exact for 16-B stores.  The
+calibration copy gives the counters' unit (bytes per count) on this box, checked against that rule."""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PMC = os.path.join(ROOT, "gpurun_out", "pmc")
+
+
+def load(counter):
+    files = glob.glob(os.path.join(PMC, counter, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        sys.exit(f"no counter_collection.csv for {counter}")
+    rows = {}
+    with open(files[0]) as f:
+        for r in csv.DictReader(f):
+            did = int(r["Dispatch_Id"])
+            name = r["Kernel_Name"]
+            v = float(r["Counter_Value"])
+            if did in rows:
+                rows[did][1] += v
+            else:
+                rows[did] = [name, v]
+    return [(d, rows[d][0], rows[d][1]) for d in sorted(rows)]
+
+
+def windows(disp):
+    marks = [i for i, (_, n, _) in enumerate(disp) if "postprocess_kernel" in n]
+    m1, m2, m3 = marks[-3:]
+    return disp[m1 + 1:m2], disp[m2 + 1:m3]
+
+
+def main():
+    meta = json.load(open(os.path.join(PMC, "meta.json")))
+    res = {"workload": meta["workload"], "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+           "--kernel-trace, csv; scripts/pmc.sh + scripts/pmc_parse.py"}
+    per = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        calib, fwd = windows(load(c))
+        cal = sum(v for _, _, v in calib)
+        known = meta["calib_bytes_read"] if c == "FETCH_SIZE" else meta["calib_bytes_written"]
+        per[c] = {"calib_counter": cal, "bytes_per_count_measured": known / cal if cal else None,
+                  "gemm": sum(v for _, n, v in fwd if "gemm_kernel" in n),
+                  "flash": sum(v for _, n, v in fwd if "flash_attn" in n),
+                  "all": sum(v for _, n, v in fwd), "n_gemm": sum(1 for _, n, _ in fwd if "gemm_kernel" in n)}
+    # unit: rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB; gfx950 FETCH_SIZE counts half of 16-B reads
+    f, w = per["FETCH_SIZE"], per["WRITE_SIZE"]
+    rd = f["gemm"] * 1024 * 2
+    wr = w["gemm"] * 1024
+    res.update({"counters": per,
+                "gemm_launches": f["n_gemm"], "expected_gemm_launches": meta["launches_per_forward"].get("gemm"),
+                "gemm_read_bytes": rd, "gemm_write_bytes": wr, "hbm_bytes_per_forward": rd + wr,
+                "forward_all_kernels_bytes": f["all"] * 1024 * 2 + w["all"] * 1024,
+                "flash_bytes": f["flash"] * 1024 * 2 + w["flash"] * 1024,
+                "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB; "
+                              "calibration copy's measured bytes/count recorded for comparison"})
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    out = os.path.join(ROOT, "gpurun_out", "pmc", "r01_gemm_traffic.json")
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
