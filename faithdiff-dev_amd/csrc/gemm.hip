@@ -43,8 +43,13 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int t
   tn = in_group / gsz;
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, bool CONV, bool GEGLU, typename TO>
-__global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int swz) {
+// KS = 2: intra-workgroup split of every 64-deep K step.  Eight waves: waves 0-3 (the loaders) take the
+// first 32 of each K step, waves 4-7 the second 32, each over the same wave tile; the halves are summed
+// through LDS before the epilogue.  Same LDS traffic and tile shape, but two waves per SIMD, so one
+// wave's LDS fragment reads overlap the other's MFMAs (with one 4-wave workgroup per CU -- 256-tile
+// launches -- the single wave per SIMD otherwise serialises them).
+template <typename T, int BM, int BN, int WM, int WN, int NS, bool CONV, bool GEGLU, typename TO, int KS>
+__global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, int swz) {
   typedef typename VecT<T>::v8 V8;
   constexpr int WAVES_N = BN / WN;
   constexpr int MT = WM / 16, NT = WN / 16;
@@ -56,13 +61,21 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
   static_assert(NS >= 2 && NS <= 4 && (NS - 2) * PER < 64, "pipeline depth");
   constexpr int BNO = GEGLU ? BN / 2 : BN;   // output columns of the tile
   constexpr int LDE = BNO + 4;               // fp32 epilogue staging row stride (16-B aligned rows)
-  constexpr int SMEM = (NS * STAGE > BM * LDE * 4) ? NS * STAGE : BM * LDE * 4;
+  constexpr int EPB = (KS == 2 && BN + 4 > LDE) ? BM * (BN + 4) * 4 : BM * LDE * 4;
+  constexpr int SMEM = (NS * STAGE > EPB) ? NS * STAGE : EPB;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
+  constexpr int NTHR = 256 * KS;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kh = wave_all >> 2;     // K half (KS = 2), 0 otherwise
+  const int wave = wave_all & 3;    // position in the 4-wave tile grid / loader index
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  // swz bits 4-5: diagnostic mode (FD_GEMM_MODE, benchmarks only): 1 = operand loads only (no LDS reads,
+  // no MFMA), 2 = LDS reads + MFMA only (no global loads).  0 in every product launch.
+  const int mode = swz >> 4;
+  swz &= 1;
   int tm, tn;
   tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, swz, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
@@ -112,6 +125,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
   const T* __restrict__ A2 = (const T*)p.A2;
 
   auto stage = [&](int kt, int buf) {
+    if (mode == 2 || kh) return;  // waves 4-7 (KS = 2) only compute
     const int k0 = kt * 64;
     unsigned char* sa = smem + buf * STAGE;
     if (CONV) {
@@ -164,8 +178,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
     if (kt + NS - 1 < nk) stage(kt + NS - 1, (kt + NS - 1) % NS);
     const unsigned char* sa = smem + (kt % NS) * STAGE;
     const unsigned char* sb = sa + A_BYTES;
+    if (mode == 1) continue;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kq = 0; kq < 2 / KS; ++kq) {
+      const int kk = KS == 2 ? kh : kq;
       V8 af[MT], bfr[NT];
       const int ch = kk * 4 + fg;
 #pragma unroll
@@ -190,6 +206,30 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
   __syncthreads();  // every wave is done reading the operand ring
   float* ep = (float*)smem;
   const float alpha = p.alpha;
+  if (KS == 2) {  // fold the second K half into the first (fixed order: bitwise reproducible)
+    constexpr int LDP = BN + 4;
+    if (kh) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ep[(wm * WM + mi * 16 + fg * 4 + j) * LDP + wn * WN + ni * 16 + fr] = acc[mi][ni][j];
+    }
+    __syncthreads();
+    if (!kh) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[mi][ni][j] += ep[(wm * WM + mi * 16 + fg * 4 + j) * LDP + wn * WN + ni * 16 + fr];
+    }
+    __syncthreads();
+  }
+  if (!kh) {
   if (GEGLU) {
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
@@ -224,6 +264,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
         }
       }
   }
+  }  // !kh
   __syncthreads();
 
   // ---- phase 2: whole-row 16-B vector residual loads and stores (8 outputs per thread per step)
@@ -234,7 +275,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
   const bool vec = (Nout % 8 == 0) && (p.ldc % 8 == 0) && ((((unsigned long long)C) & 15) == 0) &&
                    (!R || ((p.ldr % 8 == 0) && ((((unsigned long long)R) & 15) == 0)));
   constexpr int VPR = BNO / 8;
-  for (int e = tid; e < BM * VPR; e += 256) {
+  for (int e = tid; e < BM * VPR; e += NTHR) {
     const int r = e / VPR, cv = e - (e / VPR) * VPR;
     const int m = m0 + r, n = n0o + cv * 8;
     if (m >= M || n >= Nout) continue;
@@ -264,20 +305,20 @@ __global__ void __launch_bounds__(256) gemm_kernel(const fd_gemm_params p, int s
   }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, typename TO>
+template <typename T, int BM, int BN, int WM, int WN, int NS, typename TO, int KS = 1>
 static int launch_cfg(const fd_gemm_params* p, hipStream_t s, int swz) {
   const int tiles = ((p->M + BM - 1) / BM) * ((p->N + BN - 1) / BN);
-  dim3 grid(tiles, 1, p->batch > 0 ? p->batch : 1), block(256);
+  dim3 grid(tiles, 1, p->batch > 0 ? p->batch : 1), block(256 * KS);
   if (p->conv) {
     if (p->act == FD_ACT_GEGLU) return FD_ERR_ARG;
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, true, false, TO>), grid, block, 0, s, *p, swz);
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, true, false, TO, KS>), grid, block, 0, s, *p, swz);
   } else if (p->act == FD_ACT_GEGLU) {
     if constexpr (WN % 32 == 0)
-      hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, true, TO>), grid, block, 0, s, *p, swz);
+      hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, true, TO, KS>), grid, block, 0, s, *p, swz);
     else
       return FD_ERR_ARG;
   } else {
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, false, TO>), grid, block, 0, s, *p, swz);
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, false, TO, KS>), grid, block, 0, s, *p, swz);
   }
   FD_LAUNCH_CHECK();
   return FD_OK;
@@ -285,6 +326,8 @@ static int launch_cfg(const fd_gemm_params* p, hipStream_t s, int swz) {
 
 // Tile choice: cost ~ ceil(tiles / (256 CUs x resident WGs per CU)) x per-tile time; a smaller tile is
 // worth it only when it removes a partial wave.  Relative per-tile efficiencies are estimates.
+// (256x128 / 128x256 tiles with KS = 2 were measured 1.2-2x slower on every UNet shape: 2 waves/SIMD
+//  at 204 VGPRs and 1 WG/CU cannot hide the fragment-read latency that 4 waves/SIMD of 128x128 do.)
 enum { CFG_128x128, CFG_64x160, CFG_128x64, CFG_64x64, CFG_COUNT };
 static const int CFG_BM[] = {128, 64, 128, 64}, CFG_BN[] = {128, 160, 64, 64};
 
@@ -309,14 +352,25 @@ static int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
 }
-static int g_cfg = -2, g_ns = -1, g_swz = -1;
+static int g_cfg = -2, g_ns = -1, g_swz = -1, g_ks = 0;
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
-static int dispatch_ns(const fd_gemm_params* p, hipStream_t s, int ns, int swz) {
+static int dispatch_ns(const fd_gemm_params* p, hipStream_t s, int ns, int ks, int swz) {
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr bool NS3 = 3 * STAGE <= 160 * 1024, NS4 = 4 * STAGE <= 160 * 1024;
+  if (ns == 4 && !NS4) ns = NS3 ? 3 : 2;
+  if (ns == 3 && !NS3) ns = 2;
   if constexpr (std::is_same<T, TO>::value) {
+    if (ks == 2) {
+      if (ns == 2) return launch_cfg<T, BM, BN, WM, WN, 2, TO, 2>(p, s, swz);
+      if constexpr (NS3) if (ns == 3) return launch_cfg<T, BM, BN, WM, WN, 3, TO, 2>(p, s, swz);
+      if constexpr (NS4) return launch_cfg<T, BM, BN, WM, WN, 4, TO, 2>(p, s, swz);
+      return FD_ERR_ARG;
+    }
     if (ns == 2) return launch_cfg<T, BM, BN, WM, WN, 2, TO>(p, s, swz);
-    if (ns == 3) return launch_cfg<T, BM, BN, WM, WN, 3, TO>(p, s, swz);
-    return launch_cfg<T, BM, BN, WM, WN, 4, TO>(p, s, swz);
+    if constexpr (NS3) if (ns == 3) return launch_cfg<T, BM, BN, WM, WN, 3, TO>(p, s, swz);
+    if constexpr (NS4) return launch_cfg<T, BM, BN, WM, WN, 4, TO>(p, s, swz);
+    return FD_ERR_ARG;
   } else {
     return launch_cfg<T, BM, BN, WM, WN, 2, TO>(p, s, swz);
   }
@@ -327,20 +381,25 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
   if (g_cfg == -2) {
     g_cfg = env_int("FD_GEMM_CFG", -1);
     g_ns = env_int("FD_GEMM_NS", 0);
-    g_swz = env_int("FD_GEMM_SWZ", 1);
+    g_ks = env_int("FD_GEMM_KS", 0);
+    g_swz = env_int("FD_GEMM_SWZ", 1) | (env_int("FD_GEMM_MODE", 0) << 4);
   }
   int cfg = g_cfg >= 0 && g_cfg < CFG_COUNT ? g_cfg : pick_cfg(p);
   // ring depth: 4 stages (1 WG/CU) pays only on long K when one wave of tiles covers the launch; 2 stages
   // (2-3 co-resident WGs/CU) otherwise (scripts/gemm_sweep.py + in-situ traces)
   const long long tiles = (long long)(p->batch > 0 ? p->batch : 1) * ((p->M + CFG_BM[cfg] - 1) / CFG_BM[cfg]) *
                           ((p->N + CFG_BN[cfg] - 1) / CFG_BN[cfg]);
-  const int ns = g_ns ? g_ns : ((p->K >= 4096 && tiles <= 256) ? 4 : 2);
+  // KS = 2 (8 waves, intra-WG split of each K step) measured >= KS = 1 on every UNet shape
+  // (scripts/gemm_ks.sh: 2048x1280x5120 60 -> 42 us); the 4-deep ring pays whenever one wave of tiles
+  // covers the launch (one WG per CU either way).
+  const int ns = g_ns ? g_ns : ((tiles <= 256 && p->K >= 512) ? 4 : 2);
+  const int ks = g_ks ? g_ks : 2;
   if (p->act == FD_ACT_GEGLU && cfg == CFG_64x160) cfg = CFG_128x128;
   switch (cfg) {
-    case CFG_128x128: return dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, g_swz);
-    case CFG_64x160: return dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, g_swz);
-    case CFG_128x64: return dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, g_swz);
-    default: return dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, g_swz);
+    case CFG_128x128: return dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, ks, g_swz);
+    case CFG_64x160: return dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, ks, g_swz);
+    case CFG_128x64: return dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, ks, g_swz);
+    default: return dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, ks, g_swz);
   }
 }
 
