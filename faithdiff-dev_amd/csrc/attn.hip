@@ -1,8 +1,8 @@
 // Attention kernels for gfx950.
 //
 // flash_attn_d64: head_dim 64 flash attention (SDPA replacement for the 140 attn1/attn2 calls of a
-// UNet forward).  One workgroup = 4 waves = 128 queries of one (batch, head); each wave owns 32
-// queries.  K/V tiles of 64 keys are staged by global_load_lds into a double buffer.  The score
+// UNet forward).  One workgroup = NWV waves (4 by default = 128 queries; 2-wave workgroups measured
+// no faster at Lq = 1024 and 10 % slower at 4096) of one (batch, head); each wave owns 32 queries.  K/V tiles of 64 keys are staged by global_load_lds into a double buffer.  The score
 // tile is computed transposed, S^T = K Q^T (A = K rows from LDS, B = Q fragments held in VGPRs),
 // so each lane owns one query column: the row max needs only two cross-lane shuffles, and the
 // accumulator, packed to bf16/f16 in registers, is directly the B operand of O^T = V^T P^T (guide
@@ -13,8 +13,8 @@
 // softmax_rows: fp32 row softmax for the single-head d=512 VAE mid attention (GEMM + softmax + GEMM).
 #include "fd_common.h"
 
-template <typename T>
-__global__ void __launch_bounds__(256) flash_attn_d64_kernel(
+template <typename T, int NWV>
+__global__ void __launch_bounds__(64 * NWV) flash_attn_d64_kernel(
     const T* __restrict__ Q, long long ldq, long long qbs, const T* __restrict__ K, long long ldk, long long kbs,
     const T* __restrict__ V, long long ldv, long long vbs, T* __restrict__ O, long long ldo, long long obs,
     int Lq, int Lk, int kv_mod, float scale_log2, int heads, int swz) {
@@ -24,7 +24,8 @@ __global__ void __launch_bounds__(256) flash_attn_d64_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // 1-D grid; the q-blocks of one (batch, head) are contiguous after the XCD remap, so the head's K/V
   // stream is fetched into one L2 instead of all eight.
-  const int nq = (Lq + 127) / 128;
+  constexpr int QB = 32 * NWV;  // queries per workgroup
+  const int nq = (Lq + QB - 1) / QB;
   const int pid = swz ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int qblk = pid % nq, bh = pid / nq;
   const int h = bh % heads, b = bh / heads;
@@ -32,7 +33,7 @@ __global__ void __launch_bounds__(256) flash_attn_d64_kernel(
   const T* Qb = Q + (long long)b * qbs + h * 64;
   const T* Kb = K + (long long)kvb * kbs + h * 64;
   const T* Vb = V + (long long)kvb * vbs + h * 64;
-  const int q0 = qblk * 128 + wave * 32;
+  const int q0 = qblk * QB + wave * 32;
   const int fr = lane & 15, fg = lane >> 4;
 
   // Q fragments (B operand): lane holds Q[q0 + qb*16 + fr][ds*32 + 8*fg .. +7]
@@ -50,16 +51,16 @@ __global__ void __launch_bounds__(256) flash_attn_d64_kernel(
     unsigned char* sk = smem + buf * 16384;
     unsigned char* sv = sk + 8192;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = (i * 4 + wave) * 8 + lrow;
+    for (int i = 0; i < 8 / NWV; ++i) {
+      const int row = (i * NWV + wave) * 8 + lrow;
       int key = t * 64 + row;
       key = key < Lk ? key : Lk - 1;
       const int ck = slot ^ ((row >> 1) & 7);
       const int cv = slot ^ (((row >> 1) & 3) << 1);
       __builtin_amdgcn_global_load_lds((const void*)(Kb + (long long)key * ldk + ck * 8),
-                                       LDS_PTR(sk + (i * 4 + wave) * 1024), 16, 0, 0);
+                                       LDS_PTR(sk + (i * NWV + wave) * 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const void*)(Vb + (long long)key * ldv + cv * 8),
-                                       LDS_PTR(sv + (i * 4 + wave) * 1024), 16, 0, 0);
+                                       LDS_PTR(sv + (i * NWV + wave) * 1024), 16, 0, 0);
     }
   };
 
@@ -204,19 +205,28 @@ extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const 
   if (!q || !k || !v || !o) return FD_ERR_ARG;
   if (batch <= 0 || heads <= 0 || Lq <= 0 || Lk <= 0 || kv_mod < 0) return FD_ERR_SHAPE;
   if ((ldq | ldk | ldv | ldo) & 7) return FD_ERR_SHAPE;
-  static int swz = -1;
+  static int swz = -1, nwv = 0;
   if (swz < 0) {
     const char* e = getenv("FD_FLASH_SWZ");
     swz = e ? atoi(e) : 1;
+    e = getenv("FD_FLASH_WAVES");  // 4 (128 queries per workgroup, default) or 2 (64)
+    nwv = (e && atoi(e) == 2) ? 2 : 4;
   }
-  const long long nblk = (long long)((Lq + 127) / 128) * heads * batch;
+  const int QB = 32 * nwv;
+  const long long nblk = (long long)((Lq + QB - 1) / QB) * heads * batch;
   if (nblk > 0x7fffffff) return FD_ERR_SHAPE;
-  dim3 grid((unsigned)nblk), block(256);
+  dim3 grid((unsigned)nblk), block(64 * nwv);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(flash_attn_d64_kernel<T>, grid, block, 0, s, (const T*)q, ldq, qbs,
-                                          (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk,
-                                          kv_mod, sl2, heads, swz));
+  if (nwv == 4) {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, 4>), grid, block, 0, s, (const T*)q, ldq, qbs,
+                                            (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk,
+                                            kv_mod, sl2, heads, swz));
+  } else {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, 2>), grid, block, 0, s, (const T*)q, ldq, qbs,
+                                            (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk,
+                                            kv_mod, sl2, heads, swz));
+  }
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

@@ -55,8 +55,10 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   constexpr int MT = WM / 16, NT = WN / 16;
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int A_INSTR = BM / 32, B_INSTR = BN / 32;
-  constexpr int PER = A_INSTR + B_INSTR;  // global_load_lds per lane per pipeline stage
+  // loader waves: all eight under KS = 2 when both panels split into 64-row groups, else waves 0-3
+  constexpr int NL = (KS == 2 && BM % 64 == 0 && BN % 64 == 0) ? 8 : 4;
+  constexpr int A_INSTR = BM / (8 * NL), B_INSTR = BN / (8 * NL);
+  constexpr int PER = A_INSTR + B_INSTR;  // global_load_lds per loader lane per pipeline stage
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves");
   static_assert(NS >= 2 && NS <= 4 && (NS - 2) * PER < 64, "pipeline depth");
   constexpr int BNO = GEGLU ? BN / 2 : BN;   // output columns of the tile
@@ -71,6 +73,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   const int kh = wave_all >> 2;     // K half (KS = 2), 0 otherwise
   const int wave = wave_all & 3;    // position in the 4-wave tile grid / loader index
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int lw = NL == 8 ? wave_all : wave;  // loader index
   const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
   // swz bits 4-5: diagnostic mode (FD_GEMM_MODE, benchmarks only): 1 = operand loads only (no LDS reads,
   // no MFMA), 2 = LDS reads + MFMA only (no global loads).  0 in every product launch.
@@ -92,7 +95,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   bool a_ok[A_INSTR];
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
-    const int row = (i * 4 + wave) * 8 + lrow;
+    const int row = (i * NL + lw) * 8 + lrow;
     const int m = m0 + row;
     a_ok[i] = m < M;
     const int mm = m < M ? m : M - 1;
@@ -115,7 +118,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   const T* b_row[B_INSTR];
 #pragma unroll
   for (int i = 0; i < B_INSTR; ++i) {
-    const int row = (i * 4 + wave) * 8 + lrow;
+    const int row = (i * NL + lw) * 8 + lrow;
     const int n = n0 + row;
     b_row[i] = Bw + (long long)(n < N ? n : N - 1) * p.ldb + (slot ^ ((row >> 1) & 7)) * 8;
   }
@@ -125,7 +128,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   const T* __restrict__ A2 = (const T*)p.A2;
 
   auto stage = [&](int kt, int buf) {
-    if (mode == 2 || kh) return;  // waves 4-7 (KS = 2) only compute
+    if (mode == 2 || (NL == 4 && kh)) return;  // waves 4-7 only compute unless all eight load
     const int k0 = kt * 64;
     unsigned char* sa = smem + buf * STAGE;
     if (CONV) {
@@ -142,17 +145,17 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
         const T* src = second ? (A2 + pix * (p.Cin - C1) + (c0 - C1) + a_chunk[i] * 8)
                               : (A + pix * p.lda + c0 + a_chunk[i] * 8);
         const void* s = ok ? (const void*)src : (const void*)g_zero_page;
-        __builtin_amdgcn_global_load_lds(s, LDS_PTR(sa + (i * 4 + wave) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(s, LDS_PTR(sa + (i * NL + lw) * 1024), 16, 0, 0);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A_INSTR; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(a_row[i] + k0), LDS_PTR(sa + (i * 4 + wave) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(a_row[i] + k0), LDS_PTR(sa + (i * NL + lw) * 1024), 16, 0, 0);
     }
     unsigned char* sb = sa + A_BYTES;
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (i * 4 + wave) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (i * NL + lw) * 1024), 16, 0, 0);
   };
 
   f32x4 acc[MT][NT];
@@ -328,15 +331,15 @@ static int launch_cfg(const fd_gemm_params* p, hipStream_t s, int swz) {
 // worth it only when it removes a partial wave.  Relative per-tile efficiencies are estimates.
 // (256x128 / 128x256 tiles with KS = 2 were measured 1.2-2x slower on every UNet shape: 2 waves/SIMD
 //  at 204 VGPRs and 1 WG/CU cannot hide the fragment-read latency that 4 waves/SIMD of 128x128 do.)
-enum { CFG_128x128, CFG_64x160, CFG_128x64, CFG_64x64, CFG_COUNT };
-static const int CFG_BM[] = {128, 64, 128, 64}, CFG_BN[] = {128, 160, 64, 64};
+enum { CFG_128x128, CFG_64x160, CFG_128x64, CFG_64x64, CFG_256x128, CFG_AUTO_COUNT = CFG_256x128, CFG_COUNT };
+static const int CFG_BM[] = {128, 64, 128, 64, 256}, CFG_BN[] = {128, 160, 64, 64, 128};
 
 static int pick_cfg(const fd_gemm_params* p) {
   const long long b = p->batch > 0 ? p->batch : 1;
-  const double eff[] = {1.00, 0.92, 0.85, 0.60};
+  const double eff[] = {1.00, 0.92, 0.85, 0.60, 1.0};
   int best = CFG_128x128;
   double bestc = 1e30;
-  for (int c = 0; c < CFG_COUNT; ++c) {
+  for (int c = 0; c < CFG_AUTO_COUNT; ++c) {
     if (p->act == FD_ACT_GEGLU && c == CFG_64x160) continue;
     const long long tiles = b * ((p->M + CFG_BM[c] - 1) / CFG_BM[c]) * ((p->N + CFG_BN[c] - 1) / CFG_BN[c]);
     const long long waves = (tiles + 255) / 256;
@@ -399,6 +402,7 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
     case CFG_128x128: return dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, ks, g_swz);
     case CFG_64x160: return dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, ks, g_swz);
     case CFG_128x64: return dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, ks, g_swz);
+    case CFG_256x128: return dispatch_ns<T, TO, 256, 128, 128, 64>(p, s, ns, ks, g_swz);
     default: return dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, ks, g_swz);
   }
 }

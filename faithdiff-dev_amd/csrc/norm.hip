@@ -1,10 +1,10 @@
 // GroupNorm (+ fused SiLU) and LayerNorm for NHWC activations, fp32 statistics.  HBM-bound.
 //
-// GroupNorm runs as two launches so that a (batch, group) reduction of up to 16384 x 80 elements is
+// GroupNorm runs as three launches so that a (batch, group) reduction of up to 16384 x 80 elements is
 // spread over the whole chip: (1) gn_partial: one block per (image, row-chunk) reads its rows once,
-// coalesced (16-B vectors along C), and writes per-group (sum, sumsq) partials; (2) gn_apply: every
-// block folds the partials of its image in fp64 (Chan-free E[x^2]-E[x]^2 in double), builds per-channel
-// scale/shift in LDS and streams its rows: y = x*scale[c] + shift[c] (+ SiLU), one FMA per element.
+// coalesced (16-B vectors along C), and writes per-group (sum, sumsq) partials; (2) gn_finalize: one
+// block per image folds them in fp64 (E[x^2]-E[x]^2 in double) into (mean, rstd); (3) gn_apply: every
+// block builds per-channel scale/shift in LDS and streams its rows: y = x*scale[c] + shift[c] (+ SiLU).
 #include "fd_common.h"
 
 #define GN_MAXC 2560
@@ -80,43 +80,52 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ x
   }
 }
 
+// fold the per-chunk partials of one image into per-group (mean, rstd): SUB = 256/groups threads per
+// group, each a strided share of the chunks (fixed order -> bitwise reproducible), then a shuffle tree in
+// fp64.  Once per (image, group) -- the apply blocks only read the result.
+__global__ void __launch_bounds__(256) gn_finalize_kernel(const float2* __restrict__ part, float2* __restrict__ stats,
+                                                          int HW, int C, int groups, int nchunks, float eps) {
+  const int img = blockIdx.x, t = threadIdx.x;
+  const int cpg = C / groups;
+  const int SUB = 256 / groups;  // groups <= 64 -> SUB >= 4 (power of two for groups in {32, 64})
+  const int g = t / SUB, j = t % SUB;
+  double s = 0.0, q = 0.0;
+  if (g < groups) {
+    const float2* p = part + (long long)img * nchunks * groups + g;
+    for (int c = j; c < nchunks; c += SUB) {
+      const float2 v = p[(long long)c * groups];
+      s += v.x;
+      q += v.y;
+    }
+  }
+  for (int o = SUB / 2; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    q += __shfl_xor(q, o, 64);
+  }
+  if (g < groups && j == 0) {
+    const double n = (double)HW * cpg;
+    const double mean = s / n;
+    double var = q / n - mean * mean;
+    if (var < 0) var = 0;
+    stats[img * groups + g] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+  }
+}
+
 template <typename T, int NV>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                       const float2* __restrict__ part, const float* __restrict__ gamma,
+                                                       const float2* __restrict__ stats, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, int HW, int C, int groups,
-                                                       int nchunks, int rows_per_block, float eps, int silu) {
+                                                       int rows_per_block, int silu) {
   typedef typename VecT<T>::v8 V8;
   __shared__ float sc[GN_MAXC], sh[GN_MAXC];
   __shared__ float mean_s[64], rstd_s[64];
   const int img = blockIdx.y;
   const int t = threadIdx.x;
   const int cpg = C / groups;
-  // fold the per-chunk partials: SUB = 256/groups threads per group, each a strided share of the chunks
-  // (fixed order -> bitwise reproducible), then a shuffle tree in fp64
-  {
-    const int SUB = 256 / groups;  // groups <= 64 -> SUB >= 4 (power of two for groups in {32, 64})
-    const int g = t / SUB, j = t % SUB;
-    double s = 0.0, q = 0.0;
-    if (g < groups) {
-      const float2* p = part + (long long)img * nchunks * groups + g;
-      for (int c = j; c < nchunks; c += SUB) {
-        const float2 v = p[(long long)c * groups];
-        s += v.x;
-        q += v.y;
-      }
-    }
-    for (int o = SUB / 2; o > 0; o >>= 1) {
-      s += __shfl_xor(s, o, 64);
-      q += __shfl_xor(q, o, 64);
-    }
-    if (g < groups && j == 0) {
-      const double n = (double)HW * cpg;
-      const double mean = s / n;
-      double var = q / n - mean * mean;
-      if (var < 0) var = 0;
-      mean_s[g] = (float)mean;
-      rstd_s[g] = (float)(1.0 / sqrt(var + (double)eps));
-    }
+  if (t < groups) {
+    const float2 st = stats[img * groups + t];
+    mean_s[t] = st.x;
+    rstd_s[t] = st.y;
   }
   __syncthreads();
   for (int c = t; c < C; c += 256) {
@@ -149,7 +158,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
 extern "C" long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups) {
   const int rpc = gn_rows_per_chunk(nimg, HW);
   const int nch = (HW + rpc - 1) / rpc;
-  return (long long)nimg * nch * groups * sizeof(float2);
+  return (long long)nimg * (nch + 1) * groups * sizeof(float2);  // partials, then per-group stats
 }
 
 extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
@@ -175,8 +184,11 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
                                             (float2*)ws, HW, C, groups, rpc));
   }
   FD_LAUNCH_CHECK();
+  float2* stats = (float2*)ws + (long long)nimg * nch * groups;
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(nimg), dim3(256), 0, s, (const float2*)ws, stats, HW, C, groups, nch, eps);
+  FD_LAUNCH_CHECK();
   FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
-                                          (T*)y, (const float2*)ws, gamma, beta, HW, C, groups, nch, rpb, eps, silu));
+                                          (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb, silu));
   FD_LAUNCH_CHECK();
   return FD_OK;
 }
@@ -227,12 +239,14 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
   for (int k = 0; k < MAXV; ++k) {
     const int v = lane + k * 64;
     if (v < VPR) {
+      float g[8], b[8];
+      *(f32x4*)&g[0] = *(const f32x4*)(gamma + v * 8);
+      *(f32x4*)&g[4] = *(const f32x4*)(gamma + v * 8 + 4);
+      *(f32x4*)&b[0] = *(const f32x4*)(beta + v * 8);
+      *(f32x4*)&b[4] = *(const f32x4*)(beta + v * 8 + 4);
       V8 out;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int c = v * 8 + i;
-        out[i] = (T)((vals[k][i] - mean) * rstd * gamma[c] + beta[c]);
-      }
+      for (int i = 0; i < 8; ++i) out[i] = (T)((vals[k][i] - mean) * rstd * g[i] + b[i]);
       *(V8*)(yr + v * 8) = out;
     }
   }
@@ -241,6 +255,7 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
 extern "C" int fd_layer_norm(const void* x, long long ldx, void* y, long long ldy, const float* gamma,
                              const float* beta, int M, int C, float eps, int dtype, void* stream) {
   if (!x || !y || !gamma || !beta) return FD_ERR_ARG;
+  if ((((unsigned long long)gamma) | ((unsigned long long)beta)) & 15) return FD_ERR_ARG;  // 16-B vector loads
   if (M <= 0 || C <= 0 || C % 8 || C > 2048 || (ldx & 7) || (ldy & 7)) return FD_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   FD_DISPATCH_T(dtype, hipLaunchKernelGGL(layer_norm_kernel<T>, dim3((M + 3) / 4), dim3(256), 0, s, (const T*)x, ldx,
