@@ -407,6 +407,8 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
   }
 }
 
+extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream);  // gemm8.hip
+
 extern "C" int fd_gemm(const fd_gemm_params* p, void* stream) {
   if (!p || !p->A || !p->B || !p->C) return FD_ERR_ARG;
   if (p->M <= 0 || p->N <= 0 || p->K <= 0 || (p->K % 64) != 0) return FD_ERR_SHAPE;
@@ -418,6 +420,9 @@ extern "C" int fd_gemm(const fd_gemm_params* p, void* stream) {
     if (p->stride != 1 && p->stride != 2) return FD_ERR_SHAPE;
     if (p->upsample && (p->stride != 1 || p->pad != 1 || p->Hout < p->Hin || p->Wout < p->Win)) return FD_ERR_SHAPE;
   }
+  const int r8 = fd_gemm8_try(p, stream);
+  if (r8 < 0) return r8;
+  if (r8 == 1) return FD_OK;
   hipStream_t s = (hipStream_t)stream;
   FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, return dispatch_tiles<T, TO>(p, s)));
 }

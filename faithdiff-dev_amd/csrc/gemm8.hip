@@ -1,0 +1,572 @@
+// Eight-wave, 256-row-tile MFMA GEMM / implicit-GEMM convolution for gfx950 with in-launch split-K.
+//
+// Why a second GEMM: at C2 (one 1024^2 tile, CFG pair) most of the UNet's FLOPs sit in GEMMs with
+// M = 2048 (the 32^2 level: 2 x 1024 pixels) whose 128^2-tile launches cover only 64-160 of the 256 CUs,
+// and each CU's operand stream from L2 (~70 GB/s per CU, MI355X_MICROARCH.md "Indexed rows") -- not the
+// MFMA pipe -- bounds them.  This kernel raises the FLOP per operand byte (256 x 160 tile: 98 flop/B
+// vs 64 for 128^2) and restores the CU count by splitting K across workgroups (S = 1..8), combining the
+// fp32 partial tiles inside the same launch (last-arriving workgroup of a tile sums the S slabs in split
+// order -- bitwise independent of arrival order -- and runs the fused epilogue).  S is chosen from
+// (m_ref, N, K), where m_ref is the caller's per-tile row count, so batching TLC tiles into one forward
+// does not change any output bit.
+//
+// Structure (cdna_hip_programming.md section 5): 512 threads = 8 waves (WAVES_M x WAVES_N), each wave a
+// WM x WN sub-tile of v_mfma_f32_16x16x32; both operands K-contiguous ([rows][K]) staged global -> LDS by
+// global_load_lds_dwordx4 into a 3-deep ring (two stages in flight across each barrier: counted
+// s_waitcnt vmcnt, raw s_barrier); fragments are register double-buffered by K half, so the LDS reads
+// of half h+1 overlap the MFMAs of half h, and the one barrier per 64-deep K step sits between the two
+// MFMA halves.  XOR-swizzled 128-B LDS rows (source-side swizzle, rule 21).  Conv: im2col gather from
+// NHWC with out-of-image taps on a zero page; nearest upsample and two-source skip concat folded in.
+#include <stdlib.h>
+
+#include "fd_common.h"
+
+__device__ __attribute__((aligned(256))) unsigned char g_zero_page8[256];
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+#ifndef FD_GEMM8_SCHED
+#define FD_GEMM8_SCHED 1
+#endif
+#ifndef FD_GEMM8_DIAG
+#define FD_GEMM8_DIAG 0
+#endif
+
+template <typename T, int BN, int WAVES_M, bool CONV, bool GEGLU, typename TO>
+__global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, const int S, const int gm_mode,
+                                                    float* __restrict__ slabs, unsigned* __restrict__ counters) {
+  typedef typename VecT<T>::v8 V8;
+  constexpr bool SCHED = FD_GEMM8_SCHED;
+  constexpr int BM = 256, NS = 3;
+  constexpr int WAVES_N = 8 / WAVES_M;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int MT = WM / 16, NT = WN / 16;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int A_I = BM / 64;             // A loads per wave per stage (8 rows x 128 B each)
+  constexpr int B_TOT = BN / 8;            // B loads per stage over the 8 waves
+  constexpr int B_I = (B_TOT + 7) / 8;     // ... at most this many per wave
+  constexpr int B_LO = B_TOT / 8;          // waves >= B_TOT % 8 issue only this many
+  constexpr int PER_HI = A_I + B_I, PER_LO = A_I + B_LO;
+  constexpr int BNO = GEGLU ? BN / 2 : BN;
+  constexpr int LDE = BNO + 4;
+  // epilogue staged fp32 [EROWS][BNO+4] in the ring's LDS: the whole tile when it fits, else 128-row halves
+  constexpr int EROWS = (BM * LDE * 4 <= NS * STAGE) ? BM : 128;
+  constexpr int EPB = EROWS * LDE * 4;
+  constexpr int SMEM = (NS * STAGE > EPB) ? NS * STAGE : EPB;
+  static_assert(SMEM <= 163840, "LDS");
+  static_assert(!GEGLU || (WN % 32 == 0), "GEGLU pairs must not straddle waves");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WAVES_N, wn = w % WAVES_N;
+  const int M = p.M, N = p.N, K = p.K;
+  // diagnostic builds only (-DFD_GEMM8_DIAG=m; 0 in the product): 1 = no operand loads, 2 = no LDS reads /
+  // MFMA, 4 = no epilogue stores.  Compile-time, so the product loop has no branches.
+  constexpr int mode = FD_GEMM8_DIAG;
+  const int group_m = gm_mode;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+
+  // ---- block -> (tile, split): XCD-contiguous chunks (bijective remap), a tile's S splits adjacent
+  // (same XCD: the reducer reads same-L2 slabs), tiles walked in groups of group_m tile rows.
+  const int pid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = pid % S, tlin = pid / S;
+  int tm, tn;
+  {
+    const int gsz_full = group_m * tiles_n;
+    const int grp = tlin / gsz_full;
+    const int first_m = grp * group_m;
+    const int gsz = min(tiles_m - first_m, group_m);
+    const int in_g = tlin - grp * gsz_full;
+    tm = first_m + in_g % gsz;
+    tn = in_g / gsz;
+  }
+  const int tile_id = tm * tiles_n + tn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = K / 64;
+  const int kb = (int)((long long)split * nk / S), ke = (int)((long long)(split + 1) * nk / S);
+  const int nkl = ke - kb;
+
+  const T* __restrict__ A = (const T*)p.A;
+  const T* __restrict__ Bw = (const T*)p.B;
+  const T* __restrict__ A2 = (const T*)p.A2;
+  const int lrow = lane >> 3, slot = lane & 7;
+  const bool hi = (B_TOT % 8 == 0) || w < B_TOT % 8;  // this wave issues B_I (not B_LO) B loads
+
+  // ---- per-lane load state (rows fixed over the K loop)
+  const T* a_row[A_I];
+  int a_iy0[A_I], a_ix0[A_I], a_chunk[A_I];
+  long long a_pix[A_I];
+  bool a_ok[A_I];
+#pragma unroll
+  for (int i = 0; i < A_I; ++i) {
+    const int row = (w + 8 * i) * 8 + lrow;
+    const int m = m0 + row;
+    a_ok[i] = m < M;
+    const int mm = m < M ? m : M - 1;
+    a_chunk[i] = slot ^ ((row >> 1) & 7);
+    if (CONV) {
+      const int hw = p.Hout * p.Wout;
+      const int img = mm / hw;
+      const int rem = mm - img * hw;
+      const int oy = rem / p.Wout, ox = rem - (rem / p.Wout) * p.Wout;
+      a_iy0[i] = oy * p.stride - p.pad;
+      a_ix0[i] = ox * p.stride - p.pad;
+      a_pix[i] = (long long)img * p.Hin * p.Win;
+      a_row[i] = nullptr;
+    } else {
+      a_row[i] = A + (long long)mm * p.lda + a_chunk[i] * 8;
+      a_iy0[i] = a_ix0[i] = 0;
+      a_pix[i] = 0;
+    }
+  }
+  const T* b_row[B_I];
+#pragma unroll
+  for (int i = 0; i < B_I; ++i) {
+    const int row = (w + 8 * i) * 8 + lrow;  // < BN for the loads this wave issues
+    const int n = n0 + (row < BN ? row : 0);
+    b_row[i] = Bw + (long long)(n < N ? n : N - 1) * p.ldb + (slot ^ ((row >> 1) & 7)) * 8;
+  }
+  const int Hl = p.upsample ? p.Hout : p.Hin, Wl = p.upsample ? p.Wout : p.Win;
+  const int C1 = p.C1 > 0 ? p.C1 : p.Cin;
+
+  auto stage = [&](int kt, int buf) {  // kt: global K step
+    if (mode & 1) return;
+    const int k0 = kt * 64;
+    unsigned char* sa = smem + buf * STAGE;
+    if (CONV) {
+      const int tap = k0 / p.Cin;
+      const int c0 = k0 - tap * p.Cin;
+      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+      const bool second = (A2 != nullptr) && (c0 >= C1);
+#pragma unroll
+      for (int i = 0; i < A_I; ++i) {
+        const int iy = a_iy0[i] + ky, ix = a_ix0[i] + kx;
+        const bool ok = a_ok[i] && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
+        const int py = p.upsample ? (iy * p.Hin) / Hl : iy, px = p.upsample ? (ix * p.Win) / Wl : ix;
+        const long long pix = a_pix[i] + (long long)py * p.Win + px;
+        const T* src = second ? (A2 + pix * (p.Cin - C1) + (c0 - C1) + a_chunk[i] * 8)
+                              : (A + pix * p.lda + c0 + a_chunk[i] * 8);
+        const void* s = ok ? (const void*)src : (const void*)g_zero_page8;
+        __builtin_amdgcn_global_load_lds(s, LDS_PTR(sa + (w + 8 * i) * 1024), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_I; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(a_row[i] + k0), LDS_PTR(sa + (w + 8 * i) * 1024), 16, 0, 0);
+    }
+    unsigned char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < B_I; ++i)
+      if (i < B_LO || hi)
+        __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (w + 8 * i) * 1024), 16, 0, 0);
+  };
+  // all but the youngest `ahead` stages of this wave's loads have landed
+  auto wait_ahead = [&](int ahead) {
+    if (ahead >= 2) {
+      if (hi) vm_wait<2 * PER_HI>(); else vm_wait<2 * PER_LO>();
+    } else if (ahead == 1) {
+      if (hi) vm_wait<PER_HI>(); else vm_wait<PER_LO>();
+    } else {
+      vm_wait<0>();
+    }
+  };
+
+  const int fr = lane & 15, fg = lane >> 4;
+  auto read_frags = [&](int buf, int h, V8 (&af)[MT], V8 (&bf)[NT]) {
+    if (mode & 2) return;
+    const unsigned char* sa = smem + buf * STAGE;
+    const unsigned char* sb = sa + A_BYTES;
+    const int ch = h * 4 + fg;
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int r = wm * WM + mi * 16 + fr;
+      af[mi] = *(const V8*)(sa + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+    }
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni) {
+      const int r = wn * WN + ni * 16 + fr;
+      bf[ni] = *(const V8*)(sb + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const V8 (&af)[MT], const V8 (&bf)[NT]) {
+    if (mode & 2) return;
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = mfma16x16x32(af[mi], bf[ni], acc[mi][ni]);
+  };
+
+  // ---- main loop: ring of 3 stages; stage s lives in buffer s % 3.  The waits the compiler must see
+  // (LDS reads retired before the barrier) use the builtin, so it does not re-wait them -- and with
+  // them the next stage's fragment reads -- in front of the second MFMA half (an inline-asm lgkmcnt is
+  // invisible to its waitcnt pass).  Only the LDS-DMA counts are inline asm (it does not track them).
+  stage(kb, 0);
+  if (nkl > 1) stage(kb + 1, 1);
+  if (nkl > 2) stage(kb + 2, 2);
+  wait_ahead(min(nkl - 1, 2));
+  __builtin_amdgcn_s_barrier();
+  V8 a0[MT], b0[NT], a1[MT], b1[NT];
+  read_frags(0, 0, a0, b0);
+  int buf = 0;
+  // one K step: half-1 reads under the half-0 MFMAs, barrier, refill + next half-0 reads under the half-1
+  // MFMAs.  The steady-state loop has no branches inside, so sched_group_barrier can interleave one read
+  // (or LDS-DMA issue) between consecutive MFMAs within each of the two regions.
+  auto step = [&](const bool refill, const int ahead, const int kt) {
+    read_frags(buf, 1, a1, b1);
+    mma(a0, b0);
+    if (SCHED) {
+#pragma unroll
+      for (int i = 0; i < MT + NT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, MT * NT - (MT + NT), 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the half-0 MFMAs on this side of the barrier
+    wait_ahead(ahead);                   // stage kt+1 landed (kt+2 may still fly)
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage kt retired
+    __builtin_amdgcn_s_barrier();        // ... and every wave's; stage kt+1 visible to all
+    if (refill) stage(kb + kt + 3, buf);
+    buf = buf == 2 ? 0 : buf + 1;
+    read_frags(buf, 0, a0, b0);
+    mma(a1, b1);
+    if (SCHED) {
+      if (refill) {
+#pragma unroll
+        for (int i = 0; i < PER_LO; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MT + NT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+      }
+    }
+  };
+  int kt = 0;
+  for (; kt < nkl - 3; ++kt) step(true, 1, kt);
+  for (; kt < nkl - 1; ++kt) step(false, kt + 2 < nkl ? 1 : 0, kt);
+  read_frags(buf, 1, a1, b1);
+  mma(a0, b0);
+  mma(a1, b1);
+
+  // ---- split-K combine: each split stores its fp32 partial slab write-through (sc1) and drains it; one
+  // lane then takes a ticket on the tile's counter (agent-scope atomic).  The last arriver reads all S
+  // slabs with sc1 loads (no L1/L2 flush or invalidate needed: cdna_hip_programming.md section 5,
+  // "Projection GEMM" item 2, sc1 form), sums them in split order and runs the epilogue; the others exit.
+  if (S > 1) {
+    constexpr int SLAB = MT * NT * 512 * 16;  // bytes per split of one tile
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((char*)slabs + (long long)tile_id * S * SLAB, (short)0, S * SLAB, 0x00020000);
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][ni]), rs,
+                                               split * SLAB + ((mi * NT + ni) * 512 + tid) * 16, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned tk = __hip_atomic_fetch_add(counters + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *(volatile unsigned*)smem = tk;
+    }
+    __syncthreads();
+    const unsigned tk = *(volatile unsigned*)smem;
+    if (tk != (unsigned)(S - 1)) return;
+    if (tid == 0) __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+        acc[mi][ni] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((mi * NT + ni) * 512 + tid) * 16, 0, 16));
+    for (int q = 1; q < S; ++q) {
+      f32x4 part[MT][NT];
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni)
+          part[mi][ni] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, q * SLAB + ((mi * NT + ni) * 512 + tid) * 16, 0, 16));
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) acc[mi][ni] += part[mi][ni];
+    }
+  }
+
+  if (mode & 4) {
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) asm volatile("" ::"v"(acc[mi][ni]));
+    return;
+  }
+  // ---- epilogue in BM / EROWS passes.  Phase 1: accumulators -> LDS fp32 [128][LDE] (alpha applied;
+  // GEGLU pairs (h, g) are combined here, their bias loaded once per lane up front).  Phase 2: each thread
+  // owns 8 consecutive columns of a row: bias, row-group bias (time embedding), activation and residual
+  // with 16-B vector loads issued together, one 16-B store.  With one workgroup per CU nothing hides a
+  // stalled epilogue, so no per-element branches or loads.
+  TO* __restrict__ C = (TO*)p.C;
+  const TO* __restrict__ R = (const TO*)p.residual;
+  const float* __restrict__ bias = p.bias;
+  const float* __restrict__ rbias = p.rowbias;
+  const int Nout = GEGLU ? N / 2 : N;
+  const int n0o = GEGLU ? n0 / 2 : n0;
+  const float alpha = p.alpha;
+  const int act = p.act;
+  float* ep = (float*)smem;
+  constexpr int VPR = BNO / 8;
+  constexpr int ITER = 4;  // row-phase iterations whose loads are issued together
+  static_assert(EROWS * VPR % (512 * ITER) == 0, "epilogue iterations");
+  float gbh[GEGLU ? NT / 2 : 1], gbg[GEGLU ? NT / 2 : 1];
+  if (GEGLU) {
+#pragma unroll
+    for (int q = 0; q < NT / 2; ++q) {
+      const int np = min(n0 + wn * WN + 2 * q * 16 + fr, N - 17);
+      gbh[q] = bias ? bias[np] : 0.f;
+      gbg[q] = bias ? bias[np + 16] : 0.f;
+    }
+  }
+  const bool vec = (Nout % 8 == 0) && (p.ldc % 8 == 0) && ((((unsigned long long)C) & 15) == 0) &&
+                   (!R || ((p.ldr % 8 == 0) && ((((unsigned long long)R) & 15) == 0))) &&
+                   (GEGLU || !bias || ((((unsigned long long)bias) & 15) == 0)) &&
+                   (GEGLU || !rbias || ((p.rowbias_ld % 4 == 0) && ((((unsigned long long)rbias) & 15) == 0)));
+  const bool interior = vec && (m0 + BM <= M) && (n0o + BNO <= Nout);
+  typedef __attribute__((ext_vector_type(8))) TO TO8;
+#pragma unroll 1
+  for (int half = 0; half < BM / EROWS; ++half) {
+    __syncthreads();  // ring (half 0) / previous half's staging (half 1) fully consumed
+    if ((wm * WM) / EROWS == half) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        const int rl = wm * WM + mi * 16 + fg * 4 - half * EROWS;
+        if (GEGLU) {
+#pragma unroll
+          for (int ni = 0; ni < NT; ni += 2) {
+            const int col = (wn * WN) / 2 + (ni / 2) * 16 + fr;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float hv = acc[mi][ni][j] * alpha + gbh[ni / 2];
+              const float g = acc[mi][ni + 1][j] * alpha + gbg[ni / 2];
+              ep[(rl + j) * LDE + col] = hv * gelu_f(g);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int ni = 0; ni < NT; ++ni) {
+            const int col = wn * WN + ni * 16 + fr;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ep[(rl + j) * LDE + col] = acc[mi][ni][j] * alpha;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (interior) {
+#pragma unroll 1
+    for (int e0 = 0; e0 < EROWS * VPR; e0 += 512 * ITER) {
+      float v[ITER][8], bv[ITER][8], rv[ITER][8];
+      TO8 res[ITER];
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int e = e0 + tid + it * 512;
+        const int r = e / VPR, cv = e % VPR;
+        const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
+        *(f32x4*)&v[it][0] = *(const f32x4*)(ep + r * LDE + cv * 8);
+        *(f32x4*)&v[it][4] = *(const f32x4*)(ep + r * LDE + cv * 8 + 4);
+        if (!GEGLU && bias) {
+          *(f32x4*)&bv[it][0] = *(const f32x4*)(bias + n);
+          *(f32x4*)&bv[it][4] = *(const f32x4*)(bias + n + 4);
+        }
+        if (!GEGLU && rbias) {
+          const float* rb = rbias + (long long)(m / p.rows_per_group) * p.rowbias_ld + n;
+          *(f32x4*)&rv[it][0] = *(const f32x4*)rb;
+          *(f32x4*)&rv[it][4] = *(const f32x4*)(rb + 4);
+        }
+        if (R) res[it] = *(const TO8*)(R + (long long)m * p.ldr + n);
+      }
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int e = e0 + tid + it * 512;
+        const int r = e / VPR, cv = e % VPR;
+        const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
+        if (!GEGLU) {
+          if (bias) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] += bv[it][i];
+          }
+          if (rbias) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] += rv[it][i];
+          }
+          if (act == FD_ACT_SILU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = silu_f(v[it][i]);
+          } else if (act == FD_ACT_GELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = gelu_f(v[it][i]);
+          } else if (act == FD_ACT_QUICKGELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = quickgelu_f(v[it][i]);
+          }
+        }
+        if (R) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[it][i] += (float)res[it][i];
+        }
+        TO8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
+        *(TO8*)(C + (long long)m * p.ldc + n) = o;
+      }
+    }
+    } else {  // edge tiles / unaligned operands: scalar, bounds-checked
+      for (int e = tid; e < EROWS * VPR; e += 512) {
+        const int r = e / VPR, cv = e % VPR;
+        const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
+        if (m >= M || n >= Nout) continue;
+        for (int i = 0; i < 8 && n + i < Nout; ++i) {
+          float x = ep[r * LDE + cv * 8 + i];
+          if (!GEGLU) {
+            if (bias) x += bias[n + i];
+            if (rbias) x += rbias[(long long)(m / p.rows_per_group) * p.rowbias_ld + n + i];
+            x = act_f(x, act);
+          }
+          if (R) x += (float)R[(long long)m * p.ldr + n + i];
+          C[(long long)m * p.ldc + n + i] = (TO)x;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ host
+namespace {
+
+struct Plan8 {
+  int bn, waves_m, S, group_m, tiles;
+};
+
+int env_i(const char* n, int d) {
+  const char* v = getenv(n);
+  return v ? atoi(v) : d;
+}
+
+// Split count from the per-tile row count m_ref (not the batched M).  Measured on MI355X (scripts/gemm8_sweep.sh,
+// profiles/r01_gemm8_sweep.txt): one 147 KiB workgroup per CU streams ~40-70 GB/s of operands, so a 256x128 tile
+// K step costs ~1.1-1.4 us whatever the tile count, while the split-K slab round trip (write-through fp32 slabs
+// + the reducer's reads) costs ~S * tiles * 256 KiB at HBM speed (~15 us at 2048 x 1280).  Splitting therefore
+// pays only for long K (the 3x3 convs of the 32^2 level, K = 9 * 1280 and up).  Returns 0 when the 4-wave
+// kernel is the better choice (few tiles and short K, or N not a multiple of the 128-column tile).
+int choose_split(int m_ref, int N, int K, int bn) {
+  const int nk = K / 64;
+  const long long tiles = (long long)((m_ref + 255) / 256) * ((N + bn - 1) / bn);
+  if (N % bn != 0) return 0;
+  if (tiles >= 192) return 1;
+  if (K < 8192) return 0;
+  int s = (int)(256 / tiles);
+  if (s > nk / 8) s = nk / 8;
+  if (s > 8) s = 8;
+  return s < 1 ? 1 : s;
+}
+
+template <typename T, typename TO, int BN, int WAVES_M>
+int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
+  dim3 grid(pl.tiles * pl.S), block(512);
+  float* slabs = (float*)((char*)p->ws + 65536 * sizeof(unsigned));
+  unsigned* cnt = (unsigned*)p->ws;
+  if (p->conv) {
+    hipLaunchKernelGGL((gemm8_kernel<T, BN, WAVES_M, true, false, TO>), grid, block, 0, s, *p, pl.S, pl.group_m, slabs,
+                       cnt);
+  } else if (p->act == FD_ACT_GEGLU) {
+    if constexpr ((BN / (8 / WAVES_M)) % 32 == 0)
+      hipLaunchKernelGGL((gemm8_kernel<T, BN, WAVES_M, false, true, TO>), grid, block, 0, s, *p, pl.S, pl.group_m,
+                         slabs, cnt);
+    else
+      return FD_ERR_ARG;
+  } else {
+    hipLaunchKernelGGL((gemm8_kernel<T, BN, WAVES_M, false, false, TO>), grid, block, 0, s, *p, pl.S, pl.group_m, slabs,
+                       cnt);
+  }
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+}  // namespace
+
+// Plan for one launch (0 = not eligible -> the 4-wave kernel).  Shared by fd_gemm8_ws_bytes and fd_gemm8.
+static int plan8(const fd_gemm_params* p, Plan8* pl) {
+  static int enabled = -1, force_s = 0, force_bn = 0, force_gm = 0;
+  if (enabled < 0) {
+    enabled = env_i("FD_GEMM8", 1);
+    force_s = env_i("FD_GEMM8_S", 0);
+    force_bn = env_i("FD_GEMM8_BN", 0);
+    force_gm = env_i("FD_GEMM8_GM", 0);
+  }
+  const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
+  if (!enabled || m_ref < 256 || p->N < 128 || (p->batch > 1) || p->K < 128) return 0;
+  Plan8 q;
+  // 256 x 128 tiles (4 x 2 waves of 64 x 64).  256 x 160 (98 vs 85 flop/B) spills at the 256-VGPR cap of
+  // two waves per SIMD with register-double-buffered fragments; kept out until it fits.
+  (void)force_bn;
+  q.bn = 128;
+  q.waves_m = 4;
+  q.S = force_s > 0 ? force_s : choose_split(m_ref, p->N, p->K, q.bn);
+  if (q.S <= 0) return 0;
+  if (q.S > p->K / 64) q.S = p->K / 64;
+  const int tiles_m = (p->M + 255) / 256, tiles_n = (p->N + q.bn - 1) / q.bn;
+  q.tiles = tiles_m * tiles_n;
+  if (q.S > 1 && q.tiles > 65536) return 0;
+  // group_m: per-XCD chunk of tiles/8 tiles; pick the tile-row group height minimising that chunk's
+  // unique A rows + B columns (both stream K bytes each)
+  int gm = 1;
+  {
+    const long long per_xcd = ((long long)q.tiles + 7) / 8;
+    double bestc = 1e30;
+    for (int g = 1; g <= tiles_m; g *= 2) {
+      const long long cols = per_xcd < g ? 1 : (per_xcd + g - 1) / g;
+      const long long rows = per_xcd < g ? per_xcd : g;
+      const double c = rows * 256.0 + (cols < tiles_n ? cols : tiles_n) * (double)q.bn;
+      if (c < bestc - 1e-9) { bestc = c; gm = g; }
+    }
+  }
+  q.group_m = force_gm > 0 ? force_gm : gm;
+  *pl = q;
+  return 1;
+}
+
+extern "C" long long fd_gemm_ws_bytes(const fd_gemm_params* p) {
+  Plan8 pl;
+  if (!p || !plan8(p, &pl) || pl.S <= 1) return 0;
+  const long long slab = 256LL * pl.bn * 4;
+  return 65536LL * sizeof(unsigned) + (long long)pl.tiles * pl.S * slab;
+}
+
+// Returns 1 and launches when the eight-wave kernel takes this GEMM, 0 when it does not apply, < 0 on error.
+extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream) {
+  Plan8 pl;
+  if (!plan8(p, &pl)) return 0;
+  if (pl.S > 1) {
+    const long long need = 65536LL * sizeof(unsigned) + (long long)pl.tiles * pl.S * 256LL * pl.bn * 4;
+    if (!p->ws || p->ws_bytes < need) return FD_ERR_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+#define FD_G8(BN_, WM_) FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, rc = (launch8<T, TO, BN_, WM_>(p, pl, s))))
+  FD_G8(128, 4);
+#undef FD_G8
+  return rc == FD_OK ? 1 : rc;
+}

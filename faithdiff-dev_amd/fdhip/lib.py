@@ -32,12 +32,14 @@ class GemmParams(ctypes.Structure):
         ("conv", c_int), ("nimg", c_int), ("Hin", c_int), ("Win", c_int), ("Cin", c_int),
         ("Hout", c_int), ("Wout", c_int), ("stride", c_int), ("pad", c_int), ("upsample", c_int),
         ("A2", c_vp), ("C1", c_int),
+        ("m_ref", c_int), ("ws", c_vp), ("ws_bytes", c_ll),
     ]
 
 
 # name -> (restype, argtypes)
 _SIGS = {
     "fd_gemm": (c_int, [ctypes.POINTER(GemmParams), c_vp]),
+    "fd_gemm_ws_bytes": (c_ll, [ctypes.POINTER(GemmParams)]),
     "fd_conv2d_direct": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f,
                                  c_int, c_int, c_vp]),
     "fd_group_norm_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),

@@ -26,6 +26,53 @@ def reserve_gn_workspace(nbytes, device):
     _gn_ws(nbytes, device)
 
 
+# --------------------------------------------------------------------------------------- GEMM workspace
+_GEMM_WS = {}
+_TILE_GROUPS = [1]
+
+
+class tile_groups:
+    """Context: the current forward batches ``n`` TLC tiles along M.  fd_gemm derives its split-K count
+    from the per-tile row count (m_ref = M / n), so a batched forward is bitwise equal to per-tile ones."""
+
+    def __init__(self, n):
+        self.n = max(int(n), 1)
+
+    def __enter__(self):
+        _TILE_GROUPS.append(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        _TILE_GROUPS.pop()
+
+
+def reserve_gemm_workspace(nbytes, device):
+    """Pre-size the split-K workspace (zeroed: its head holds the tile counters).  Call before capture."""
+    key = torch.device(device)
+    ws = _GEMM_WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        if ws is not None:
+            torch.cuda.synchronize(key)
+        _GEMM_WS[key] = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=key)
+    return _GEMM_WS[key]
+
+
+def _attach_ws(p, device):
+    groups = _TILE_GROUPS[-1]
+    p.m_ref = p.M // groups if groups > 1 and p.M % groups == 0 else p.M
+    need = L.load().fd_gemm_ws_bytes(ctypes.byref(p))
+    if need <= 0:
+        return
+    key = torch.device(device)
+    ws = _GEMM_WS.get(key)
+    if ws is None or ws.numel() < need:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"fd_gemm split-K workspace too small inside graph capture ({need} B): "
+                               "run the forward once eagerly or call ops.reserve_gemm_workspace first")
+        ws = reserve_gemm_workspace(int(need * 1.25), device)
+    p.ws, p.ws_bytes = ws.data_ptr(), ws.numel()
+
+
 # --------------------------------------------------------------------------------------- packing
 def pack_conv3x3(w):
     """[Cout, Cin, 3, 3] -> [Cout, 9*Cin] with k = (ky*3 + kx)*Cin + c (tap-major, channel-contiguous)."""
@@ -109,6 +156,7 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
     p.act = L.ACT[act]
     p.dtype = L.dtype_code(a.dtype)
     p.out_dtype = L.dtype_code(odt)
+    _attach_ws(p, a.device)
     _launch_gemm(p, "fd_gemm")
     return out
 
@@ -146,6 +194,7 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
     p.conv, p.nimg, p.Hin, p.Win, p.Cin = 1, nimg, H, W, Cin
     p.Hout, p.Wout, p.stride, p.pad, p.upsample = Hout, Wout, stride, pad, int(upsample)
     p.A2 = x2.data_ptr() if x2 is not None else None
+    _attach_ws(p, x.device)
     _launch_gemm(p, "fd_gemm(conv)")
     return out
 

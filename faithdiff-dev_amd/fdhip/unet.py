@@ -246,6 +246,10 @@ class HipUNet:
         cond: NHWC [B*H*W, 512] image latents (dtype) or None.  Returns eps NHWC [B*H*W, 4] (dtype)."""
         assert self.ctx is not None, "call set_context(prompt_embeds) first"
         assert B % self.ncfg == 0
+        with ops.tile_groups(B // self.ncfg):
+            return self._forward(x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample)
+
+    def _forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample):
         temb = self.embeddings(t, time_ids, text_embeds, B)
         self._kv = ops.gemm(self.ctx, self.kv_w)  # [ncfg*77, sum 2C]: every attn2 K/V of this forward
         x0 = ops.conv_direct(x, *self.conv_in, B, H, Wd, 4, 3, 1, 1, out_dtype=self.dtype)

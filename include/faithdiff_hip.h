@@ -34,8 +34,9 @@ enum { FD_BF16 = 0, FD_F16 = 1, FD_F32 = 2 };
 enum { FD_ACT_NONE = 0, FD_ACT_SILU = 1, FD_ACT_GELU = 2, FD_ACT_QUICKGELU = 3, FD_ACT_GEGLU = 4 };
 
 /* ---------------------------------------------------------------------------------------------
- * GEMM / implicit-GEMM convolution on MFMA (v_mfma_f32_16x16x32_{bf16,f16}), LDS double-buffered
- * via global_load_lds.  C[b][m][n] = epi( alpha * sum_k A[b][m][k] * B[b][n][k] ).
+ * GEMM / implicit-GEMM convolution on MFMA (v_mfma_f32_16x16x32_{bf16,f16}), operands staged through
+ * LDS by global_load_lds.  Two kernels: 8-wave 256-row tiles with in-launch split-K (M >= 256) and
+ * 4-wave 128/64-row tiles (small M, batched).  C[b][m][n] = epi( alpha * sum_k A[b][m][k] * B[b][n][k] ).
  *   epi(v) = act(v + bias[n] + rowbias[(m / rows_per_group) * rowbias_ld + n]) + residual[m][n]
  *   act == FD_ACT_GEGLU: B rows are packed in groups of 32 = [16 "hidden" | 16 "gate"]; the
  *   output has N/2 columns: out = (h + b_h) * gelu(g + b_g)   (diffusers GEGLU).
@@ -71,9 +72,19 @@ typedef struct fd_gemm_params {
   int nimg, Hin, Win, Cin, Hout, Wout, stride, pad, upsample;
   const void* A2;
   int C1;
+  /* split-K / tiling (0 / NULL = defaults).  m_ref: rows of ONE TLC tile's forward; the split-K count
+   * (the only choice that changes summation order) is derived from (m_ref, N, K), so batching tiles
+   * into one launch leaves every output bit unchanged.  ws: caller-owned workspace of at least
+   * fd_gemm_ws_bytes(p) bytes whose first 256 KiB (split-K tile counters) are zero before the first
+   * launch; launches leave them zero again. */
+  int m_ref;
+  void* ws;
+  long long ws_bytes;
 } fd_gemm_params;
 
 int fd_gemm(const fd_gemm_params* p, void* stream);
+/* Workspace fd_gemm needs for this launch (0 = none). */
+long long fd_gemm_ws_bytes(const fd_gemm_params* p);
 
 /* Direct convolution for the few convs with Cin < 64 (k*k*Cin in {36, 27, 8, 4}) (UNet conv_in 4->320, VAE conv_in 3->128,
  * decoder conv_in 4->512, quant_conv / post_quant_conv 1x1).  x NHWC (dtype), w fp32

@@ -1,5 +1,9 @@
 #!/usr/bin/env python3
-"""Time a few GEMM shapes under the current FD_GEMM_* env (one process per setting); JSON lines out."""
+"""Time GEMM shapes under the current FD_GEMM_* env; JSON lines out.
+
+Each shape's launches are captured in one hipGraph (REP back-to-back launches) and the graph replayed, so the
+per-launch time excludes the ~10 us ctypes/Python enqueue cost that dominates small shapes when launched eagerly.
+Usage: gemm_probe.py [MxNxK[:act] ...]; conv shapes as convHxWxCinxCout (nimg 2)."""
 import json
 import os
 import sys
@@ -12,26 +16,46 @@ from fdhip import lib as L  # noqa: E402
 
 L.require_device()
 bf = torch.bfloat16
-SHAPES = [(2048, 1280, 1280), (2048, 1280, 5120), (2048, 1280, 12800), (2048, 3840, 1280), (8192, 640, 640)]
+SHAPES = ["2048x1280x1280", "2048x1280x5120", "2048x3840x1280", "2048x10240x1280:geglu", "8192x640x640"]
 if len(sys.argv) > 1:
-    SHAPES = [tuple(int(x) for x in s.split(":")[0].split("x")) + ((s.split(":")[1],) if ":" in s else ())
-              for s in sys.argv[1:]]
+    SHAPES = sys.argv[1:]
 tag = {k: v for k, v in os.environ.items() if k.startswith("FD_GEMM")}
-for shp in SHAPES:
-    M, N, K = shp[:3]
-    act = shp[3] if len(shp) > 3 else "none"
-    a = torch.randn(M, K, device="cuda").to(bf)
-    w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(bf)
-    out = torch.empty(M, N // 2 if act == "geglu" else N, device="cuda", dtype=bf)
-    for _ in range(5):
-        ops.gemm(a, w, out=out, act=act)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    it = 30
-    e0.record()
-    for _ in range(it):
-        ops.gemm(a, w, out=out, act=act)
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) / it * 1e3
-    print(json.dumps({**tag, "shape": f"{M}x{N}x{K}:{act}", "us": round(us, 2), "tflops": round(2 * M * N * K / us / 1e6, 1)}))
+REP = int(os.environ.get("PROBE_REP", "20"))
+g = torch.Generator(device="cuda").manual_seed(0)
+for s in SHAPES:
+    if s.startswith("conv"):
+        H, W, Cin, Cout = (int(x) for x in s[4:].split("x"))
+        x = torch.rand(2 * H * W, Cin, device="cuda", generator=g).to(bf) * 2 - 1
+        wp = ((torch.rand(Cout, 9 * Cin, device="cuda", generator=g) * 2 - 1) / (9 * Cin) ** 0.5).to(bf)
+        b = torch.zeros(Cout, device="cuda")
+        out = torch.empty(2 * H * W, Cout, device="cuda", dtype=bf)
+        fn = lambda: ops.conv3x3(x, wp, b, 2, H, W, out=out)  # noqa: E731
+        flops = 2 * 2 * H * W * Cout * 9 * Cin
+    else:
+        dims, act = (s.split(":") + ["none"])[:2]
+        M, N, K = (int(v) for v in dims.split("x"))
+        a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(bf)
+        w = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) / K ** 0.5).to(bf)
+        out = torch.empty(M, N // 2 if act == "geglu" else N, device="cuda", dtype=bf)
+        fn = lambda: ops.gemm(a, w, out=out, act=act)  # noqa: E731
+        flops = 2 * M * N * K
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=st):
+            for _ in range(REP):
+                fn()
+        graph.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        best = 1e30
+        for _ in range(5):
+            e0.record(st)
+            graph.replay()
+            e1.record(st)
+            torch.cuda.synchronize()
+            best = min(best, e0.elapsed_time(e1) / REP * 1e3)
+    print(json.dumps({**tag, "shape": s, "us": round(best, 2), "tflops": round(flops / best / 1e6, 1)}), flush=True)
