@@ -232,75 +232,131 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
     }
     __syncthreads();
   }
+  // phase 1 writes alpha * acc (GEGLU: the combined h * gelu(g), bias hoisted); phase 2 (whole-row, 8 columns
+  // per thread) adds bias / row-group bias, applies the activation and the residual with 16-B vector loads
+  // issued together -- no per-element branches or dependent loads (they serialise a 1-WG/CU launch).
+  const float* __restrict__ bias = p.bias;
+  const float* __restrict__ rbias = p.rowbias;
+  const int act = p.act;
   if (!kh) {
-  if (GEGLU) {
+    if (GEGLU) {
+      float gbh[NT / 2 > 0 ? NT / 2 : 1], gbg[NT / 2 > 0 ? NT / 2 : 1];
 #pragma unroll
-    for (int mi = 0; mi < MT; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < NT; ni += 2) {
-        const int np = n0 + wn * WN + ni * 16 + fr;  // packed "hidden" column; gate at np + 16
-        const int col = (wn * WN) / 2 + (ni / 2) * 16 + fr;
-        const float bh = (p.bias && np < N) ? p.bias[np] : 0.f, bg = (p.bias && np < N) ? p.bias[np + 16] : 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = wm * WM + mi * 16 + fg * 4 + j;
-          const float h = acc[mi][ni][j] * alpha + bh;
-          const float g = acc[mi][ni + 1][j] * alpha + bg;
-          ep[row * LDE + col] = h * gelu_f(g);
-        }
+      for (int q = 0; q < NT / 2; ++q) {
+        const int np = min(n0 + wn * WN + 2 * q * 16 + fr, N - 17);
+        gbh[q] = bias ? bias[np] : 0.f;
+        gbg[q] = bias ? bias[np + 16] : 0.f;
       }
-  } else {
 #pragma unroll
-    for (int mi = 0; mi < MT; ++mi)
+      for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < NT; ++ni) {
-        const int col = wn * WN + ni * 16 + fr;
-        const int n = n0 + col;
-        const float b = (p.bias && n < N) ? p.bias[n] : 0.f;
+        for (int ni = 0; ni + 1 < NT; ni += 2) {
+          const int col = (wn * WN) / 2 + (ni / 2) * 16 + fr;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = wm * WM + mi * 16 + fg * 4 + j;
-          const int m = m0 + row;
-          float v = acc[mi][ni][j] * alpha + b;
-          if (p.rowbias && m < M && n < N) v += p.rowbias[(long long)(m / p.rows_per_group) * p.rowbias_ld + n];
-          ep[row * LDE + col] = act_f(v, p.act);
+          for (int j = 0; j < 4; ++j) {
+            const int row = wm * WM + mi * 16 + fg * 4 + j;
+            const float h = acc[mi][ni][j] * alpha + gbh[ni / 2];
+            const float g = acc[mi][ni + 1][j] * alpha + gbg[ni / 2];
+            ep[row * LDE + col] = h * gelu_f(g);
+          }
         }
-      }
-  }
+    } else {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) {
+          const int col = wn * WN + ni * 16 + fr;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ep[(wm * WM + mi * 16 + fg * 4 + j) * LDE + col] = acc[mi][ni][j] * alpha;
+        }
+    }
   }  // !kh
   __syncthreads();
 
-  // ---- phase 2: whole-row 16-B vector residual loads and stores (8 outputs per thread per step)
+  // ---- phase 2
   TO* __restrict__ C = (TO*)p.C + bz * p.strideC;
   const TO* __restrict__ R = p.residual ? (const TO*)p.residual + bz * p.strideR : nullptr;
   const int Nout = GEGLU ? N / 2 : N;
   const int n0o = GEGLU ? n0 / 2 : n0;
   const bool vec = (Nout % 8 == 0) && (p.ldc % 8 == 0) && ((((unsigned long long)C) & 15) == 0) &&
-                   (!R || ((p.ldr % 8 == 0) && ((((unsigned long long)R) & 15) == 0)));
+                   (!R || ((p.ldr % 8 == 0) && ((((unsigned long long)R) & 15) == 0))) &&
+                   (GEGLU || !bias || ((((unsigned long long)bias) & 15) == 0)) &&
+                   (GEGLU || !rbias || ((p.rowbias_ld % 4 == 0) && ((((unsigned long long)rbias) & 15) == 0)));
   constexpr int VPR = BNO / 8;
-  for (int e = tid; e < BM * VPR; e += NTHR) {
-    const int r = e / VPR, cv = e - (e / VPR) * VPR;
-    const int m = m0 + r, n = n0o + cv * 8;
-    if (m >= M || n >= Nout) continue;
-    const float* src = ep + r * LDE + cv * 8;
-    float v[8];
-    *(f32x4*)&v[0] = *(const f32x4*)src;
-    *(f32x4*)&v[4] = *(const f32x4*)(src + 4);
-    if (vec && n + 8 <= Nout) {
-      if (R) {
-        typedef __attribute__((ext_vector_type(8))) TO TO8;
-        const TO8 rv = *(const TO8*)(R + (long long)m * p.ldr + n);
+  constexpr int TOT = BM * VPR;
+  constexpr int ITER = (TOT + NTHR - 1) / NTHR;
+  typedef __attribute__((ext_vector_type(8))) TO TO8;
+  if (vec && m0 + BM <= M && n0o + BNO <= Nout) {
+    float v[ITER][8], bv[ITER][8], rv[ITER][8];
+    TO8 res[ITER];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] += (float)rv[i];
+    for (int it = 0; it < ITER; ++it) {
+      const int e = tid + it * NTHR;
+      if (TOT % NTHR == 0 || e < TOT) {
+        const int r = e / VPR, cv = e - (e / VPR) * VPR;
+        const int m = m0 + r, n = n0o + cv * 8;
+        *(f32x4*)&v[it][0] = *(const f32x4*)(ep + r * LDE + cv * 8);
+        *(f32x4*)&v[it][4] = *(const f32x4*)(ep + r * LDE + cv * 8 + 4);
+        if (!GEGLU && bias) {
+          *(f32x4*)&bv[it][0] = *(const f32x4*)(bias + n);
+          *(f32x4*)&bv[it][4] = *(const f32x4*)(bias + n + 4);
+        }
+        if (!GEGLU && rbias) {
+          const float* rb = rbias + (long long)(m / p.rows_per_group) * p.rowbias_ld + n;
+          *(f32x4*)&rv[it][0] = *(const f32x4*)rb;
+          *(f32x4*)&rv[it][4] = *(const f32x4*)(rb + 4);
+        }
+        if (R) res[it] = *(const TO8*)(R + (long long)m * p.ldr + n);
       }
-      typedef __attribute__((ext_vector_type(8))) TO TO8;
-      TO8 o;
+    }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (TO)v[i];
-      *(TO8*)(C + (long long)m * p.ldc + n) = o;
-    } else {
+    for (int it = 0; it < ITER; ++it) {
+      const int e = tid + it * NTHR;
+      if (TOT % NTHR == 0 || e < TOT) {
+        const int r = e / VPR, cv = e - (e / VPR) * VPR;
+        const int m = m0 + r, n = n0o + cv * 8;
+        if (!GEGLU) {
+          if (bias) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] += bv[it][i];
+          }
+          if (rbias) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] += rv[it][i];
+          }
+          if (act == FD_ACT_SILU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = silu_f(v[it][i]);
+          } else if (act == FD_ACT_GELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = gelu_f(v[it][i]);
+          } else if (act == FD_ACT_QUICKGELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = quickgelu_f(v[it][i]);
+          }
+        }
+        if (R) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[it][i] += (float)res[it][i];
+        }
+        TO8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
+        *(TO8*)(C + (long long)m * p.ldc + n) = o;
+      }
+    }
+  } else {  // edge tiles / unaligned operands: scalar, bounds-checked
+    for (int e = tid; e < TOT; e += NTHR) {
+      const int r = e / VPR, cv = e - (e / VPR) * VPR;
+      const int m = m0 + r, n = n0o + cv * 8;
+      if (m >= M || n >= Nout) continue;
       for (int i = 0; i < 8 && n + i < Nout; ++i) {
-        float x = v[i];
+        float x = ep[r * LDE + cv * 8 + i];
+        if (!GEGLU) {
+          if (bias) x += bias[n + i];
+          if (rbias) x += rbias[(long long)(m / p.rows_per_group) * p.rowbias_ld + n + i];
+          x = act_f(x, act);
+        }
         if (R) x += (float)R[(long long)m * p.ldr + n + i];
         C[(long long)m * p.ldc + n + i] = (TO)x;
       }
@@ -329,14 +385,13 @@ static int launch_cfg(const fd_gemm_params* p, hipStream_t s, int swz) {
 
 // Tile choice: cost ~ ceil(tiles / (256 CUs x resident WGs per CU)) x per-tile time; a smaller tile is
 // worth it only when it removes a partial wave.  Relative per-tile efficiencies are estimates.
-// (256x128 / 128x256 tiles with KS = 2 were measured 1.2-2x slower on every UNet shape: 2 waves/SIMD
-//  at 204 VGPRs and 1 WG/CU cannot hide the fragment-read latency that 4 waves/SIMD of 128x128 do.)
-enum { CFG_128x128, CFG_64x160, CFG_128x64, CFG_64x64, CFG_256x128, CFG_AUTO_COUNT = CFG_256x128, CFG_COUNT };
-static const int CFG_BM[] = {128, 64, 128, 64, 256}, CFG_BN[] = {128, 160, 64, 64, 128};
+// (256-row tiles live in gemm8.hip: 8 waves, register-double-buffered fragments, split-K.)
+enum { CFG_128x128, CFG_64x160, CFG_128x64, CFG_64x64, CFG_AUTO_COUNT, CFG_COUNT = CFG_AUTO_COUNT };
+static const int CFG_BM[] = {128, 64, 128, 64}, CFG_BN[] = {128, 160, 64, 64};
 
 static int pick_cfg(const fd_gemm_params* p) {
   const long long b = p->batch > 0 ? p->batch : 1;
-  const double eff[] = {1.00, 0.92, 0.85, 0.60, 1.0};
+  const double eff[] = {1.00, 0.92, 0.85, 0.60};
   int best = CFG_128x128;
   double bestc = 1e30;
   for (int c = 0; c < CFG_AUTO_COUNT; ++c) {
@@ -402,7 +457,6 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
     case CFG_128x128: return dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, ks, g_swz);
     case CFG_64x160: return dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, ks, g_swz);
     case CFG_128x64: return dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, ks, g_swz);
-    case CFG_256x128: return dispatch_ns<T, TO, 256, 128, 128, 64>(p, s, ns, ks, g_swz);
     default: return dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, ks, g_swz);
   }
 }
