@@ -306,7 +306,7 @@ def main():
         "vae_decode_tflops": None if vae_ms is None else round(arch.vae_decode_flops(h, w) / (vae_ms / 1e3) / 1e12, 1),
         "roofline": {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(gemm_tf / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                     "kernel": "gemm_kernel (all MFMA GEMM + implicit-GEMM conv launches of one UNet forward)",
+                     "kernel": "gemm8_kernel + gemm_kernel (all MFMA GEMM + implicit-GEMM conv launches of one UNet forward)",
                      "launches": n_g, "algorithmic_flops": fl_g, "kernel_ms_per_forward": round(ms_g, 3),
                      "avg_launch_us": round(ms_g / n_g * 1e3, 2),
                      "traffic_note": "HBM bytes per forward of these launches (PMC pass)" if traffic else

@@ -9,6 +9,12 @@ from collections import defaultdict
 def short(name):
     m = re.match(r"_Z\d+(\w+?)I", name)
     base = m.group(1) if m else name[:40]
+    if "gemm8_kernel" in name:
+        t = re.search(r"gemm8_kernelI(DF16b|DF16_)Li(\d+)ELi(\d+)ELb(\d)ELb(\d)E", name)
+        if t:
+            dt = "bf16" if t.group(1) == "DF16b" else "f16"
+            kind = "conv" if t.group(4) == "1" else ("geglu" if t.group(5) == "1" else "gemm")
+            return f"gemm8[{kind},{dt},256x{t.group(2)}]"
     if "gemm_kernel" in name:
         t = re.search(r"gemm_kernelI(DF16b|DF16_)Li(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb(\d)ELb(\d)E(\w+?)Ev", name)
         if t:

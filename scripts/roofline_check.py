@@ -13,8 +13,9 @@ def main(trace, bench_log):
     rows = list(csv.DictReader(open(trace)))
     fwd = sum(1 for r in rows if "time_features_kernel" in r["Kernel_Name"] and "DF16b" in r["Kernel_Name"])
     out = {"forwards_in_trace": fwd}
-    for key, pat in (("gemm", "gemm_kernelIDF16b"), ("flash", "flash_attn_d64_kernelIDF16b")):
-        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if pat in r["Kernel_Name"]]
+    for key, pats in (("gemm", ("gemm_kernelIDF16b", "gemm8_kernelIDF16b")), ("flash", ("flash_attn_d64_kernelIDF16b",))):
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows
+             if any(pat in r["Kernel_Name"] for pat in pats)]
         out[key] = {"launches_per_forward": len(d) / fwd, "ms_per_forward": sum(d) / fwd / 1e3,
                     "avg_launch_us": sum(d) / len(d)}
     bench = None
