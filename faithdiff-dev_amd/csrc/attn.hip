@@ -13,13 +13,18 @@
 // softmax_rows: fp32 row softmax for the single-head d=512 VAE mid attention (GEMM + softmax + GEMM).
 #include "fd_common.h"
 
+// amdgpu_waves_per_eu(1, 2): let the compiler use the full 256-VGPR budget of two waves per SIMD instead of
+// capping arch VGPRs at 128 and spilling the O / S accumulators through AGPR moves (192 v_accvgpr per tile).
 template <typename T, int NWV>
-__global__ void __launch_bounds__(64 * NWV) flash_attn_d64_kernel(
+__global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1, 2))) flash_attn_d64_kernel(
     const T* __restrict__ Q, long long ldq, long long qbs, const T* __restrict__ K, long long ldk, long long kbs,
     const T* __restrict__ V, long long ldv, long long vbs, T* __restrict__ O, long long ldo, long long obs,
     int Lq, int Lk, int kv_mod, float scale_log2, int heads, int swz) {
   typedef typename VecT<T>::v8 V8;
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
+  // 3-deep K/V ring: tile t+2 is issued while tile t is consumed (counted vmcnt, raw s_barrier), so each
+  // tile's load has two tiles of compute to land in.
+  constexpr int NBUF = 3;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // 1-D grid; the q-blocks of one (batch, head) are contiguous after the XCD remap, so the head's K/V
@@ -47,6 +52,7 @@ __global__ void __launch_bounds__(64 * NWV) flash_attn_d64_kernel(
   }
 
   const int lrow = lane >> 3, slot = lane & 7;
+  constexpr int PER = 2 * (8 / NWV);  // glds per wave per tile
   auto stage = [&](int t, int buf) {
     unsigned char* sk = smem + buf * 16384;
     unsigned char* sv = sk + 8192;
@@ -73,12 +79,15 @@ __global__ void __launch_bounds__(64 * NWV) flash_attn_d64_kernel(
 
   const int nt = (Lk + 63) / 64;
   stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if (nt > 1) stage(1, 1);
+  if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
+  int buf = 0;
   for (int t = 0; t < nt; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nt) stage(t + 1, buf ^ 1);
+    // buffer (t+2)%3 was last read in iteration t-1, which every wave finished before the barrier
+    if (t + 2 < nt) stage(t + 2, buf == 0 ? 2 : buf - 1);
     const unsigned char* sk = smem + buf * 16384;
     const unsigned char* sv = sk + 8192;
 
@@ -121,21 +130,28 @@ __global__ void __launch_bounds__(64 * NWV) flash_attn_d64_kernel(
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(mrow[qb], mx * scale_log2);
-      const float alpha = exp2f(mrow[qb] - mnew);
       float ls = 0.f;
       float pv[4][4];
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float e = exp2f(st[kb][qb][i] * scale_log2 - mnew);
+          // raw v_exp_f32 (no denormal range fix-up: results below 2^-126 flush to 0, irrelevant to a softmax
+          // numerator already divided by a sum >= 1)
+          const float e = __builtin_amdgcn_exp2f(fmaf(st[kb][qb][i], scale_log2, -mnew));
           pv[kb][i] = e;
           ls += e;
         }
-      lrow_sum[qb] = lrow_sum[qb] * alpha + ls;
-      mrow[qb] = mnew;
+      // exact skip of the O / l rescale when no query of this wave raised its running max (most tiles
+      // after the first few): alpha would be exactly 1
+      if (__any(mnew != mrow[qb])) {
+        const float alpha = __builtin_amdgcn_exp2f(mrow[qb] - mnew);
+        lrow_sum[qb] *= alpha;
 #pragma unroll
-      for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
+        for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
+      }
+      lrow_sum[qb] += ls;
+      mrow[qb] = mnew;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         V8 v;
@@ -173,8 +189,14 @@ __global__ void __launch_bounds__(64 * NWV) flash_attn_d64_kernel(
         o[db][1] = mfma16x16x32(vf, pf[1][s], o[db][1]);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (t + 1 < nt) {
+      // tile t+1 landed (tile t+2, if issued, may still fly); every wave done reading tile t
+      if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+    }
+    buf = buf == 2 ? 0 : buf + 1;
   }
 
   // ---- finalise: lane holds O^T[d = db*16 + 4*fg + j][q = qb*16 + fr]
