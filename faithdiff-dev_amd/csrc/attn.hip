@@ -11,18 +11,25 @@
 //
 // mha_seq_axis: the information transformer's MultiheadAttention over the batch axis (L = CFG pair).
 // softmax_rows: fp32 row softmax for the single-head d=512 VAE mid attention (GEMM + softmax + GEMM).
+#include <type_traits>
+
 #include "fd_common.h"
 
 // amdgpu_waves_per_eu(1, 2): let the compiler use the full 256-VGPR budget of two waves per SIMD instead of
 // capping arch VGPRs at 128 and spilling the O / S accumulators through AGPR moves (192 v_accvgpr per tile).
+#ifndef FD_FLASH_TR_EARLY
+#define FD_FLASH_TR_EARLY 1
+#endif
 template <typename T, int NWV>
 __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1, 2))) flash_attn_d64_kernel(
     const T* __restrict__ Q, long long ldq, long long qbs, const T* __restrict__ K, long long ldk, long long kbs,
     const T* __restrict__ V, long long ldv, long long vbs, T* __restrict__ O, long long ldo, long long obs,
     int Lq, int Lk, int kv_mod, float scale_log2, int heads, int swz) {
   typedef typename VecT<T>::v8 V8;
+  constexpr bool TR_EARLY = FD_FLASH_TR_EARLY;
   // 3-deep K/V ring: tile t+2 is issued while tile t is consumed (counted vmcnt, raw s_barrier), so each
-  // tile's load has two tiles of compute to land in.
+  // tile's load has two tiles of compute to land in.  (A software-pipelined variant -- scores of tile t+1
+  // under tile t's softmax, 4-deep ring -- measured 1.3x slower: 256 VGPRs and 4x the code.)
   constexpr int NBUF = 3;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
   const int lane = threadIdx.x & 63;
@@ -52,23 +59,61 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
   }
 
   const int lrow = lane >> 3, slot = lane & 7;
-  constexpr int PER = 2 * (8 / NWV);  // glds per wave per tile
-  auto stage = [&](int t, int buf) {
-    unsigned char* sk = smem + buf * 16384;
-    unsigned char* sv = sk + 8192;
+  constexpr int LPW = 8 / NWV;       // 8-row pieces of K (and of V) per wave per tile
+  constexpr int PER = 2 * LPW;       // glds per wave per tile
+  // per-lane byte offsets of this lane's K / V source rows inside a 64-key tile (XOR-swizzled 16-B chunk),
+  // against a wave-uniform tile base that advances by 64 rows per tile: global_load_lds in saddr + voffset
+  // form, no per-tile 64-bit address math
+  unsigned koff[LPW], voff[LPW];
 #pragma unroll
-    for (int i = 0; i < 8 / NWV; ++i) {
-      const int row = (i * NWV + wave) * 8 + lrow;
-      int key = t * 64 + row;
-      key = key < Lk ? key : Lk - 1;
-      const int ck = slot ^ ((row >> 1) & 7);
-      const int cv = slot ^ (((row >> 1) & 3) << 1);
-      __builtin_amdgcn_global_load_lds((const void*)(Kb + (long long)key * ldk + ck * 8),
-                                       LDS_PTR(sk + (i * NWV + wave) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(Vb + (long long)key * ldv + cv * 8),
-                                       LDS_PTR(sv + (i * NWV + wave) * 1024), 16, 0, 0);
+  for (int i = 0; i < LPW; ++i) {
+    const int row = (i * NWV + wave) * 8 + lrow;
+    koff[i] = (unsigned)(row * ldk + ((slot ^ ((row >> 1) & 7)) * 8)) * sizeof(T);
+    voff[i] = (unsigned)(row * ldv + ((slot ^ (((row >> 1) & 3) << 1)) * 8)) * sizeof(T);
+  }
+  const int nt = (Lk + 63) / 64;
+  auto stage = [&](int t, int bufi) {
+    unsigned char* sk = smem + bufi * 16384;
+    unsigned char* sv = sk + 8192;
+    if (t * 64 + 64 <= Lk) {
+      const char* kt = (const char*)(Kb + (long long)t * 64 * ldk);
+      const char* vt = (const char*)(Vb + (long long)t * 64 * ldv);
+#pragma unroll
+      for (int i = 0; i < LPW; ++i) {
+        __builtin_amdgcn_global_load_lds((const void*)(kt + koff[i]), LDS_PTR(sk + (i * NWV + wave) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(vt + voff[i]), LDS_PTR(sv + (i * NWV + wave) * 1024), 16, 0, 0);
+      }
+    } else {  // ragged last tile: rows past Lk re-read key Lk-1 (masked out of the softmax)
+#pragma unroll
+      for (int i = 0; i < LPW; ++i) {
+        const int row = (i * NWV + wave) * 8 + lrow;
+        const int key = min(t * 64 + row, Lk - 1);
+        const int ck = slot ^ ((row >> 1) & 7);
+        const int cv = slot ^ (((row >> 1) & 3) << 1);
+        __builtin_amdgcn_global_load_lds((const void*)(Kb + (long long)key * ldk + ck * 8),
+                                         LDS_PTR(sk + (i * NWV + wave) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(Vb + (long long)key * ldv + cv * 8),
+                                         LDS_PTR(sv + (i * NWV + wave) * 1024), 16, 0, 0);
+      }
     }
   };
+
+  // lane-constant LDS read offsets (the buffer, key-block and half offsets are immediates):
+  //   K fragment of (kb, ds): row kb*16 + fr, chunk (ds*4 + fg) ^ ((fr >> 1) & 7)
+  //   V^T transposed read of (db, s, lo/hi): row 32s + 4fg + (fr>>2) (+16), chunk (2db + (pp>>1)) ^ sw
+  int kro[2], vro[4];
+#pragma unroll
+  for (int ds = 0; ds < 2; ++ds) kro[ds] = fr * 128 + (((ds * 4 + fg) ^ ((fr >> 1) & 7)) << 4);
+  {
+    const int q = fr >> 2, pp = lane & 3;
+    const int r0 = 4 * fg + q;
+    const int sw = ((r0 >> 1) & 3) << 1;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const int col = db * 16 + 4 * pp;
+      vro[db] = r0 * 128 + (((col >> 3) ^ sw) << 4) + (col & 7) * 2;
+    }
+  }
 
   f32x4 o[4][2];
 #pragma unroll
@@ -77,44 +122,68 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
     for (int j = 0; j < 2; ++j) o[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float mrow[2] = {-INFINITY, -INFINITY}, lrow_sum[2] = {0.f, 0.f};
 
-  const int nt = (Lk + 63) / 64;
+  typedef f32x4 Sc[4][2];
+  // S^T(tile in buffer BUF) = K Q^T  (16 MFMAs)
+  auto qk = [&](auto bufc, Sc& sd) {
+    constexpr int BUF = decltype(bufc)::value;
+    const unsigned char* sk = smem + BUF * 16384;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      sd[kb][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      sd[kb][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds) {
+        const V8 kf = *(const V8*)(sk + kro[ds] + kb * 2048);
+        sd[kb][0] = mfma16x16x32(kf, qf[0][ds], sd[kb][0]);
+        sd[kb][1] = mfma16x16x32(kf, qf[1][ds], sd[kb][1]);
+      }
+    }
+  };
+
+  // V^T fragments of the tile in buffer BUF: inline asm, because hipcc treats the ds_read_tr builtin as
+  // aliasing every in-flight LDS-DMA and drains vmcnt(0) in front of it (waiting out the K/V prefetch);
+  // the asm reads are retired by an explicit lgkmcnt(0) + sched_barrier before the P.V MFMAs
+  auto read_vtr = [&](auto bufc, s16x4 (&vtr)[4][2][2]) {
+    constexpr int BUF = decltype(bufc)::value;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const unsigned va = (unsigned)(unsigned long)(LDS_PTR(smem + vro[db]));
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[db][s2][0]) : "v"(va),
+                     "i"(BUF * 16384 + 8192 + s2 * 4096));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[db][s2][1]) : "v"(va),
+                     "i"(BUF * 16384 + 8192 + s2 * 4096 + 2048));
+      }
+    }
+  };
+  const int nfull = Lk / 64;  // tiles with no key past Lk
   stage(0, 0);
   if (nt > 1) stage(1, 1);
   if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  int buf = 0;
-  for (int t = 0; t < nt; ++t) {
-    // buffer (t+2)%3 was last read in iteration t-1, which every wave finished before the barrier
-    if (t + 2 < nt) stage(t + 2, buf == 0 ? 2 : buf - 1);
-    const unsigned char* sk = smem + buf * 16384;
-    const unsigned char* sv = sk + 8192;
-
-    // ---- S^T = K Q^T
-    f32x4 st[4][2];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      st[kb][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      st[kb][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      const int r = kb * 16 + fr;
-#pragma unroll
-      for (int ds = 0; ds < 2; ++ds) {
-        const V8 kf = *(const V8*)(sk + r * 128 + (((ds * 4 + fg) ^ ((r >> 1) & 7)) << 4));
-        st[kb][0] = mfma16x16x32(kf, qf[0][ds], st[kb][0]);
-        st[kb][1] = mfma16x16x32(kf, qf[1][ds], st[kb][1]);
-      }
-    }
-    // ---- mask the key tail
-    if (t * 64 + 64 > Lk) {
+  // one 64-key tile in ring buffer BUF (compile-time, so every LDS address is base + immediate);
+  // MASK: the ragged last tile (keys >= Lk scored -inf)
+  auto iter = [&](auto bufc, auto maskc, int t) {
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr bool MASK = decltype(maskc)::value;
+    // buffer (BUF+2)%3 was last read in the previous tile, which every wave finished before the barrier
+    if (t + 2 < nt) stage(t + 2, (BUF + 2) % 3);
+    Sc sc;
+    qk(bufc, sc);
+    s16x4 vtr[4][2][2];
+    if (TR_EARLY) read_vtr(bufc, vtr);  // V^T reads in flight under the softmax VALU
+    if (MASK) {
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key = t * 64 + kb * 16 + fg * 4 + i;
           if (key >= Lk) {
-            st[kb][0][i] = -INFINITY;
-            st[kb][1][i] = -INFINITY;
+            sc[kb][0][i] = -INFINITY;
+            sc[kb][1][i] = -INFINITY;
           }
         }
     }
@@ -126,7 +195,7 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[kb][qb][i]);
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[kb][qb][i]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(mrow[qb], mx * scale_log2);
@@ -138,7 +207,7 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
         for (int i = 0; i < 4; ++i) {
           // raw v_exp_f32 (no denormal range fix-up: results below 2^-126 flush to 0, irrelevant to a softmax
           // numerator already divided by a sum >= 1)
-          const float e = __builtin_amdgcn_exp2f(fmaf(st[kb][qb][i], scale_log2, -mnew));
+          const float e = __builtin_amdgcn_exp2f(fmaf(sc[kb][qb][i], scale_log2, -mnew));
           pv[kb][i] = e;
           ls += e;
         }
@@ -153,40 +222,30 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
       lrow_sum[qb] += ls;
       mrow[qb] = mnew;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s2 = 0; s2 < 2; ++s2) {
         V8 v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          v[i] = (T)pv[2 * s][i];
-          v[4 + i] = (T)pv[2 * s + 1][i];
+          v[i] = (T)pv[2 * s2][i];
+          v[4 + i] = (T)pv[2 * s2 + 1][i];
         }
-        pf[qb][s] = v;
+        pf[qb][s2] = v;
       }
     }
     // ---- O^T += V^T P^T   (A = V^T via transposed LDS reads)
+    if (!TR_EARLY) read_vtr(bufc, vtr);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        s16x4 lo, hi;
-        {
-          const int q = fr >> 2, pp = lane & 3;
-          const int col = db * 16 + 4 * pp;
-          const int r0 = 32 * s + 4 * fg + q, r1 = r0 + 16;
-          const int ch = col >> 3, boff = (col & 7) * 2;
-          const int a0 = r0 * 128 + ((ch ^ (((r0 >> 1) & 3) << 1)) << 4) + boff;
-          const int a1 = r1 * 128 + ((ch ^ (((r1 >> 1) & 3) << 1)) << 4) + boff;
-          lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(sv + a0));
-          hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(sv + a1));
-        }
-        V8 vf;
-        {
-          typedef __attribute__((ext_vector_type(8))) short s16x8;
-          s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          vf = __builtin_bit_cast(V8, w);
-        }
-        o[db][0] = mfma16x16x32(vf, pf[0][s], o[db][0]);
-        o[db][1] = mfma16x16x32(vf, pf[1][s], o[db][1]);
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const s16x4 lo = vtr[db][s2][0], hi = vtr[db][s2][1];
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        const s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const V8 vf = __builtin_bit_cast(V8, w);
+        o[db][0] = mfma16x16x32(vf, pf[0][s2], o[db][0]);
+        o[db][1] = mfma16x16x32(vf, pf[1][s2], o[db][1]);
       }
     }
     if (t + 1 < nt) {
@@ -196,7 +255,26 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_s_barrier();
     }
-    buf = buf == 2 ? 0 : buf + 1;
+  };
+  typedef std::integral_constant<int, 0> B0;
+  typedef std::integral_constant<int, 1> B1;
+  typedef std::integral_constant<int, 2> B2;
+  typedef std::integral_constant<bool, false> NM;
+  typedef std::integral_constant<bool, true> YM;
+  int t = 0;
+  for (; t + 3 <= nfull; t += 3) {
+    iter(B0(), NM(), t);
+    iter(B1(), NM(), t + 1);
+    iter(B2(), NM(), t + 2);
+  }
+  // the remaining 0-2 full tiles and the ragged tail (buffer index t % 3 continues the ring)
+  for (; t < nt; ++t) {
+    const bool m = t >= nfull;
+    switch (t % 3) {
+      case 0: if (m) iter(B0(), YM(), t); else iter(B0(), NM(), t); break;
+      case 1: if (m) iter(B1(), YM(), t); else iter(B1(), NM(), t); break;
+      default: if (m) iter(B2(), YM(), t); else iter(B2(), NM(), t); break;
+    }
   }
 
   // ---- finalise: lane holds O^T[d = db*16 + 4*fg + j][q = qb*16 + fr]

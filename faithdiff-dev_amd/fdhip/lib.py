@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfaithdiff_hip.so")
+# FD_LIB_PATH (benchmarks only): an alternative build of the same library for in-session A/B timing
+LIB_PATH = os.environ.get("FD_LIB_PATH") or os.path.join(_HERE, "libfaithdiff_hip.so")
 
 FD_BF16, FD_F16, FD_F32 = 0, 1, 2
 ACT = {"none": 0, "silu": 1, "gelu": 2, "quickgelu": 3, "geglu": 4}
