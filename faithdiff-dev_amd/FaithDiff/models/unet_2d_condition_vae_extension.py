@@ -124,7 +124,9 @@ class UNet2DConditionModel:
         self._hip = None
 
     def quantize_8bit(self):
-        """utils/system.py:13-32 analogue: fp8 e4m3 weight storage for the UNet (encoder stays fp16)."""
+        """utils/system.py:13-32: every UNet parameter (core + extras, incl. norms and biases) becomes unscaled
+        float8_e4m3fn; compute stays 16-bit (bf16 here, fp16 under the reference's autocast).  The denoise
+        encoder stays fp16 (:24-26).  See fdhip.arch.quantize_e4m3."""
         self._fp8 = True
         self._hip = None
 
@@ -159,7 +161,8 @@ class UNet2DConditionModel:
             from fdhip.unet import HipUNet
             cdt = torch.bfloat16 if self._dtype in (torch.float32, torch.bfloat16, torch.float8_e4m3fn) \
                 else self._dtype
-            self._hip = HipUNet(self._sd, self._device, cdt)
+            sd = arch.quantize_e4m3(self._sd) if self._fp8 else self._sd
+            self._hip = HipUNet(sd, self._device, cdt)
         return self._hip
 
     def release_host_weights(self):

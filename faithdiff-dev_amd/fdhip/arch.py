@@ -194,6 +194,16 @@ def random_init(shapes, seed=0, device="cpu", dtype=torch.float32, gain=1.0):
     return sd
 
 
+def quantize_e4m3(sd):
+    """utils/system.py:13-32 (quantize_8bit) semantics: ``unet.to(torch.float8_e4m3fn)`` casts EVERY floating
+    parameter of the UNet -- core, FaithDiff extras, norm weights and biases -- to OCP e4m3 with no scale
+    (round to nearest even; |x| > 448 is not representable and becomes NaN, as in torch); the pipeline then
+    computes at 16 bit under autocast, i.e. on the e4m3 values widened exactly.  Returns those widened
+    values in fp32 (e4m3 is a subset of bf16, so the HIP UNet stores them without a second rounding).
+    The denoise encoder is not part of ``sd`` here; the reference keeps it fp16 (:24-26)."""
+    return {k: (v.to(torch.float8_e4m3fn).to(torch.float32) if v.is_floating_point() else v) for k, v in sd.items()}
+
+
 def count(shapes):
     n = 0
     for s in shapes.values():

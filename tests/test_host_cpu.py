@@ -151,3 +151,24 @@ def test_synthetic_text_encoder_deterministic():
     assert a.shape == (1, 77, 2048) and pa.shape == (1, 1280)
     assert torch.equal(a, b) and torch.equal(pa, pb) and not torch.equal(a, c)
     assert c.abs().sum() > 0  # "" is encoded, not zeroed (pipeline:622-675)
+
+
+def test_quantize_e4m3_semantics():
+    """a18: quantize_8bit = torch's float8_e4m3fn cast of every UNet parameter (RNE, no scale, NaN past 448),
+    widened exactly; integers untouched.  The drop-in's use_fp8 flag routes the UNet through it."""
+    import torch
+    from fdhip import arch
+    x = torch.tensor([0.1, 447.9, 1000.0, 1e-4, -3.3, 2.0 ** -9, 0.0])
+    q = arch.quantize_e4m3({"w": x, "i": torch.tensor([3])})
+    assert torch.equal(q["i"], torch.tensor([3]))
+    exp = x.to(torch.float8_e4m3fn).to(torch.float32)
+    assert torch.equal(torch.nan_to_num(q["w"], nan=-1.0), torch.nan_to_num(exp, nan=-1.0))
+    assert torch.isnan(q["w"][2]) and q["w"][3] == 0 and q["w"][5] == 2.0 ** -9
+    # every e4m3 value is exact in bf16 (the HIP UNet stores them without a second rounding)
+    allv = torch.arange(256, dtype=torch.uint8).view(torch.float8_e4m3fn).to(torch.float32)
+    fin = allv[torch.isfinite(allv)]
+    assert torch.equal(fin.to(torch.bfloat16).to(torch.float32), fin)
+    from FaithDiff.models.unet_2d_condition_vae_extension import UNet2DConditionModel
+    u = UNet2DConditionModel({})
+    u.quantize_8bit()
+    assert u._fp8
