@@ -33,7 +33,7 @@ def FaithDiff_pipeline(sdxl_path, VAE_FP16_path, FaithDiff_path, use_fp8=False, 
     unet.to(dtype=unet_dtype)
     pipe = FaithDiffStableDiffusionXLPipeline.from_pretrained(
         sdxl_path, vae=vae, add_sample=True, denoise_encoder=unet.denoise_encoder, DDPM_scheduler=DDPMScheduler(),
-        add_watermarker=False, torch_dtype=dtype, variant="fp16", unet=unet)
+        add_watermarker=False, torch_dtype=dtype, variant="fp16", unet=unet, seed=seed)
     pipe.unet = unet
     return pipe
 

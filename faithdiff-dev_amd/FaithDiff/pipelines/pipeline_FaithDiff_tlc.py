@@ -92,16 +92,27 @@ class FaithDiffStableDiffusionXLPipeline:
     # ------------------------------------------------------------------ construction
     @classmethod
     def from_pretrained(cls, sdxl_path, vae=None, denoise_encoder=None, DDPM_scheduler=None, add_sample=True,
-                        add_watermarker=False, torch_dtype=None, variant=None, unet=None, **kwargs):
+                        add_watermarker=False, torch_dtype=None, variant=None, unet=None, seed=0, **kwargs):
+        """Like diffusers' from_pretrained of the SDXL directory: the two CLIP text encoders and tokenizers come
+        from ``sdxl_path`` (text_encoder/, text_encoder_2/, tokenizer/, tokenizer_2/; 'random-init' = seeded
+        weights of the real architecture + the framing-only fallback tokenizer), unless passed in."""
+        from ..models.clip_text import CLIPTextModel, CLIPTextModelWithProjection, load_tokenizer
+        te = kwargs.get("text_encoder") or CLIPTextModel.from_pretrained(sdxl_path, "text_encoder", seed=seed + 11)
+        te2 = kwargs.get("text_encoder_2") or CLIPTextModelWithProjection.from_pretrained(sdxl_path, "text_encoder_2",
+                                                                                           seed=seed + 13)
+        tok = kwargs.get("tokenizer") or load_tokenizer(sdxl_path, "tokenizer", pad_token_id=49407)
+        tok2 = kwargs.get("tokenizer_2") or load_tokenizer(sdxl_path, "tokenizer_2", pad_token_id=0)
         return cls(vae=vae, denoise_encoder=denoise_encoder, unet=unet, scheduler=EulerDiscreteScheduler(),
-                   DDPM_scheduler=DDPM_scheduler or DDPMScheduler(), add_watermarker=add_watermarker)
+                   DDPM_scheduler=DDPM_scheduler or DDPMScheduler(), add_watermarker=add_watermarker,
+                   text_encoder=te, text_encoder_2=te2, tokenizer=tok, tokenizer_2=tok2)
 
     def to(self, device=None, dtype=None):
         dev = torch.device(device) if device is not None else self.device
         if dev.type == "cuda" and dev.index is not None:
             torch.cuda.set_device(dev)
         self.device = dev
-        for m in (self.vae, self.denoise_encoder, self.unet):
+        for m in (self.vae, self.denoise_encoder, self.unet, self.text_encoder_2,
+                  None if isinstance(self.text_encoder, SyntheticTextEncoder) else self.text_encoder):
             if m is not None:
                 m.to(device=dev)
         return self
@@ -173,20 +184,64 @@ class FaithDiffStableDiffusionXLPipeline:
                       do_classifier_free_guidance=True, negative_prompt=None, negative_prompt_2=None,
                       prompt_embeds=None, negative_prompt_embeds=None, pooled_prompt_embeds=None,
                       negative_pooled_prompt_embeds=None, lora_scale=None, clip_skip=None):
-        """:485-717 contract; text features from the synthetic encoder unless embeddings are passed."""
+        """:485-717.  With the two CLIP encoders (HIP, FaithDiff/models/clip_text.py): tokenize each prompt with
+        its tokenizer (max_length 77, truncation), keep hidden_states[-2] (or -(clip_skip + 2)) of both and concat
+        (:587-615), the pooled output is text_encoder_2's projected EOS row (:608); the negative prompt ("" when
+        None and force_zeros is off) is *encoded* the same way (:622-675).  Without them (pipelines built around
+        pre-computed embeddings) the seeded synthetic stand-in is used."""
+        if self.text_encoder_2 is None:
+            if prompt_embeds is None:
+                if isinstance(prompt, list):
+                    prompt = prompt[0]
+                prompt_embeds, pooled_prompt_embeds = self.text_encoder(prompt)
+            zero_out = negative_prompt is None and self.config.force_zeros_for_empty_prompt
+            if do_classifier_free_guidance and negative_prompt_embeds is None and zero_out:
+                negative_prompt_embeds = torch.zeros_like(prompt_embeds)
+                negative_pooled_prompt_embeds = torch.zeros_like(pooled_prompt_embeds)
+            elif do_classifier_free_guidance and negative_prompt_embeds is None:
+                neg = negative_prompt or ""
+                if isinstance(neg, list):
+                    neg = neg[0]
+                negative_prompt_embeds, negative_pooled_prompt_embeds = self.text_encoder(neg)
+            return prompt_embeds, negative_prompt_embeds, pooled_prompt_embeds, negative_pooled_prompt_embeds
+
+        tokenizers = [self.tokenizer, self.tokenizer_2] if self.tokenizer is not None else [self.tokenizer_2]
+        encoders = [self.text_encoder, self.text_encoder_2] if self.tokenizer is not None else [self.text_encoder_2]
+        prompt = [prompt] if isinstance(prompt, str) else prompt
+        batch_size = len(prompt) if prompt is not None else prompt_embeds.shape[0]
+
+        def run(texts_per_encoder, skip):
+            embs, pooled = [], None
+            for texts, tok, enc in zip(texts_per_encoder, tokenizers, encoders):
+                ids = tok(texts, padding="max_length", max_length=tok.model_max_length, truncation=True,
+                          return_tensors="pt").input_ids
+                out = enc(ids, output_hidden_states=True)
+                pooled = out[0]  # only the final encoder's pooled output is kept (:607-608)
+                embs.append(out.hidden_states[-2] if skip is None else out.hidden_states[-(skip + 2)])
+            return torch.cat(embs, dim=-1), pooled
+
         if prompt_embeds is None:
-            if isinstance(prompt, list):
-                prompt = prompt[0]
-            prompt_embeds, pooled_prompt_embeds = self.text_encoder(prompt)
+            prompt_2 = prompt_2 or prompt
+            prompt_2 = [prompt_2] if isinstance(prompt_2, str) else prompt_2
+            prompt_embeds, pooled_prompt_embeds = run([prompt, prompt_2], clip_skip)
         zero_out = negative_prompt is None and self.config.force_zeros_for_empty_prompt
         if do_classifier_free_guidance and negative_prompt_embeds is None and zero_out:
             negative_prompt_embeds = torch.zeros_like(prompt_embeds)
             negative_pooled_prompt_embeds = torch.zeros_like(pooled_prompt_embeds)
         elif do_classifier_free_guidance and negative_prompt_embeds is None:
-            neg = negative_prompt or ""
-            if isinstance(neg, list):
-                neg = neg[0]
-            negative_prompt_embeds, negative_pooled_prompt_embeds = self.text_encoder(neg)
+            negative_prompt = negative_prompt or ""
+            negative_prompt_2 = negative_prompt_2 or negative_prompt
+            negative_prompt = batch_size * [negative_prompt] if isinstance(negative_prompt, str) else negative_prompt
+            negative_prompt_2 = (batch_size * [negative_prompt_2] if isinstance(negative_prompt_2, str)
+                                 else negative_prompt_2)
+            if prompt is not None and type(prompt) is not type(negative_prompt):
+                raise TypeError(f"`negative_prompt` should be the same type to `prompt`, but got "
+                                f"{type(negative_prompt)} != {type(prompt)}.")
+            if batch_size != len(negative_prompt):
+                raise ValueError(f"`negative_prompt`: {negative_prompt} has batch size {len(negative_prompt)}, but "
+                                 f"`prompt`: {prompt} has batch size {batch_size}. Please make sure that passed "
+                                 "`negative_prompt` matches the batch size of `prompt`.")
+            negative_prompt_embeds, negative_pooled_prompt_embeds = run([negative_prompt, negative_prompt_2], None)
         return prompt_embeds, negative_prompt_embeds, pooled_prompt_embeds, negative_pooled_prompt_embeds
 
     def check_inputs(self, lr_img, prompt, prompt_2, height, width, callback_steps, negative_prompt=None,

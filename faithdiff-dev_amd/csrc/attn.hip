@@ -24,7 +24,7 @@ template <typename T, int NWV>
 __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1, 2))) flash_attn_d64_kernel(
     const T* __restrict__ Q, long long ldq, long long qbs, const T* __restrict__ K, long long ldk, long long kbs,
     const T* __restrict__ V, long long ldv, long long vbs, T* __restrict__ O, long long ldo, long long obs,
-    int Lq, int Lk, int kv_mod, float scale_log2, int heads, int swz) {
+    int Lq, int Lk, int kv_mod, int causal, float scale_log2, int heads, int swz) {
   typedef typename VecT<T>::v8 V8;
   constexpr bool TR_EARLY = FD_FLASH_TR_EARLY;
   // 3-deep K/V ring: tile t+2 is issued while tile t is consumed (counted vmcnt, raw s_barrier), so each
@@ -181,8 +181,11 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key = t * 64 + kb * 16 + fg * 4 + i;
-          if (key >= Lk) {
+          // ragged tail; causal (CLIP text encoders): query q0 + qb*16 + fr sees keys <= itself
+          if (key >= Lk || (causal && key > q0 + fr)) {
             sc[kb][0][i] = -INFINITY;
+          }
+          if (key >= Lk || (causal && key > q0 + 16 + fr)) {
             sc[kb][1][i] = -INFINITY;
           }
         }
@@ -262,14 +265,14 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
   typedef std::integral_constant<bool, false> NM;
   typedef std::integral_constant<bool, true> YM;
   int t = 0;
-  for (; t + 3 <= nfull; t += 3) {
+  for (; !causal && t + 3 <= nfull; t += 3) {
     iter(B0(), NM(), t);
     iter(B1(), NM(), t + 1);
     iter(B2(), NM(), t + 2);
   }
   // the remaining 0-2 full tiles and the ragged tail (buffer index t % 3 continues the ring)
   for (; t < nt; ++t) {
-    const bool m = t >= nfull;
+    const bool m = causal || t >= nfull;
     switch (t % 3) {
       case 0: if (m) iter(B0(), YM(), t); else iter(B0(), NM(), t); break;
       case 1: if (m) iter(B1(), YM(), t); else iter(B1(), NM(), t); break;
@@ -300,8 +303,8 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
 
 extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const void* k, long long ldk,
                                    long long kbs, const void* v, long long ldv, long long vbs, void* o, long long ldo,
-                                   long long obs, int batch, int heads, int Lq, int Lk, int kv_mod, float scale,
-                                   int dtype, void* stream) {
+                                   long long obs, int batch, int heads, int Lq, int Lk, int kv_mod, int causal,
+                                   float scale, int dtype, void* stream) {
   if (!q || !k || !v || !o) return FD_ERR_ARG;
   if (batch <= 0 || heads <= 0 || Lq <= 0 || Lk <= 0 || kv_mod < 0) return FD_ERR_SHAPE;
   if ((ldq | ldk | ldv | ldo) & 7) return FD_ERR_SHAPE;
@@ -321,11 +324,11 @@ extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const 
   if (nwv == 4) {
     FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, 4>), grid, block, 0, s, (const T*)q, ldq, qbs,
                                             (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk,
-                                            kv_mod, sl2, heads, swz));
+                                            kv_mod, causal, sl2, heads, swz));
   } else {
     FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, 2>), grid, block, 0, s, (const T*)q, ldq, qbs,
                                             (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk,
-                                            kv_mod, sl2, heads, swz));
+                                            kv_mod, causal, sl2, heads, swz));
   }
   FD_LAUNCH_CHECK();
   return FD_OK;

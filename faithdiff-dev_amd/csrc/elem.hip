@@ -633,3 +633,37 @@ extern "C" int fd_device_check(void) {
 }
 
 extern "C" const char* fd_version(void) { return "libfaithdiff_hip 0.1 gfx950"; }
+
+// ------------------------------------------------------------------------------------------------
+// CLIP text embeddings (transformers CLIPTextEmbeddings, called from encode_prompt, pipeline:587-598):
+// out[b*L + l][:] = tok[ids[b*L + l]][:] + pos[l][:]   (tables in the compute dtype, sum in fp32).
+// One thread per 8 channels (16-B loads / store).
+template <typename T>
+__global__ void embed_tokens_kernel(const int* __restrict__ ids, const T* __restrict__ tok, const T* __restrict__ pos,
+                                    T* __restrict__ out, int rows, int L, int D, int vocab) {
+  typedef typename VecT<T>::v8 V8;
+  const int per = D / 8;
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)rows * per) return;
+  const int r = e / per, c = (e - (long long)r * per) * 8;
+  int id = ids[r];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
+  const V8 a = *(const V8*)(tok + (long long)id * D + c);
+  const V8 p = *(const V8*)(pos + (long long)(r % L) * D + c);
+  V8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (T)((float)a[i] + (float)p[i]);
+  *(V8*)(out + (long long)r * D + c) = o;
+}
+
+extern "C" int fd_embed_tokens(const int* ids, const void* tok, const void* pos, void* out, int batch, int L, int D,
+                               int vocab, int dtype, void* stream) {
+  if (!ids || !tok || !pos || !out) return FD_ERR_ARG;
+  if (batch <= 0 || L <= 0 || D <= 0 || (D % 8) || vocab <= 0) return FD_ERR_SHAPE;
+  const long long total = (long long)batch * L * (D / 8);
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(embed_tokens_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                                          s, ids, (const T*)tok, (const T*)pos, (T*)out, batch * L, L, D, vocab));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}

@@ -179,7 +179,7 @@ def random_init(shapes, seed=0, device="cpu", dtype=torch.float32, gain=1.0):
         g = torch.Generator(device=device).manual_seed((zlib.crc32(name.encode()) ^ (seed * 0x9E3779B1)) & 0x7FFFFFFF)
         u = torch.rand(shape, generator=g, device=device, dtype=torch.float32) * 2 - 1
         is_norm = (".norm" in name or ".ln_" in name or name.startswith("conv_norm_out") or "group_norm" in name
-                   or "norm_in" in name or "conv_norm_out" in name)
+                   or "norm_in" in name or "conv_norm_out" in name or "layer_norm" in name)
         if len(shape) == 1:
             if is_norm and name.endswith("weight"):
                 t = 1.0 + 0.1 * u
@@ -192,6 +192,36 @@ def random_init(shapes, seed=0, device="cpu", dtype=torch.float32, gain=1.0):
             t = u * (gain / fan_in ** 0.5)
         sd[name] = t.to(dtype)
     return sd
+
+
+# SDXL text encoders (diffusers StableDiffusionXLPipeline: text_encoder = CLIPTextModel ViT-L/14,
+# text_encoder_2 = CLIPTextModelWithProjection OpenCLIP ViT-bigG/14), transformers config fields.
+CLIP_L = dict(vocab=49408, D=768, layers=12, heads=12, inter=3072, act="quickgelu", proj=None, max_pos=77)
+CLIP_G = dict(vocab=49408, D=1280, layers=32, heads=20, inter=5120, act="gelu", proj=1280, max_pos=77)
+
+
+def clip_param_shapes(cfg):
+    """transformers CLIPTextModel / CLIPTextModelWithProjection state-dict keys (real weights load as-is)."""
+    D, I = cfg["D"], cfg["inter"]
+    d = {"text_model.embeddings.token_embedding.weight": (cfg["vocab"], D),
+         "text_model.embeddings.position_embedding.weight": (cfg["max_pos"], D)}
+    for i in range(cfg["layers"]):
+        p = f"text_model.encoder.layers.{i}"
+        for n in ("q_proj", "k_proj", "v_proj", "out_proj"):
+            d[f"{p}.self_attn.{n}.weight"] = (D, D)
+            d[f"{p}.self_attn.{n}.bias"] = (D,)
+        for n in ("layer_norm1", "layer_norm2"):
+            d[f"{p}.{n}.weight"] = (D,)
+            d[f"{p}.{n}.bias"] = (D,)
+        d[f"{p}.mlp.fc1.weight"] = (I, D)
+        d[f"{p}.mlp.fc1.bias"] = (I,)
+        d[f"{p}.mlp.fc2.weight"] = (D, I)
+        d[f"{p}.mlp.fc2.bias"] = (D,)
+    d["text_model.final_layer_norm.weight"] = (D,)
+    d["text_model.final_layer_norm.bias"] = (D,)
+    if cfg["proj"]:
+        d["text_projection.weight"] = (cfg["proj"], D)
+    return d
 
 
 def quantize_e4m3(sd):

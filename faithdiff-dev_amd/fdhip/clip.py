@@ -1,0 +1,85 @@
+"""SDXL's two CLIP text encoders on the HIP kernel library.
+
+encode_prompt (pipeline_FaithDiff_tlc.py:485-717) runs CLIP ViT-L/14 (CLIPTextModel) and OpenCLIP ViT-bigG/14
+(CLIPTextModelWithProjection) on 77 token ids and keeps hidden_states[-2] of each (concat -> 2048 channels)
+plus the projected pooled output of the second (:608-613).  The algorithm is transformers' CLIPTextTransformer
+(transformers==4.46.1, reference requirements.txt:3): token + position embedding; per layer a pre-LN causal
+self-attention (q/k/v/out with bias, head dim 64, scale 1/8) and a pre-LN MLP fc1 -> act (quick_gelu for L,
+gelu for bigG) -> fc2, both residual; final LayerNorm; pooled = final-LN row at argmax(input_ids) (the
+legacy eos_token_id == 2 path of both SDXL configs; EOS 49407 is the largest id, so this is the first EOS);
+text_projection without bias.  Each Linear is one fd_gemm (bias / activation / residual in the epilogue), the
+attention one causal fd_flash_attn, the embeddings one fd_embed_tokens; activations bf16 (the reference: fp16).
+"""
+import torch
+
+from . import arch
+from . import lib as L
+from . import ops
+
+
+class HipCLIPTextModel:
+    def __init__(self, sd, cfg, device="cuda", dtype=torch.bfloat16):
+        L.require_device()
+        self.cfg, self.device, self.dtype = dict(cfg), torch.device(device), dtype
+        W = lambda k: sd[k].to(device=self.device, dtype=dtype).contiguous()  # noqa: E731
+        Fp = lambda k: sd[k].to(device=self.device, dtype=torch.float32).contiguous()  # noqa: E731
+        self.tok = W("text_model.embeddings.token_embedding.weight")
+        self.pos = W("text_model.embeddings.position_embedding.weight")
+        self.layers = []
+        for i in range(cfg["layers"]):
+            q = f"text_model.encoder.layers.{i}"
+            p = f"{q}.self_attn"
+            self.layers.append(dict(
+                ln1=(Fp(f"{q}.layer_norm1.weight"), Fp(f"{q}.layer_norm1.bias")),
+                qkv=torch.cat([sd[f"{p}.{n}_proj.weight"] for n in "qkv"], 0).to(self.device, dtype).contiguous(),
+                qkv_b=torch.cat([sd[f"{p}.{n}_proj.bias"] for n in "qkv"], 0).to(self.device,
+                                                                                 torch.float32).contiguous(),
+                out=(W(f"{p}.out_proj.weight"), Fp(f"{p}.out_proj.bias")),
+                ln2=(Fp(f"{q}.layer_norm2.weight"), Fp(f"{q}.layer_norm2.bias")),
+                fc1=(W(f"{q}.mlp.fc1.weight"), Fp(f"{q}.mlp.fc1.bias")),
+                fc2=(W(f"{q}.mlp.fc2.weight"), Fp(f"{q}.mlp.fc2.bias"))))
+        self.fln = (Fp("text_model.final_layer_norm.weight"), Fp("text_model.final_layer_norm.bias"))
+        self.proj = W("text_projection.weight") if cfg.get("proj") else None
+
+    @torch.no_grad()
+    def forward(self, input_ids):
+        """input_ids [B, T] (any int dtype, host or device).  Returns a dict: hidden_states (list of [B, T, D] in
+        the compute dtype: the embeddings, then each layer's output, as transformers' output_hidden_states),
+        last_hidden_state, pooled ([B, D], final-LN EOS row), text_embeds ([B, proj] with a projection)."""
+        ids = torch.as_tensor(input_ids)
+        B, T = ids.shape
+        D = self.cfg["D"]
+        H = D // 64
+        eos = ids.argmax(dim=-1).tolist()
+        ids_d = ids.to(device=self.device, dtype=torch.int32).contiguous().reshape(-1)
+        M = B * T
+        h = torch.empty((M, D), dtype=self.dtype, device=self.device)
+        ops.embed_tokens(ids_d, self.tok, self.pos, h, B, T)
+        hidden = [h.reshape(B, T, D)]
+        n = torch.empty_like(h)
+        qkv = torch.empty((M, 3 * D), dtype=self.dtype, device=self.device)
+        att = torch.empty_like(h)
+        act = "quickgelu" if self.cfg["act"] == "quickgelu" else "gelu"
+        for lay in self.layers:
+            h = h.clone()  # every layer's output is kept (hidden_states)
+            ops.layer_norm(h, *lay["ln1"], 1e-5, out=n)
+            ops.gemm(n, lay["qkv"], bias=lay["qkv_b"], out=qkv)
+            ops.flash_attn(qkv, qkv[:, D:], qkv[:, 2 * D:], att, B, H, T, T, 3 * D, 3 * D, 3 * D, D,
+                           T * 3 * D, T * 3 * D, T * 3 * D, T * D, kv_mod=0, scale=0.125, causal=True)
+            ops.gemm(att, lay["out"][0], bias=lay["out"][1], residual=h, out=h)
+            ops.layer_norm(h, *lay["ln2"], 1e-5, out=n)
+            m = ops.gemm(n, lay["fc1"][0], bias=lay["fc1"][1], act=act)
+            ops.gemm(m, lay["fc2"][0], bias=lay["fc2"][1], residual=h, out=h)
+            hidden.append(h.reshape(B, T, D))
+        last = torch.empty_like(h)
+        ops.layer_norm(h, *self.fln, 1e-5, out=last)
+        pooled = torch.stack([last[b * T + eos[b]] for b in range(B)], 0).contiguous()
+        out = dict(hidden_states=hidden, last_hidden_state=last.reshape(B, T, D), pooled=pooled)
+        if self.proj is not None:
+            out["text_embeds"] = ops.gemm(pooled, self.proj)
+        return out
+
+
+def random_clip(cfg, seed, device="cpu"):
+    """Seeded random-init state dict of the real architecture (no weights offline)."""
+    return arch.random_init(arch.clip_param_shapes(cfg), seed=seed, device=device)

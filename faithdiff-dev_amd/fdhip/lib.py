@@ -47,7 +47,8 @@ _SIGS = {
     "fd_group_norm": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_int, c_int, c_vp, c_vp]),
     "fd_layer_norm": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp]),
     "fd_flash_attn": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_int, c_int,
-                              c_int, c_int, c_int, c_f, c_int, c_vp]),
+                              c_int, c_int, c_int, c_int, c_f, c_int, c_vp]),
+    "fd_embed_tokens": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "fd_mha_seq_axis": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "fd_softmax_rows": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_f, c_int, c_vp]),
     "fd_concat_channels": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_ll, c_int, c_vp]),

@@ -237,12 +237,21 @@ def layer_norm(x, gamma, beta, eps=1e-5, out=None, M=None, ldx=None):
 
 
 # --------------------------------------------------------------------------------------- attention
-def flash_attn(q, k, v, out, batch, heads, Lq, Lk, ldq, ldk, ldv, ldo, qbs, kbs, vbs, obs, kv_mod=0, scale=0.125):
+def flash_attn(q, k, v, out, batch, heads, Lq, Lk, ldq, ldk, ldv, ldo, qbs, kbs, vbs, obs, kv_mod=0, scale=0.125,
+               causal=False):
     _timed("flash_attn", 4.0 * batch * heads * Lq * Lk * 64, 0, label=f"flash b={batch} h={heads} Lq={Lq} Lk={Lk}",
            launch=lambda: L.check(
         L.load().fd_flash_attn(L.ptr(q), ldq, qbs, L.ptr(k), ldk, kbs, L.ptr(v), ldv, vbs, L.ptr(out), ldo, obs,
-                               batch, heads, Lq, Lk, kv_mod, scale, L.dtype_code(q.dtype), L.stream()),
+                               batch, heads, Lq, Lk, kv_mod, int(causal), scale, L.dtype_code(q.dtype), L.stream()),
         "fd_flash_attn"))
+    return out
+
+
+def embed_tokens(ids, tok, pos, out, batch, L_):
+    """ids int32 [batch*L_] (device); tok [vocab, D], pos [>=L_, D] -> out [batch*L_, D]."""
+    D = tok.shape[1]
+    L.check(L.load().fd_embed_tokens(L.ptr(ids), L.ptr(tok), L.ptr(pos), L.ptr(out), batch, L_, D, tok.shape[0],
+                                     L.dtype_code(tok.dtype), L.stream()), "fd_embed_tokens")
     return out
 
 

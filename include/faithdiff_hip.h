@@ -115,14 +115,14 @@ int fd_layer_norm(const void* x, long long ldx, void* y, long long ldy, const fl
  * q/k/v/o are row-major token matrices; head h of batch b lives at
  *   q + b*q_bstride + t*ldq + h*64 (same for o); k/v use batch index (kv_mod ? b % kv_mod : b), so
  *   the cross-attention K/V of the [neg, pos] prompt pair serve every tile of a batched forward.
- *   Lk may be any size (masked tail).
+ *   Lk may be any size (masked tail).  causal != 0: query i sees keys <= i (CLIP text encoders).
  * Replaces: SDPA (flash / mem-efficient) behind diffusers AttnProcessor2_0 for attn1 (self,
  *   T = 4096 / 1024 per tile) and attn2 (cross, Lk = 77) of all 70 BasicTransformerBlocks.
  * ------------------------------------------------------------------------------------------- */
 int fd_flash_attn(const void* q, long long ldq, long long q_bstride, const void* k, long long ldk,
                   long long k_bstride, const void* v, long long ldv, long long v_bstride, void* o, long long ldo,
-                  long long o_bstride, int batch, int heads, int Lq, int Lk, int kv_mod, float scale, int dtype,
-                  void* stream);
+                  long long o_bstride, int batch, int heads, int Lq, int Lk, int kv_mod, int causal, float scale,
+                  int dtype, void* stream);
 
 /* The information transformer's nn.MultiheadAttention(640, 8) with batch_first=False fed
  * (L=B, N=HW, E) (ext:242,251-254,576-577): for each pixel n, softmax attention over the L rows of
@@ -202,6 +202,11 @@ int fd_postprocess_u8(const void* x, void* y, long long n, int dtype, void* stre
  * b; horizontal: a left of b); e = min(extent, overlapping dims). */
 int fd_blend_edge(const void* a, void* b, int Ha, int Wa, int Hb, int Wb, int C, int extent, int vertical, int dtype,
                   void* stream);
+
+/* CLIP text embeddings (transformers CLIPTextEmbeddings behind encode_prompt, pipeline:587-598):
+ * out[b*L + l][:] = tok[ids[b*L + l]][:] + pos[l][:]; ids int32 on device, tables [vocab][D] / [L][D] in dtype. */
+int fd_embed_tokens(const int* ids, const void* tok, const void* pos, void* out, int batch, int L, int D, int vocab,
+                    int dtype, void* stream);
 
 /* library / device checks */
 int fd_device_check(void);

@@ -153,6 +153,44 @@ def test_synthetic_text_encoder_deterministic():
     assert c.abs().sum() > 0  # "" is encoded, not zeroed (pipeline:622-675)
 
 
+@pytest.mark.parametrize("which", ["L", "G"])
+def test_clip_param_shapes_match_transformers(which):
+    """The HIP text encoders' state-dict keys and shapes are transformers' (real SDXL text_encoder* weights load
+    strictly); built on the meta device, no memory."""
+    from transformers import CLIPTextConfig, CLIPTextModel, CLIPTextModelWithProjection
+    from fdhip import arch
+    cfg = arch.CLIP_L if which == "L" else arch.CLIP_G
+    tcfg = CLIPTextConfig(vocab_size=cfg["vocab"], hidden_size=cfg["D"], intermediate_size=cfg["inter"],
+                          num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"],
+                          max_position_embeddings=cfg["max_pos"], projection_dim=cfg["proj"] or 768)
+    with torch.device("meta"):
+        m = (CLIPTextModelWithProjection if cfg["proj"] else CLIPTextModel)(tcfg)
+    # transformers 4.x (the reference's pin, and the saved SDXL files) prefixes the text tower with
+    # "text_model."; newer releases drop the prefix in the module tree (and remap old files on load)
+    want = {(k if k.startswith(("text_model.", "text_projection")) else "text_model." + k): tuple(v.shape)
+            for k, v in m.state_dict().items() if "position_ids" not in k}
+    assert want == {k: tuple(v) for k, v in arch.clip_param_shapes(cfg).items()}
+    n = sum(int(np.prod(s)) for s in want.values())
+    assert n == (123060480 if which == "L" else 694659840)  # CLIP ViT-L/14 text, OpenCLIP bigG/14 text + proj
+
+
+def test_fallback_tokenizer_framing():
+    """Stand-in tokenizer (no vocab files offline): CLIP framing -- BOS, <= 75 ids, EOS, pad to 77 with the
+    tokenizer's pad id; deterministic; truncation keeps the EOS."""
+    from FaithDiff.models.clip_text import FallbackCLIPTokenizer
+    t1, t2 = FallbackCLIPTokenizer(49407), FallbackCLIPTokenizer(0)
+    a = t1("A photo of a cat.", padding="max_length", max_length=77, truncation=True).input_ids
+    b = t2("A photo of a cat.", padding="max_length", max_length=77, truncation=True).input_ids
+    assert a.shape == (1, 77) and a[0, 0] == 49406
+    n = int((a[0] != 49407).sum())  # BOS + 5 words + '.' = 7 non-pad ids before the EOS
+    assert n == 7 and a[0, n] == 49407 and (a[0, n:] == 49407).all()
+    assert torch.equal(a[0, :n + 1], b[0, :n + 1]) and (b[0, n + 1:] == 0).all()
+    assert int(a[0].argmax()) == n and int(b[0].argmax()) == n  # pooled row = first EOS for both encoders
+    long = t1(" ".join(["word"] * 200), max_length=77).input_ids
+    assert long.shape == (1, 77) and long[0, -1] == 49407
+    assert torch.equal(t1("x y", max_length=77).input_ids, t1("x y", max_length=77).input_ids)
+
+
 def test_quantize_e4m3_semantics():
     """a18: quantize_8bit = torch's float8_e4m3fn cast of every UNet parameter (RNE, no scale, NaN past 448),
     widened exactly; integers untouched.  The drop-in's use_fp8 flag routes the UNet through it."""

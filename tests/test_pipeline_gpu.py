@@ -114,8 +114,9 @@ def test_pipeline_matches_oracle(H, W, target, steps):
     out = pipe(lr_img=img, prompt=prompt, negative_prompt="", num_inference_steps=steps, guidance_scale=5.0,
                start_point="lr", height=H, width=W, overlap=0.5, target_size=target, latents=noise,
                posterior_noise=post, callback_on_step_end=cb).images[0]
-    pe, ppe = pipe.text_encoder(prompt)
-    npe, nppe = pipe.text_encoder("")
+    # the prompt embeddings the pipeline used (its HIP CLIP encoders are deterministic; their own parity vs
+    # transformers is tests/test_clip_gpu.py): the oracle denoises on the same context
+    pe, npe, ppe, nppe = (t.float().cpu() for t in pipe.encode_prompt(prompt, negative_prompt=""))
     ref = run_pipeline(ru, rv, re_, to_tensor(img), pe, npe, ppe, nppe, noise, post, num_inference_steps=steps,
                        guidance_scale=5.0, overlap=0.5, target_size=target, original_size=(H, W), start_point="lr")
     lat_ref = ref["latents"]
