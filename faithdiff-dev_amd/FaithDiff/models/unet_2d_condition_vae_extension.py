@@ -220,6 +220,7 @@ class Encoder:
         self.tile_latent_min_size = int(self.tile_sample_min_size / 8)
         self.tile_overlap_factor = 0.25
         self.use_tiling = False
+        self.process_group = None  # set by pipe.enable_tile_parallel: tiles sharded over its ranks
 
     def enable_tiling(self):
         self.use_tiling = True
@@ -246,7 +247,7 @@ class Encoder:
         """x NHWC fp16 [H*W, 3] -> NHWC fp16 [(H/8)*(W/8), 512] (tiled per ext:164-196 when enabled)."""
         if self.use_tiling and (W > self.tile_latent_min_size or H > self.tile_latent_min_size):
             from fdhip.tiling import tiled_encoder_forward
-            return tiled_encoder_forward(self, x, H, W)
+            return tiled_encoder_forward(self, x, H, W, self.process_group)
         return self.hip().encode(x, 1, H, W)
 
     def __call__(self, sample):
@@ -284,6 +285,7 @@ class AutoencoderKL:
         self._device = torch.device("cpu")
         self._enc = self._dec = None
         self.use_tiling = False
+        self.process_group = None  # set by pipe.enable_tile_parallel: tiled encode / decode sharded over its ranks
         self.tile_overlap_factor = 0.25
         # diffusers sets these from config.sample_size at construction; later config changes (as
         # set_encoder_tile_settings makes, pipeline:895) do not move them -- reproduced.
@@ -339,14 +341,14 @@ class AutoencoderKL:
     def encode_moments_nhwc(self, x, H, W):
         if self.use_tiling and (H > self.tile_sample_min_size or W > self.tile_sample_min_size):
             from fdhip.tiling import tiled_vae_encode
-            return tiled_vae_encode(self, x, H, W)
+            return tiled_vae_encode(self, x, H, W, self.process_group)
         return self.encoder_hip().encode(x, 1, H, W)
 
     def decode_nhwc(self, z, h, w):
         tl = self.tile_latent_min_size
         if self.use_tiling and (h > tl or w > tl):
             from fdhip.tiling import tiled_vae_decode
-            return tiled_vae_decode(self, z, h, w)
+            return tiled_vae_decode(self, z, h, w, self.process_group)
         return self.decoder_hip().decode(z, 1, h, w)
 
     def encode(self, x, return_dict=True):

@@ -143,8 +143,12 @@ class FaithDiffStableDiffusionXLPipeline:
         self.denoise_encoder.disable_tiling()
 
     def enable_tile_parallel(self, group=None):
-        """Shard TLC tiles over the ranks of `group` (default WORLD) with one all-gather per step."""
+        """Shard TLC tiles over the ranks of `group` (default WORLD) with one all-gather per step; the tiled VAE
+        encode / decode and the tiled denoise encoder shard their tiles the same way (fdhip.tiling.map_tiles)."""
         self.process_group = group if group is not None else dist.group.WORLD
+        for m in (self.vae, self.denoise_encoder):
+            if m is not None:
+                m.process_group = self.process_group
 
     # ------------------------------------------------------------------ properties (:915-948)
     @property

@@ -36,6 +36,36 @@ class TileShard:
         return buf[:self.ntiles]
 
 
+def broadcast_state_dict(sd, group=None, src=0, device=None, bucket_bytes=256 << 20):
+    """Make every rank's weights rank `src`'s, in place (weights broadcast once over RCCL/xGMI,
+    instead of every rank reading the checkpoint; with same-seed random init it is a no-op consistency pass).
+    Tensors go through `device` (the rank's GPU under RCCL, CPU under gloo) in flat buckets of one dtype, in
+    sorted key order, so every rank issues the same collectives."""
+    if group is None and (not dist.is_initialized() or dist.get_world_size() == 1):
+        return sd
+    src_global = dist.get_global_rank(group, src) if group is not None else src
+    keys = sorted(k for k, v in sd.items() if torch.is_tensor(v))
+    by_dtype = {}
+    for k in keys:
+        by_dtype.setdefault(sd[k].dtype, []).append(k)
+    for dt in sorted(by_dtype, key=str):
+        bucket, nbytes = [], 0
+        for k in by_dtype[dt] + [None]:
+            if k is not None:
+                bucket.append(k)
+                nbytes += sd[k].numel() * sd[k].element_size()
+            if bucket and (k is None or nbytes >= bucket_bytes):
+                flat = torch.cat([sd[b].reshape(-1) for b in bucket]).to(device or sd[bucket[0]].device)
+                dist.broadcast(flat, src=src_global, group=group)
+                off = 0
+                for b in bucket:
+                    n = sd[b].numel()
+                    sd[b].copy_(flat[off:off + n].view_as(sd[b]).to(sd[b].device))
+                    off += n
+                bucket, nbytes = [], 0
+    return sd
+
+
 def run_tile_loop(nsteps, shard, tile_shape, compute, blend, device, dtype=torch.float32, on_step=None):
     """Returns the final canvas.  tile_shape = (4, kh, kw)."""
     local = torch.zeros((shard.per,) + tuple(tile_shape), dtype=dtype, device=device)

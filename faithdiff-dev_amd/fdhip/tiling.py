@@ -11,9 +11,35 @@ Blending is the reference's recurrence: tile (i, j) is first blended (in place) 
 tile above, then with the already-final tile to its left (blend_v / blend_h), then cropped.  Every
 per-element step is a device kernel (fd_blend_edge, strided copies); only the tile bookkeeping is host.
 """
+import math
+
 import torch
+import torch.distributed as dist
 
 from . import ops
+
+
+def map_tiles(specs, fn, C, device, dtype, group=None):
+    """Run fn(*spec[:-1]) -> [spec[-1] rows, C] for every tile spec, in tile order.  With a process group of G
+    ranks (the tiles of a tiled VAE decode / encode are independent), rank r computes the
+    contiguous shard [r*ceil(N/G), ...) into row-padded slots and ONE all_gather_into_tensor (RCCL over xGMI on
+    the GPUs) hands every rank every tile; the blend that follows is then the same on all ranks, bit for bit."""
+    world = dist.get_world_size(group) if group is not None else 1
+    if world == 1:
+        return [fn(*s[:-1]) for s in specs]
+    rank = dist.get_rank(group)
+    n = len(specs)
+    per = math.ceil(n / world)
+    begin = min(rank * per, n)
+    count = max(0, min(n, begin + per) - begin)
+    maxr = max(s[-1] for s in specs)
+    local = torch.zeros((per, maxr, C), dtype=dtype, device=device)
+    for k in range(count):
+        s = specs[begin + k]
+        local[k, :s[-1]].copy_(fn(*s[:-1]))
+    buf = torch.empty((world * per, maxr, C), dtype=dtype, device=device)
+    dist.all_gather_into_tensor(buf, local, group=group)
+    return [buf[t, :specs[t][-1]] for t in range(n)]
 
 
 def _crop(src, H, W, C, i, j, th, tw):
@@ -46,32 +72,28 @@ def _assemble(rows, C, blend, limit, out_h, out_w, device, dtype):
     return out
 
 
-def tiled_vae_decode(vae, z, h, w):
-    """z: NHWC [h*w, 4] (already / scaling_factor) -> NHWC [8h * 8w, 3]."""
+def tiled_vae_decode(vae, z, h, w, group=None):
+    """z: NHWC [h*w, 4] (already / scaling_factor) -> NHWC [8h * 8w, 3].  group: shard the tiles (map_tiles)."""
     tl, ts, f = vae.tile_latent_min_size, vae.tile_sample_min_size, vae.tile_overlap_factor
     overlap, blend, limit = int(tl * (1 - f)), int(ts * f), ts - int(ts * f)
     dec = vae.decoder_hip()
-    rows = []
-    for i in range(0, h, overlap):
-        row = []
-        for j in range(0, w, overlap):
-            th, tw = min(tl, h - i), min(tl, w - j)
-            y = dec.decode(_crop(z, h, w, 4, i, j, th, tw), 1, th, tw)
-            row.append((y, 8 * th, 8 * tw))
-        rows.append(row)
+    grid = [[(i, j, min(tl, h - i), min(tl, w - j)) for j in range(0, w, overlap)] for i in range(0, h, overlap)]
+    specs = [(i, j, th, tw, 64 * th * tw) for row in grid for (i, j, th, tw) in row]
+    outs = map_tiles(specs, lambda i, j, th, tw: dec.decode(_crop(z, h, w, 4, i, j, th, tw), 1, th, tw), 3,
+                     z.device, z.dtype, group)
+    it = iter(outs)
+    rows = [[(next(it), 8 * th, 8 * tw) for (_, _, th, tw) in row] for row in grid]
     return _assemble(rows, 3, blend, limit, 8 * h, 8 * w, z.device, z.dtype)
 
 
-def _tiled_encode(encode_fn, x, H, W, C_out, ts, tl, f):
+def _tiled_encode(encode_fn, x, H, W, C_out, ts, tl, f, group=None):
     overlap, blend, limit = int(ts * (1 - f)), int(tl * f), tl - int(tl * f)
-    rows = []
-    for i in range(0, H, overlap):
-        row = []
-        for j in range(0, W, overlap):
-            th, tw = min(ts, H - i), min(ts, W - j)
-            y = encode_fn(_crop(x, H, W, 3, i, j, th, tw), th, tw)
-            row.append((y, th // 8, tw // 8))
-        rows.append(row)
+    grid = [[(i, j, min(ts, H - i), min(ts, W - j)) for j in range(0, W, overlap)] for i in range(0, H, overlap)]
+    specs = [(i, j, th, tw, (th // 8) * (tw // 8)) for row in grid for (i, j, th, tw) in row]
+    outs = map_tiles(specs, lambda i, j, th, tw: encode_fn(_crop(x, H, W, 3, i, j, th, tw), th, tw), C_out,
+                     x.device, x.dtype, group)
+    it = iter(outs)
+    rows = [[(next(it), th // 8, tw // 8) for (_, _, th, tw) in row] for row in grid]
     # output extent: the cropped tiles tile the latent exactly when 8 * limit == overlap; otherwise
     # (the reference's quirk at non-default settings) the concatenation defines the size.
     out_h = sum(min(limit, r[0][1]) for r in rows)
@@ -79,15 +101,15 @@ def _tiled_encode(encode_fn, x, H, W, C_out, ts, tl, f):
     return _assemble(rows, C_out, blend, limit, out_h, out_w, x.device, x.dtype)
 
 
-def tiled_vae_encode(vae, x, H, W):
+def tiled_vae_encode(vae, x, H, W, group=None):
     """x: NHWC [H*W, 3] -> moments NHWC [(H/8)*(W/8), 8] (quant_conv output)."""
     enc = vae.encoder_hip()
     return _tiled_encode(lambda t, th, tw: enc.encode(t, 1, th, tw), x, H, W, 8, vae.tile_sample_min_size,
-                         vae.tile_latent_min_size, vae.tile_overlap_factor)
+                         vae.tile_latent_min_size, vae.tile_overlap_factor, group)
 
 
-def tiled_encoder_forward(encoder, x, H, W):
+def tiled_encoder_forward(encoder, x, H, W, group=None):
     """FaithDiff Encoder.tiled_encode (ext:164-190): x NHWC [H*W, 3] -> [(H/8)*(W/8), 512]."""
     enc = encoder.hip()
     return _tiled_encode(lambda t, th, tw: enc.encode(t, 1, th, tw), x, H, W, 512, encoder.tile_sample_min_size,
-                         encoder.tile_latent_min_size, encoder.tile_overlap_factor)
+                         encoder.tile_latent_min_size, encoder.tile_overlap_factor, group)

@@ -71,6 +71,60 @@ def _run(world, h, w, steps):
     return sorted(res, key=lambda r: r[0])
 
 
+def _vae_tiles_and_weights_worker(rank, world, port, q):
+    """map_tiles (the sharded tiled VAE decode / encode exchange) and broadcast_state_dict under gloo."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from FaithDiff.pipelines.tile_parallel import broadcast_state_dict
+        from fdhip.tiling import map_tiles
+        specs = [(i, j, th, tw, th * tw) for i, th in ((0, 7), (5, 3)) for j, tw in ((0, 8), (6, 5), (9, 2))]
+
+        def fn(i, j, th, tw):  # a tile "decode": deterministic in its coordinates, ragged sizes
+            g = torch.Generator().manual_seed(100 * i + j)
+            return torch.randn(th * tw, 3, generator=g)
+
+        tiles = map_tiles(specs, fn, 3, "cpu", torch.float32, dist.group.WORLD)
+        # ranks start from different weights; after the broadcast all hold rank 0's
+        g = torch.Generator().manual_seed(rank)
+        sd = {"a.weight": torch.randn(5, 7, generator=g), "b.bias": torch.randn(3, generator=g),
+              "c.idx": torch.arange(4) + rank, "d.half": torch.randn(6, generator=g).half()}
+        broadcast_state_dict(sd, None, 0, "cpu", bucket_bytes=64)
+        # numpy (pickled by value): torch tensors would travel as shared-memory handles that die with the worker
+        q.put((rank, [t.numpy().copy() for t in tiles], {k: v.numpy().copy() for k, v in sd.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_vae_tiles_and_weight_broadcast(world):
+    from fdhip.tiling import map_tiles
+    specs = [(i, j, th, tw, th * tw) for i, th in ((0, 7), (5, 3)) for j, tw in ((0, 8), (6, 5), (9, 2))]
+
+    def fn(i, j, th, tw):
+        g = torch.Generator().manual_seed(100 * i + j)
+        return torch.randn(th * tw, 3, generator=g)
+
+    ref = map_tiles(specs, fn, 3, "cpu", torch.float32, None)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_vae_tiles_and_weights_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sd0 = res[0][2]
+    for rank, tiles, sd in res:
+        assert len(tiles) == len(ref) and all((a == b.numpy()).all() for a, b in zip(tiles, ref)), rank
+        assert all((sd[k] == sd0[k]).all() for k in sd0), rank
+    g = torch.Generator().manual_seed(0)
+    assert (sd0["a.weight"] == torch.randn(5, 7, generator=g).numpy()).all()
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_tile_parallel_bitwise_equals_single_rank(world):
     h, w, steps = 160, 224, 3  # 4 x 6 = 24 tiles of 64x64
