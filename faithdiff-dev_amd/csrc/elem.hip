@@ -181,15 +181,16 @@ extern "C" int fd_transpose(const void* x, long long ldx, void* y, long long ldy
 }
 
 // ------------------------------------------------------------------------------------------------
-// Direct conv for Cin < 64 (K = k*k*Cin <= 72).  Block = 8 consecutive output pixels x all Cout
+// Direct conv for Cin < 64 (K = k*k*Cin <= 72).  Block = 32 consecutive output pixels x all Cout
 // (threads stride over Cout); each thread keeps its output channel's K weights in registers and
-// reuses them for the 8 pixels; input taps are wave-uniform (broadcast) loads; stores are coalesced.
+// reuses them for the 32 pixels (8 pixels per block re-read the whole weight matrix 4x as often: conv_in at
+// 128^2 took 84 us); input taps are wave-uniform (broadcast) LDS reads; stores are coalesced.
 template <typename TI, typename TO, int KK>
 __global__ void __launch_bounds__(256) conv_direct_kernel(const TI* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ bias, TO* __restrict__ y, int nimg,
                                                           int Hin, int Win, int Cin, int Cout, int Hout, int Wout,
                                                           int ks, int stride, int pad, float in_scale) {
-  constexpr int P = 8;
+  constexpr int P = 32;
   const long long npix = (long long)nimg * Hout * Wout;
   const long long p0 = (long long)blockIdx.x * P;
   // im2col of the block's 8 output pixels (8 x K values) staged once in LDS, read as broadcasts
@@ -235,7 +236,7 @@ extern "C" int fd_conv2d_direct(const void* x, const float* w, const float* bias
   const int K = ksize * ksize * Cin;
   const int Hout = (Hin + 2 * pad - ksize) / stride + 1, Wout = (Win + 2 * pad - ksize) / stride + 1;
   const long long npix = (long long)nimg * Hout * Wout;
-  dim3 grid((unsigned)((npix + 7) / 8)), block(Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64);
+  dim3 grid((unsigned)((npix + 31) / 32)), block(Cout >= 256 ? 256 : ((Cout + 63) / 64) * 64);
   hipStream_t s = (hipStream_t)stream;
 #define FD_CONV_DIRECT(KK)                                                                                    \
   FD_DISPATCH_I(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv_direct_kernel<TI, TO, KK>), grid, block, 0, \
