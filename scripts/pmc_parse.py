@@ -48,9 +48,9 @@ def main():
         cal = sum(v for _, _, v in calib)
         known = meta["calib_bytes_read"] if c == "FETCH_SIZE" else meta["calib_bytes_written"]
         per[c] = {"calib_counter": cal, "bytes_per_count_measured": known / cal if cal else None,
-                  "gemm": sum(v for _, n, v in fwd if "gemm_kernel" in n),
+                  "gemm": sum(v for _, n, v in fwd if ("gemm_kernel" in n or "gemm8_kernel" in n)),
                   "flash": sum(v for _, n, v in fwd if "flash_attn" in n),
-                  "all": sum(v for _, n, v in fwd), "n_gemm": sum(1 for _, n, _ in fwd if "gemm_kernel" in n)}
+                  "all": sum(v for _, n, v in fwd), "n_gemm": sum(1 for _, n, _ in fwd if ("gemm_kernel" in n or "gemm8_kernel" in n))}
     # unit: rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB; gfx950 FETCH_SIZE counts half of 16-B reads
     f, w = per["FETCH_SIZE"], per["WRITE_SIZE"]
     rd = f["gemm"] * 1024 * 2
