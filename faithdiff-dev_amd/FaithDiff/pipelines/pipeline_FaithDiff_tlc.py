@@ -12,8 +12,9 @@ rescale), Euler step, then the gaussian fp32 blend (:1324-1409) -> latents / 0.1
 What differs (MI355X-first, documented in DESIGN.md): the latent state stays fp32 between steps (the
 reference rounds it to fp16 at :1409); several tiles share one UNet forward (rows are independent
 except the extras' batch-axis MHA, which is grouped per tile); the per-element loop work is fused
-device kernels (fd_tlc_*); tiles can be sharded over ranks (tile_parallel.py); text encoders are a
-seeded synthetic stand-in unless embeddings are passed (CLIP weights are not available offline).
+device kernels (fd_tlc_*); tiles can be sharded over ranks (tile_parallel.py); the CLIP text encoders
+run on the HIP kernels (fdhip/clip.py) when built by from_pretrained, with a seeded synthetic stand-in
+only for pipelines constructed without them.
 """
 import inspect
 import zlib
