@@ -35,20 +35,25 @@ __device__ __forceinline__ void vm_wait() {
 #define FD_GEMM8_DIAG 0
 #endif
 
-template <typename T, int BN, int WAVES_M, bool CONV, bool GEGLU, typename TO>
-__global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, const int S, const int gm_mode,
-                                                    float* __restrict__ slabs, unsigned* __restrict__ counters) {
+// BM x BN tile over NW waves (WAVES_M x WAVES_N).  Instances: 256 x 128 over 8 waves (the split-K kernel
+// above) and 64 x 160 over 4 waves (one wave per SIMD, 32 x 80 each: the M = 2048 projections' 256-tile
+// launches, where the previous 4-wave kernel split each K step over two waves and exposed the LDS-read
+// latency in front of every MFMA group).
+template <typename T, int BM, int BN, int NW, int WAVES_M, bool CONV, bool GEGLU, typename TO>
+__global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, const int S, const int gm_mode,
+                                                        float* __restrict__ slabs, unsigned* __restrict__ counters) {
   typedef typename VecT<T>::v8 V8;
   constexpr bool SCHED = FD_GEMM8_SCHED;
-  constexpr int BM = 256, NS = 3;
-  constexpr int WAVES_N = 8 / WAVES_M;
+  constexpr int NS = 3, NTHR = 64 * NW;
+  constexpr int WAVES_N = NW / WAVES_M;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int MT = WM / 16, NT = WN / 16;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
-  constexpr int A_I = BM / 64;             // A loads per wave per stage (8 rows x 128 B each)
-  constexpr int B_TOT = BN / 8;            // B loads per stage over the 8 waves
-  constexpr int B_I = (B_TOT + 7) / 8;     // ... at most this many per wave
-  constexpr int B_LO = B_TOT / 8;          // waves >= B_TOT % 8 issue only this many
+  constexpr int A_I = BM / (8 * NW);       // A loads per wave per stage (8 rows x 128 B each)
+  constexpr int B_TOT = BN / 8;            // B loads per stage over the NW waves
+  constexpr int B_I = (B_TOT + NW - 1) / NW;  // ... at most this many per wave
+  constexpr int B_LO = B_TOT / NW;         // waves >= B_TOT % NW issue only this many
+  static_assert(A_I * 8 * NW == BM, "A rows per stage");
   constexpr int PER_HI = A_I + B_I, PER_LO = A_I + B_LO;
   constexpr int BNO = GEGLU ? BN / 2 : BN;
   constexpr int LDE = BNO + 4;
@@ -94,7 +99,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
   const T* __restrict__ Bw = (const T*)p.B;
   const T* __restrict__ A2 = (const T*)p.A2;
   const int lrow = lane >> 3, slot = lane & 7;
-  const bool hi = (B_TOT % 8 == 0) || w < B_TOT % 8;  // this wave issues B_I (not B_LO) B loads
+  const bool hi = (B_TOT % NW == 0) || w < B_TOT % NW;  // this wave issues B_I (not B_LO) B loads
 
   // ---- per-lane load state (rows fixed over the K loop)
   const T* a_row[A_I];
@@ -103,7 +108,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
   bool a_ok[A_I];
 #pragma unroll
   for (int i = 0; i < A_I; ++i) {
-    const int row = (w + 8 * i) * 8 + lrow;
+    const int row = (w + NW * i) * 8 + lrow;
     const int m = m0 + row;
     a_ok[i] = m < M;
     const int mm = m < M ? m : M - 1;
@@ -126,7 +131,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
   const T* b_row[B_I];
 #pragma unroll
   for (int i = 0; i < B_I; ++i) {
-    const int row = (w + 8 * i) * 8 + lrow;  // < BN for the loads this wave issues
+    const int row = (w + NW * i) * 8 + lrow;  // < BN for the loads this wave issues
     const int n = n0 + (row < BN ? row : 0);
     b_row[i] = Bw + (long long)(n < N ? n : N - 1) * p.ldb + (slot ^ ((row >> 1) & 7)) * 8;
   }
@@ -151,18 +156,18 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
         const T* src = second ? (A2 + pix * (p.Cin - C1) + (c0 - C1) + a_chunk[i] * 8)
                               : (A + pix * p.lda + c0 + a_chunk[i] * 8);
         const void* s = ok ? (const void*)src : (const void*)g_zero_page8;
-        __builtin_amdgcn_global_load_lds(s, LDS_PTR(sa + (w + 8 * i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(s, LDS_PTR(sa + (w + NW * i) * 1024), 16, 0, 0);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A_I; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(a_row[i] + k0), LDS_PTR(sa + (w + 8 * i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(a_row[i] + k0), LDS_PTR(sa + (w + NW * i) * 1024), 16, 0, 0);
     }
     unsigned char* sb = sa + A_BYTES;
 #pragma unroll
     for (int i = 0; i < B_I; ++i)
       if (i < B_LO || hi)
-        __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (w + 8 * i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (w + NW * i) * 1024), 16, 0, 0);
   };
   // all but the youngest `ahead` stages of this wave's loads have landed
   auto wait_ahead = [&](int ahead) {
@@ -241,17 +246,26 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
     read_frags(buf, 0, a0, b0);
     mma(a1, b1);
     if (SCHED) {
-      if (refill) {
+      if constexpr (PER_LO + MT + NT <= MT * NT) {
+        if (refill) {
 #pragma unroll
-        for (int i = 0; i < PER_LO; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+          for (int i = 0; i < PER_LO; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+          }
         }
-      }
 #pragma unroll
-      for (int i = 0; i < MT + NT; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        for (int i = 0; i < MT + NT; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        }
+      } else {  // fewer MFMAs than loads + reads: one of each (while any remain) behind every MFMA
+#pragma unroll
+        for (int i = 0; i < MT * NT; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          if (refill && i < PER_LO) __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+          if (i < MT + NT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        }
       }
     }
   };
@@ -266,8 +280,58 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
   // lane then takes a ticket on the tile's counter (agent-scope atomic).  The last arriver reads all S
   // slabs with sc1 loads (no L1/L2 flush or invalidate needed: cdna_hip_programming.md section 5,
   // "Projection GEMM" item 2, sc1 form), sums them in split order and runs the epilogue; the others exit.
-  if (S > 1) {
-    constexpr int SLAB = MT * NT * 512 * 16;  // bytes per split of one tile
+  if (S == 2) {
+    // Pairwise combine: the first split to finish publishes its partial (sc1 stores, drained, then an sc1
+    // flag); the second waits for the flag, adds the partial to its own and runs the epilogue.  Half the
+    // slab traffic of the S-way form, and the sum a + b is bitwise the same whichever split came first.
+    // The waiting split only ever waits on one that has already taken its ticket (it is running), so
+    // no co-residency assumption is needed.
+    constexpr int SLAB = MT * NT * NTHR * 16;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((char*)slabs + (long long)tile_id * SLAB, (short)0, SLAB, 0x00020000);
+    unsigned* flag = counters + 32768 + tile_id;
+    __syncthreads();  // every wave is past its last LDS read: smem[0] is free
+    if (tid == 0) {
+      const unsigned tk = __hip_atomic_fetch_add(counters + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *(volatile unsigned*)smem = tk;
+    }
+    __syncthreads();
+    const unsigned tk = *(volatile unsigned*)smem;
+    if (tk == 0) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][ni]), rs,
+                                                 ((mi * NT + ni) * NTHR + tid) * 16, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {
+      // bounded: a lost flag would give a wrong tile, never a hung GPU
+      for (int it = 0; it < (1 << 24); ++it) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    f32x4 part[MT][NT];
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+        part[mi][ni] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((mi * NT + ni) * NTHR + tid) * 16, 0, 16));
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) acc[mi][ni] += part[mi][ni];
+  } else if (S > 1) {
+    constexpr int SLAB = MT * NT * NTHR * 16;  // bytes per split of one tile
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((char*)slabs + (long long)tile_id * S * SLAB, (short)0, S * SLAB, 0x00020000);
 #pragma unroll
@@ -275,7 +339,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][ni]), rs,
-                                               split * SLAB + ((mi * NT + ni) * 512 + tid) * 16, 0, 16);
+                                               split * SLAB + ((mi * NT + ni) * NTHR + tid) * 16, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -291,7 +355,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni)
         acc[mi][ni] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((mi * NT + ni) * 512 + tid) * 16, 0, 16));
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((mi * NT + ni) * NTHR + tid) * 16, 0, 16));
     for (int q = 1; q < S; ++q) {
       f32x4 part[MT][NT];
 #pragma unroll
@@ -299,7 +363,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
 #pragma unroll
         for (int ni = 0; ni < NT; ++ni)
           part[mi][ni] = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, q * SLAB + ((mi * NT + ni) * 512 + tid) * 16, 0, 16));
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, q * SLAB + ((mi * NT + ni) * NTHR + tid) * 16, 0, 16));
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
@@ -329,8 +393,9 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
   const int act = p.act;
   float* ep = (float*)smem;
   constexpr int VPR = BNO / 8;
-  constexpr int ITER = 4;  // row-phase iterations whose loads are issued together
-  static_assert(EROWS * VPR % (512 * ITER) == 0, "epilogue iterations");
+  // row-phase iterations whose loads are issued together
+  constexpr int ITER = (EROWS * VPR) % (NTHR * 4) == 0 ? 4 : (EROWS * VPR) % (NTHR * 5) == 0 ? 5 : 1;
+  static_assert(EROWS * VPR % (NTHR * ITER) == 0, "epilogue iterations");
   float gbh[GEGLU ? NT / 2 : 1], gbg[GEGLU ? NT / 2 : 1];
   if (GEGLU) {
 #pragma unroll
@@ -377,12 +442,12 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
     __syncthreads();
     if (interior) {
 #pragma unroll 1
-    for (int e0 = 0; e0 < EROWS * VPR; e0 += 512 * ITER) {
+    for (int e0 = 0; e0 < EROWS * VPR; e0 += NTHR * ITER) {
       float v[ITER][8], bv[ITER][8], rv[ITER][8];
       TO8 res[ITER];
 #pragma unroll
       for (int it = 0; it < ITER; ++it) {
-        const int e = e0 + tid + it * 512;
+        const int e = e0 + tid + it * NTHR;
         const int r = e / VPR, cv = e % VPR;
         const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
         *(f32x4*)&v[it][0] = *(const f32x4*)(ep + r * LDE + cv * 8);
@@ -400,7 +465,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
       }
 #pragma unroll
       for (int it = 0; it < ITER; ++it) {
-        const int e = e0 + tid + it * 512;
+        const int e = e0 + tid + it * NTHR;
         const int r = e / VPR, cv = e % VPR;
         const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
         if (!GEGLU) {
@@ -434,7 +499,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
       }
     }
     } else {  // edge tiles / unaligned operands: scalar, bounds-checked
-      for (int e = tid; e < EROWS * VPR; e += 512) {
+      for (int e = tid; e < EROWS * VPR; e += NTHR) {
         const int r = e / VPR, cv = e % VPR;
         const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
         if (m >= M || n >= Nout) continue;
@@ -457,7 +522,7 @@ __global__ void __launch_bounds__(512) gemm8_kernel(const fd_gemm_params p, cons
 namespace {
 
 struct Plan8 {
-  int bn, waves_m, S, group_m, tiles;
+  int bm, bn, nw, waves_m, S, group_m, tiles;
 };
 
 int env_i(const char* n, int d) {
@@ -483,23 +548,23 @@ int choose_split(int m_ref, int N, int K, int bn) {
   return s < 1 ? 1 : s;
 }
 
-template <typename T, typename TO, int BN, int WAVES_M>
+template <typename T, typename TO, int BM, int BN, int NW, int WAVES_M>
 int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
-  dim3 grid(pl.tiles * pl.S), block(512);
+  dim3 grid(pl.tiles * pl.S), block(64 * NW);
   float* slabs = (float*)((char*)p->ws + 65536 * sizeof(unsigned));
   unsigned* cnt = (unsigned*)p->ws;
   if (p->conv) {
-    hipLaunchKernelGGL((gemm8_kernel<T, BN, WAVES_M, true, false, TO>), grid, block, 0, s, *p, pl.S, pl.group_m, slabs,
-                       cnt);
+    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, true, false, TO>), grid, block, 0, s, *p, pl.S,
+                       pl.group_m, slabs, cnt);
   } else if (p->act == FD_ACT_GEGLU) {
-    if constexpr ((BN / (8 / WAVES_M)) % 32 == 0)
-      hipLaunchKernelGGL((gemm8_kernel<T, BN, WAVES_M, false, true, TO>), grid, block, 0, s, *p, pl.S, pl.group_m,
-                         slabs, cnt);
+    if constexpr ((BN / (NW / WAVES_M)) % 32 == 0)
+      hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, false, true, TO>), grid, block, 0, s, *p, pl.S,
+                         pl.group_m, slabs, cnt);
     else
       return FD_ERR_ARG;
   } else {
-    hipLaunchKernelGGL((gemm8_kernel<T, BN, WAVES_M, false, false, TO>), grid, block, 0, s, *p, pl.S, pl.group_m, slabs,
-                       cnt);
+    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, false, false, TO>), grid, block, 0, s, *p, pl.S,
+                       pl.group_m, slabs, cnt);
   }
   FD_LAUNCH_CHECK();
   return FD_OK;
@@ -508,28 +573,48 @@ int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
 }  // namespace
 
 // Plan for one launch (0 = not eligible -> the 4-wave kernel).  Shared by fd_gemm8_ws_bytes and fd_gemm8.
+// Every decision reads m_ref (rows per TLC tile), never the batched M, so batching tiles changes no bit:
+// the 4-wave kernel sums each K step's two halves in separate waves, these kernels in one accumulator,
+// and any tile shape of the same kernel family gives the same k order.
 static int plan8(const fd_gemm_params* p, Plan8* pl) {
-  static int enabled = -1, force_s = 0, force_bn = 0, force_gm = 0;
+  static int enabled = -1, force_s = 0, force_gm = 0, r4 = 1, pair128 = 0;
   if (enabled < 0) {
     enabled = env_i("FD_GEMM8", 1);
     force_s = env_i("FD_GEMM8_S", 0);
-    force_bn = env_i("FD_GEMM8_BN", 0);
     force_gm = env_i("FD_GEMM8_GM", 0);
+    r4 = env_i("FD_GEMM_R4", 1);  // 64 x 160 one-wave-per-SIMD kernel: 0 off, 1 <= 256 tiles, 2 every non-GEGLU
+    pair128 = env_i("FD_GEMM_P128", 0);
   }
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
-  if (!enabled || m_ref < 256 || p->N < 128 || (p->batch > 1) || p->K < 128) return 0;
+  if (!enabled || p->batch > 1 || p->K < 128) return 0;
   Plan8 q;
   // 256 x 128 tiles (4 x 2 waves of 64 x 64).  256 x 160 (98 vs 85 flop/B) spills at the 256-VGPR cap of
   // two waves per SIMD with register-double-buffered fragments; kept out until it fits.
-  (void)force_bn;
+  q.bm = 256;
   q.bn = 128;
+  q.nw = 8;
   q.waves_m = 4;
-  q.S = force_s > 0 ? force_s : choose_split(m_ref, p->N, p->K, q.bn);
-  if (q.S <= 0) return 0;
+  q.S = (m_ref >= 256 && p->N >= 128) ? (force_s > 0 ? force_s : choose_split(m_ref, p->N, p->K, q.bn)) : 0;
+  if (q.S <= 0) {
+    const long long tiles_ref = (long long)((m_ref + 63) / 64) * ((p->N + 159) / 160);
+    const bool ok = r4 && p->act != FD_ACT_GEGLU && m_ref >= 64 && p->N >= 160 &&
+                    (r4 == 2 || (!p->conv && tiles_ref <= 256));
+    if (!ok) return 0;
+    q.bm = 64;
+    q.bn = 160;
+    q.nw = 4;
+    q.waves_m = 2;
+    q.S = 1;
+    if (pair128 && m_ref >= 128 && tiles_ref <= 256 && p->K >= 1024) {
+      // 128 x 160 tiles with K split in two (pairwise combine): 0.64x the operand bytes per CU
+      q.bm = 128;
+      q.S = 2;
+    }
+  }
   if (q.S > p->K / 64) q.S = p->K / 64;
-  const int tiles_m = (p->M + 255) / 256, tiles_n = (p->N + q.bn - 1) / q.bn;
+  const int tiles_m = (p->M + q.bm - 1) / q.bm, tiles_n = (p->N + q.bn - 1) / q.bn;
   q.tiles = tiles_m * tiles_n;
-  if (q.S > 1 && q.tiles > 65536) return 0;
+  if (q.S > 1 && q.tiles > (q.S == 2 ? 32768 : 65536)) return 0;
   // group_m: per-XCD chunk of tiles/8 tiles; pick the tile-row group height minimising that chunk's
   // unique A rows + B columns (both stream K bytes each)
   int gm = 1;
@@ -539,7 +624,7 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     for (int g = 1; g <= tiles_m; g *= 2) {
       const long long cols = per_xcd < g ? 1 : (per_xcd + g - 1) / g;
       const long long rows = per_xcd < g ? per_xcd : g;
-      const double c = rows * 256.0 + (cols < tiles_n ? cols : tiles_n) * (double)q.bn;
+      const double c = rows * (double)q.bm + (cols < tiles_n ? cols : tiles_n) * (double)q.bn;
       if (c < bestc - 1e-9) { bestc = c; gm = g; }
     }
   }
@@ -551,7 +636,7 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
 extern "C" long long fd_gemm_ws_bytes(const fd_gemm_params* p) {
   Plan8 pl;
   if (!p || !plan8(p, &pl) || pl.S <= 1) return 0;
-  const long long slab = 256LL * pl.bn * 4;
+  const long long slab = (long long)pl.bm * pl.bn * 4;
   return 65536LL * sizeof(unsigned) + (long long)pl.tiles * pl.S * slab;
 }
 
@@ -560,13 +645,20 @@ extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream) {
   Plan8 pl;
   if (!plan8(p, &pl)) return 0;
   if (pl.S > 1) {
-    const long long need = 65536LL * sizeof(unsigned) + (long long)pl.tiles * pl.S * 256LL * pl.bn * 4;
+    const long long need = 65536LL * sizeof(unsigned) + (long long)pl.tiles * pl.S * pl.bm * pl.bn * 4;
     if (!p->ws || p->ws_bytes < need) return FD_ERR_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
   int rc;
-#define FD_G8(BN_, WM_) FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, rc = (launch8<T, TO, BN_, WM_>(p, pl, s))))
-  FD_G8(128, 4);
+#define FD_G8(BM_, BN_, NW_, WM_) \
+  FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, rc = (launch8<T, TO, BM_, BN_, NW_, WM_>(p, pl, s))))
+  if (pl.bm == 256) {
+    FD_G8(256, 128, 8, 4);
+  } else if (pl.bm == 128) {
+    FD_G8(128, 160, 4, 2);
+  } else {
+    FD_G8(64, 160, 4, 2);
+  }
 #undef FD_G8
   return rc == FD_OK ? 1 : rc;
 }

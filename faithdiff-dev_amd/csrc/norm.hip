@@ -37,17 +37,28 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ x
   const int r0 = chunk * rows_per_chunk;
   const int r1 = min(r0 + rows_per_chunk, HW);
   if (ro < RP) {
-    for (int r = r0 + ro; r < r1; r += RP) {
-      const T* row = x + ((long long)img * HW + r) * C;
+    // U rows' loads in flight per thread, accumulated in row order (same sums as a one-row loop)
+    constexpr int U = 4;
+    for (int r = r0 + ro; r < r1; r += RP * U) {
+      V8 val[U][NV];
 #pragma unroll
-      for (int n = 0; n < NV; ++n) {
-        const V8 val = *(const V8*)(row + (v + n * VPR) * 8);
+      for (int u = 0; u < U; ++u) {
+        const int rr = r + u * RP;
+        const T* row = x + ((long long)img * HW + (rr < r1 ? rr : r)) * C;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float f = (float)val[i];
-          s[n * 8 + i] += f;
-          q[n * 8 + i] += f * f;
-        }
+        for (int n = 0; n < NV; ++n) val[u][n] = *(const V8*)(row + (v + n * VPR) * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (r + u * RP >= r1) break;
+#pragma unroll
+        for (int n = 0; n < NV; ++n)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float f = (float)val[u][n][i];
+            s[n * 8 + i] += f;
+            q[n * 8 + i] += f * f;
+          }
       }
     }
 #pragma unroll
@@ -92,10 +103,22 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const float2* __restri
   double s = 0.0, q = 0.0;
   if (g < groups) {
     const float2* p = part + (long long)img * nchunks * groups + g;
-    for (int c = j; c < nchunks; c += SUB) {
-      const float2 v = p[(long long)c * groups];
-      s += v.x;
-      q += v.y;
+    // 8 independent loads in flight, summed in chunk order (a one-at-a-time loop here is a chain of
+    // dependent L2 round trips: 10 us at 256 chunks)
+    constexpr int U = 8;
+    for (int c = j; c < nchunks; c += SUB * U) {
+      float2 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int cc = c + u * SUB;
+        v[u] = p[(long long)(cc < nchunks ? cc : c) * groups];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (c + u * SUB < nchunks) {
+          s += v[u].x;
+          q += v[u].y;
+        }
     }
   }
   for (int o = SUB / 2; o > 0; o >>= 1) {
@@ -122,6 +145,18 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
   const int img = blockIdx.y;
   const int t = threadIdx.x;
   const int cpg = C / groups;
+  const int VPR = C / 8;
+  const long long base = (long long)img * HW * C;
+  const long long e1 = (long long)min(blockIdx.x * rows_per_block + rows_per_block, HW) * VPR;
+  const long long eb = (long long)blockIdx.x * rows_per_block * VPR;  // a whole-row boundary
+  long long e = eb + t;
+  // the block's first U vectors are requested before the stats / gamma / beta round trips, and each
+  // batch of U is in flight together (a load-compute-store loop exposes one HBM latency per vector)
+  constexpr int U = 4;
+  V8 val[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (e + u * 256 < e1) val[u] = *(const V8*)(x + base + (e + u * 256) * 8);
   if (t < groups) {
     const float2 st = stats[img * groups + t];
     mean_s[t] = st.x;
@@ -135,22 +170,27 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
     sh[c] = (beta ? beta[c] : 0.f) - mean_s[g] * a;
   }
   __syncthreads();
-  const int VPR = C / 8;
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(r0 + rows_per_block, HW);
-  const long long base = (long long)img * HW * C;
-  for (long long e = (long long)r0 * VPR + t; e < (long long)r1 * VPR; e += 256) {
-    const long long r = e / VPR;
-    const int v = e - r * VPR;
-    const V8 val = *(const V8*)(x + base + r * C + v * 8);
-    V8 out;
+  for (; e < e1; e += 256 * U) {
+    V8 nxt[U];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float f = (float)val[i] * sc[v * 8 + i] + sh[v * 8 + i];
-      if (silu) f = silu_f(f);
-      out[i] = (T)f;
+    for (int u = 0; u < U; ++u)
+      if (e + (U + u) * 256 < e1) nxt[u] = *(const V8*)(x + base + (e + (U + u) * 256) * 8);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long ee = e + u * 256;
+      if (ee >= e1) break;
+      const int v = (int)(ee - eb) % VPR;
+      V8 out;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float f = (float)val[u][i] * sc[v * 8 + i] + sh[v * 8 + i];
+        if (silu) f = silu_f(f);
+        out[i] = (T)f;
+      }
+      *(V8*)(y + base + ee * 8) = out;
     }
-    *(V8*)(y + base + r * C + v * 8) = out;
+#pragma unroll
+    for (int u = 0; u < U; ++u) val[u] = nxt[u];
   }
   (void)NV;
 }
@@ -206,16 +246,29 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
   if (row >= M) return;
   const int VPR = C / 8;
   const T* xr = x + row * ldx;
+  // row, gamma and beta are all requested up front: one memory round trip per row, not two
+  V8 raw[MAXV];
+  f32x4 g4[MAXV][2], b4[MAXV][2];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int v = lane + k * 64;
+    if (v < VPR) {
+      raw[k] = *(const V8*)(xr + v * 8);
+      g4[k][0] = *(const f32x4*)(gamma + v * 8);
+      g4[k][1] = *(const f32x4*)(gamma + v * 8 + 4);
+      b4[k][0] = *(const f32x4*)(beta + v * 8);
+      b4[k][1] = *(const f32x4*)(beta + v * 8 + 4);
+    }
+  }
   float vals[MAXV][8];
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     const int v = lane + k * 64;
     if (v < VPR) {
-      const V8 val = *(const V8*)(xr + v * 8);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        vals[k][i] = (float)val[i];
+        vals[k][i] = (float)raw[k][i];
         s += vals[k][i];
       }
     }
@@ -239,14 +292,10 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
   for (int k = 0; k < MAXV; ++k) {
     const int v = lane + k * 64;
     if (v < VPR) {
-      float g[8], b[8];
-      *(f32x4*)&g[0] = *(const f32x4*)(gamma + v * 8);
-      *(f32x4*)&g[4] = *(const f32x4*)(gamma + v * 8 + 4);
-      *(f32x4*)&b[0] = *(const f32x4*)(beta + v * 8);
-      *(f32x4*)&b[4] = *(const f32x4*)(beta + v * 8 + 4);
       V8 out;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) out[i] = (T)((vals[k][i] - mean) * rstd * g[i] + b[i]);
+      for (int i = 0; i < 8; ++i)
+        out[i] = (T)((vals[k][i] - mean) * rstd * g4[k][i >> 2][i & 3] + b4[k][i >> 2][i & 3]);
       *(V8*)(yr + v * 8) = out;
     }
   }
