@@ -17,6 +17,17 @@
 
 // amdgpu_waves_per_eu(1, 2): let the compiler use the full 256-VGPR budget of two waves per SIMD instead of
 // capping arch VGPRs at 128 and spilling the O / S accumulators through AGPR moves (192 v_accvgpr per tile).
+// max over lanes l, l^16, l^32, l^48 (the 4 row groups of a 16 x 16 MFMA block): gfx950 permlane swaps
+// (VALU) instead of two ds_bpermute round trips in the softmax's dependent chain
+__device__ __forceinline__ float xor_max_16_32(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const unsigned v = __float_as_uint(x);
+  const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
 #ifndef FD_FLASH_TR_EARLY
 #define FD_FLASH_TR_EARLY 1
 #endif
@@ -120,7 +131,14 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) o[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float mrow[2] = {-INFINITY, -INFINITY}, lrow_sum[2] = {0.f, 0.f};
+  float mrow[2] = {-INFINITY, -INFINITY};
+  // softmax denominators on the MFMA pipe: lsum[qb] += ones(16 x 32) . P^T -- every row of the 16 x 16
+  // block is the running sum for query column fr, of the same bf16 P the numerator uses (32 VALU adds
+  // per tile traded for 4 MFMAs)
+  f32x4 lsum[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+  V8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (T)1.0f;
 
   typedef f32x4 Sc[4][2];
   // S^T(tile in buffer BUF) = K Q^T  (16 MFMAs)
@@ -199,10 +217,8 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[kb][qb][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xor_max_16_32(mx);
       const float mnew = fmaxf(mrow[qb], mx * scale_log2);
-      float ls = 0.f;
       float pv[4][4];
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
@@ -212,17 +228,15 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
           // numerator already divided by a sum >= 1)
           const float e = __builtin_amdgcn_exp2f(fmaf(sc[kb][qb][i], scale_log2, -mnew));
           pv[kb][i] = e;
-          ls += e;
         }
       // exact skip of the O / l rescale when no query of this wave raised its running max (most tiles
       // after the first few): alpha would be exactly 1
       if (__any(mnew != mrow[qb])) {
         const float alpha = __builtin_amdgcn_exp2f(mrow[qb] - mnew);
-        lrow_sum[qb] *= alpha;
+        lsum[qb] *= alpha;
 #pragma unroll
         for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
       }
-      lrow_sum[qb] += ls;
       mrow[qb] = mnew;
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -250,6 +264,11 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
         o[db][0] = mfma16x16x32(vf, pf[0][s2], o[db][0]);
         o[db][1] = mfma16x16x32(vf, pf[1][s2], o[db][1]);
       }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      lsum[0] = mfma16x16x32(ones, pf[0][s2], lsum[0]);
+      lsum[1] = mfma16x16x32(ones, pf[1][s2], lsum[1]);
     }
     if (t + 1 < nt) {
       // tile t+1 landed (tile t+2, if issued, may still fly); every wave done reading tile t
@@ -283,10 +302,7 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
   // ---- finalise: lane holds O^T[d = db*16 + 4*fg + j][q = qb*16 + fr]
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
-    float l = lrow_sum[qb];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = 1.0f / l;
+    const float inv = 1.0f / lsum[qb][0];
     const int q = q0 + qb * 16 + fr;
     if (q >= Lq) continue;
     T* orow = O + (long long)b * obs + (long long)q * ldo + h * 64;

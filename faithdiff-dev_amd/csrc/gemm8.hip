@@ -39,12 +39,13 @@ __device__ __forceinline__ void vm_wait() {
 // above) and 64 x 160 over 4 waves (one wave per SIMD, 32 x 80 each: the M = 2048 projections' 256-tile
 // launches, where the previous 4-wave kernel split each K step over two waves and exposed the LDS-read
 // latency in front of every MFMA group).
-template <typename T, int BM, int BN, int NW, int WAVES_M, bool CONV, bool GEGLU, typename TO>
+template <typename T, int BM, int BN, int NW, int WAVES_M, int NS, bool CONV, bool GEGLU, typename TO>
 __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, const int S, const int gm_mode,
                                                         float* __restrict__ slabs, unsigned* __restrict__ counters) {
   typedef typename VecT<T>::v8 V8;
   constexpr bool SCHED = FD_GEMM8_SCHED;
-  constexpr int NS = 3, NTHR = 64 * NW;
+  constexpr int NTHR = 64 * NW;
+  static_assert(NS >= 3 && NS <= 5, "ring depth");
   constexpr int WAVES_N = NW / WAVES_M;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int MT = WM / 16, NT = WN / 16;
@@ -170,8 +171,13 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (w + NW * i) * 1024), 16, 0, 0);
   };
   // all but the youngest `ahead` stages of this wave's loads have landed
-  auto wait_ahead = [&](int ahead) {
-    if (ahead >= 2) {
+  auto wait_ahead = [&](int ahead) {  // ahead <= NS - 1 (the prologue); NS - 2 in the steady loop
+    constexpr int P4 = NS >= 5 ? 4 : 0, P3 = NS >= 4 ? 3 : 0;
+    if (NS >= 5 && ahead >= 4) {
+      if (hi) vm_wait<P4 * PER_HI>(); else vm_wait<P4 * PER_LO>();
+    } else if (NS >= 4 && ahead == 3) {
+      if (hi) vm_wait<P3 * PER_HI>(); else vm_wait<P3 * PER_LO>();
+    } else if (ahead == 2) {
       if (hi) vm_wait<2 * PER_HI>(); else vm_wait<2 * PER_LO>();
     } else if (ahead == 1) {
       if (hi) vm_wait<PER_HI>(); else vm_wait<PER_LO>();
@@ -179,6 +185,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
       vm_wait<0>();
     }
   };
+
 
   const int fr = lane & 15, fg = lane >> 4;
   auto read_frags = [&](int buf, int h, V8 (&af)[MT], V8 (&bf)[NT]) {
@@ -215,10 +222,10 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   // (LDS reads retired before the barrier) use the builtin, so it does not re-wait them -- and with
   // them the next stage's fragment reads -- in front of the second MFMA half (an inline-asm lgkmcnt is
   // invisible to its waitcnt pass).  Only the LDS-DMA counts are inline asm (it does not track them).
-  stage(kb, 0);
-  if (nkl > 1) stage(kb + 1, 1);
-  if (nkl > 2) stage(kb + 2, 2);
-  wait_ahead(min(nkl - 1, 2));
+#pragma unroll
+  for (int s0 = 0; s0 < NS; ++s0)
+    if (s0 < nkl) stage(kb + s0, s0);
+  wait_ahead(min(nkl - 1, NS - 1));
   __builtin_amdgcn_s_barrier();
   V8 a0[MT], b0[NT], a1[MT], b1[NT];
   read_frags(0, 0, a0, b0);
@@ -241,8 +248,8 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     wait_ahead(ahead);                   // stage kt+1 landed (kt+2 may still fly)
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage kt retired
     __builtin_amdgcn_s_barrier();        // ... and every wave's; stage kt+1 visible to all
-    if (refill) stage(kb + kt + 3, buf);
-    buf = buf == 2 ? 0 : buf + 1;
+    if (refill) stage(kb + kt + NS, buf);
+    buf = buf == NS - 1 ? 0 : buf + 1;
     read_frags(buf, 0, a0, b0);
     mma(a1, b1);
     if (SCHED) {
@@ -270,8 +277,8 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     }
   };
   int kt = 0;
-  for (; kt < nkl - 3; ++kt) step(true, 1, kt);
-  for (; kt < nkl - 1; ++kt) step(false, kt + 2 < nkl ? 1 : 0, kt);
+  for (; kt < nkl - NS; ++kt) step(true, NS - 2, kt);
+  for (; kt < nkl - 1; ++kt) step(false, min(NS - 2, nkl - 2 - kt), kt);
   read_frags(buf, 1, a1, b1);
   mma(a0, b0);
   mma(a1, b1);
@@ -522,7 +529,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
 namespace {
 
 struct Plan8 {
-  int bm, bn, nw, waves_m, S, group_m, tiles;
+  int bm, bn, nw, waves_m, ns, S, group_m, tiles;
 };
 
 int env_i(const char* n, int d) {
@@ -548,22 +555,22 @@ int choose_split(int m_ref, int N, int K, int bn) {
   return s < 1 ? 1 : s;
 }
 
-template <typename T, typename TO, int BM, int BN, int NW, int WAVES_M>
+template <typename T, typename TO, int BM, int BN, int NW, int WAVES_M, int NS>
 int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
   dim3 grid(pl.tiles * pl.S), block(64 * NW);
   float* slabs = (float*)((char*)p->ws + 65536 * sizeof(unsigned));
   unsigned* cnt = (unsigned*)p->ws;
   if (p->conv) {
-    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, true, false, TO>), grid, block, 0, s, *p, pl.S,
+    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, true, false, TO>), grid, block, 0, s, *p, pl.S,
                        pl.group_m, slabs, cnt);
   } else if (p->act == FD_ACT_GEGLU) {
     if constexpr ((BN / (NW / WAVES_M)) % 32 == 0)
-      hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, false, true, TO>), grid, block, 0, s, *p, pl.S,
+      hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, true, TO>), grid, block, 0, s, *p, pl.S,
                          pl.group_m, slabs, cnt);
     else
       return FD_ERR_ARG;
   } else {
-    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, false, false, TO>), grid, block, 0, s, *p, pl.S,
+    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO>), grid, block, 0, s, *p, pl.S,
                        pl.group_m, slabs, cnt);
   }
   FD_LAUNCH_CHECK();
@@ -577,13 +584,15 @@ int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
 // the 4-wave kernel sums each K step's two halves in separate waves, these kernels in one accumulator,
 // and any tile shape of the same kernel family gives the same k order.
 static int plan8(const fd_gemm_params* p, Plan8* pl) {
-  static int enabled = -1, force_s = 0, force_gm = 0, r4 = 1, pair128 = 0;
+  static int enabled = -1, force_s = 0, force_gm = 0, r4 = 1, pair128 = 0, r4_ns = 3, b4 = 0;
   if (enabled < 0) {
     enabled = env_i("FD_GEMM8", 1);
     force_s = env_i("FD_GEMM8_S", 0);
     force_gm = env_i("FD_GEMM8_GM", 0);
     r4 = env_i("FD_GEMM_R4", 1);  // 64 x 160 one-wave-per-SIMD kernel: 0 off, 1 <= 256 tiles, 2 every non-GEGLU
     pair128 = env_i("FD_GEMM_P128", 0);
+    r4_ns = env_i("FD_GEMM_R4_NS", 3);
+    b4 = env_i("FD_GEMM_B4", 0);
   }
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if (!enabled || p->batch > 1 || p->K < 128) return 0;
@@ -594,9 +603,23 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
   q.bn = 128;
   q.nw = 8;
   q.waves_m = 4;
+  q.ns = 3;
   q.S = (m_ref >= 256 && p->N >= 128) ? (force_s > 0 ? force_s : choose_split(m_ref, p->N, p->K, q.bn)) : 0;
   if (q.S <= 0) {
     const long long tiles_ref = (long long)((m_ref + 63) / 64) * ((p->N + 159) / 160);
+    const long long tiles128 = (long long)((m_ref + 127) / 128) * ((p->N + 159) / 160);
+    if (b4 && p->act != FD_ACT_GEGLU && p->N >= 160 && tiles128 >= 256) {
+      // large M (the 64^2 / 128^2 levels): 128 x 160 tiles, one wave per SIMD, 0.64x the operand bytes
+      // per output of the 64 x 160 tile
+      q.bm = 128;
+      q.bn = 160;
+      q.nw = 4;
+      q.waves_m = 2;
+      q.ns = 3;
+      q.S = 1;
+      goto planned;
+    }
+    {
     const bool ok = r4 && p->act != FD_ACT_GEGLU && m_ref >= 64 && p->N >= 160 &&
                     (r4 == 2 || (!p->conv && tiles_ref <= 256));
     if (!ok) return 0;
@@ -604,13 +627,17 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     q.bn = 160;
     q.nw = 4;
     q.waves_m = 2;
+    q.ns = r4_ns;
     q.S = 1;
     if (pair128 && m_ref >= 128 && tiles_ref <= 256 && p->K >= 1024) {
       // 128 x 160 tiles with K split in two (pairwise combine): 0.64x the operand bytes per CU
       q.bm = 128;
+      q.ns = 3;
       q.S = 2;
     }
+    }
   }
+planned:
   if (q.S > p->K / 64) q.S = p->K / 64;
   const int tiles_m = (p->M + q.bm - 1) / q.bm, tiles_n = (p->N + q.bn - 1) / q.bn;
   q.tiles = tiles_m * tiles_n;
@@ -650,14 +677,18 @@ extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream) {
   }
   hipStream_t s = (hipStream_t)stream;
   int rc;
-#define FD_G8(BM_, BN_, NW_, WM_) \
-  FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, rc = (launch8<T, TO, BM_, BN_, NW_, WM_>(p, pl, s))))
+#define FD_G8(BM_, BN_, NW_, WM_, NS_) \
+  FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, rc = (launch8<T, TO, BM_, BN_, NW_, WM_, NS_>(p, pl, s))))
   if (pl.bm == 256) {
-    FD_G8(256, 128, 8, 4);
+    FD_G8(256, 128, 8, 4, 3);
   } else if (pl.bm == 128) {
-    FD_G8(128, 160, 4, 2);
+    FD_G8(128, 160, 4, 2, 3);
+  } else if (pl.ns >= 5) {
+    FD_G8(64, 160, 4, 2, 5);
+  } else if (pl.ns == 4) {
+    FD_G8(64, 160, 4, 2, 4);
   } else {
-    FD_G8(64, 160, 4, 2);
+    FD_G8(64, 160, 4, 2, 3);
   }
 #undef FD_G8
   return rc == FD_OK ? 1 : rc;

@@ -19,8 +19,13 @@ bf = torch.bfloat16
 SHAPES = ["2048x1280x1280", "2048x1280x5120", "2048x3840x1280", "2048x10240x1280:geglu", "8192x640x640"]
 if len(sys.argv) > 1:
     SHAPES = sys.argv[1:]
-tag = {k: v for k, v in os.environ.items() if k.startswith("FD_GEMM")}
+tag = {k: v for k, v in os.environ.items() if k.startswith(("FD_GEMM", "PROBE_"))}
 REP = int(os.environ.get("PROBE_REP", "20"))
+# PROBE_COPIES=n: n distinct weight copies cycled through the graph (n x |W| past the 256 MB Infinity Cache
+# gives cold weights, as inside a UNet forward where every weight is read once)
+COPIES = int(os.environ.get("PROBE_COPIES", "1"))
+if COPIES > 1:
+    REP = max(REP, COPIES)
 g = torch.Generator(device="cuda").manual_seed(0)
 for s in SHAPES:
     if s.startswith("conv"):
@@ -36,8 +41,13 @@ for s in SHAPES:
         M, N, K = (int(v) for v in dims.split("x"))
         a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).to(bf)
         w = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) / K ** 0.5).to(bf)
+        ws_ = [w] + [w.clone() for _ in range(COPIES - 1)]
         out = torch.empty(M, N // 2 if act == "geglu" else N, device="cuda", dtype=bf)
-        fn = lambda: ops.gemm(a, w, out=out, act=act)  # noqa: E731
+        ctr = [0]
+
+        def fn(a=a, ws_=ws_, out=out, act=act):
+            ctr[0] += 1
+            return ops.gemm(a, ws_[ctr[0] % len(ws_)], out=out, act=act)
         flops = 2 * M * N * K
     st = torch.cuda.Stream()
     with torch.cuda.stream(st):
