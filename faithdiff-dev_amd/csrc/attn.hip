@@ -19,13 +19,19 @@
 // capping arch VGPRs at 128 and spilling the O / S accumulators through AGPR moves (192 v_accvgpr per tile).
 // max over lanes l, l^16, l^32, l^48 (the 4 row groups of a 16 x 16 MFMA block): gfx950 permlane swaps
 // (VALU) instead of two ds_bpermute round trips in the softmax's dependent chain
+// (plain v_max_f32 in asm: fmaxf on a permlane result makes hipcc canonicalise both inputs first)
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ float xor_max_16_32(float x) {
   const unsigned u = __float_as_uint(x);
   const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  x = vmax_raw(__uint_as_float(a[0]), __uint_as_float(a[1]));
   const unsigned v = __float_as_uint(x);
   const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+  return vmax_raw(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
 #ifndef FD_FLASH_TR_EARLY

@@ -589,7 +589,9 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     enabled = env_i("FD_GEMM8", 1);
     force_s = env_i("FD_GEMM8_S", 0);
     force_gm = env_i("FD_GEMM8_GM", 0);
-    r4 = env_i("FD_GEMM_R4", 1);  // 64 x 160 one-wave-per-SIMD kernel: 0 off, 1 <= 256 tiles, 2 every non-GEGLU
+    // 64 x 160 one-wave-per-SIMD kernel: 0 off (default: 0.5 % slower in the bench step than the 4-wave
+    // kernel though faster in isolation), 1 <= 256 tiles, 2 every non-GEGLU
+    r4 = env_i("FD_GEMM_R4", 0);
     pair128 = env_i("FD_GEMM_P128", 0);
     r4_ns = env_i("FD_GEMM_R4_NS", 3);
     b4 = env_i("FD_GEMM_B4", 0);
