@@ -48,7 +48,8 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int t
 // through LDS before the epilogue.  Same LDS traffic and tile shape, but two waves per SIMD, so one
 // wave's LDS fragment reads overlap the other's MFMAs (with one 4-wave workgroup per CU -- 256-tile
 // launches -- the single wave per SIMD otherwise serialises them).
-template <typename T, int BM, int BN, int WM, int WN, int NS, bool CONV, bool GEGLU, typename TO, int KS>
+template <typename T, int BM, int BN, int WM, int WN, int NS, bool CONV, bool GEGLU, typename TO, int KS,
+          bool LNF = false>
 __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, int swz) {
   typedef typename VecT<T>::v8 V8;
   constexpr int WAVES_N = BN / WN;
@@ -64,8 +65,20 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   constexpr int BNO = GEGLU ? BN / 2 : BN;   // output columns of the tile
   constexpr int LDE = BNO + 4;               // fp32 epilogue staging row stride (16-B aligned rows)
   constexpr int EPB = (KS == 2 && BN + 4 > LDE) ? BM * (BN + 4) * 4 : BM * LDE * 4;
-  constexpr int SMEM = (NS * STAGE > EPB) ? NS * STAGE : EPB;
+  // LN-fold producer (64 x 160 tiles only, the configuration fd_gemm forces for it): per-(row, 8-column
+  // slot) (sum, sumsq) after the fp32 staging tile
+  constexpr bool LNP = (BM == 64 && BN == 160 && !GEGLU && !CONV);
+  constexpr int LNS_OFF = (EPB + 15) / 16 * 16, LNS = LNP ? BM * (BNO / 8) * 8 : 0;
+  // LN-fold consumer (LNF): (mean, rstd) of the tile's rows and ln_c of its columns, in the same LDS object
+  // as the ring (a second __shared__ array makes hipcc assume ds_reads may alias the LDS-DMA targets and
+  // drain vmcnt(0) in front of them)
+  // (after the ring AND the staging areas: ln_cs is written while other waves may still read the ring)
+  constexpr int LNC_OFF = (NS * STAGE > LNS_OFF + LNS) ? NS * STAGE : LNS_OFF + LNS;
+  constexpr int LNC = LNF ? BM * 8 + BN * 4 : 0;
+  constexpr int SMEM = LNC_OFF + LNC;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+  float2* const ln_tab = (float2*)(smem + LNC_OFF);
+  float* const ln_cs = (float*)(smem + LNC_OFF + BM * 8);
 
   constexpr int NTHR = 256 * KS;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -82,6 +95,21 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   int tm, tn;
   tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, swz, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
+  // LN-fold consumer: the producer's (sum, sumsq) partials of this tile's rows and ln_c of its columns,
+  // requested before the first operand stage so their latency is hidden by the K loop (unconditional
+  // 16-B loads, index clamped, lnP even: a conditional load per partial gets sunk into the fold's
+  // branches, one dependent round trip each)
+  const int lnP = p.K / 160;
+  f32x4 lnv4[LNF ? 4 : 1];
+  float lncv = 0.f;
+  if (LNF) {
+    if (tid < BM) {
+      const f32x4* src = (const f32x4*)((const float2*)p.ln_in + (long long)min(m0 + tid, p.M - 1) * lnP);
+#pragma unroll
+      for (int i = 0; i < (LNF ? 4 : 1); ++i) lnv4[i] = src[min(i, lnP / 2 - 1)];
+    }
+    if (tid < BN) lncv = p.ln_c[min(n0 + tid, p.N - 1)];
+  }
   const long long bz = blockIdx.z;
   const T* __restrict__ A = (const T*)p.A + bz * p.strideA;
   const T* __restrict__ Bw = (const T*)p.B + bz * p.strideB;
@@ -204,6 +232,9 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
     }
   }
 
+  constexpr bool lnf = LNF;
+  if (LNF && tid < BN) ln_cs[tid] = lncv;
+
   // ---- epilogue, phase 1: acc[mi][ni][j] = C[wm*WM + mi*16 + 4*fg + j][wn*WN + ni*16 + fr] (tile-local)
   // -> alpha, bias, per-row-group bias, activation / GEGLU in fp32 -> LDS tile [BM][LDE] (fp32)
   __syncthreads();  // every wave is done reading the operand ring
@@ -238,28 +269,62 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   const float* __restrict__ bias = p.bias;
   const float* __restrict__ rbias = p.rowbias;
   const int act = p.act;
+  if (lnf) {  // (mean, rstd) per row from the partials, fp64 fold in a fixed order
+    if (tid < BM) {
+      double s = 0.0, q = 0.0;
+#pragma unroll
+      for (int i = 0; i < (LNF ? 4 : 1); ++i)
+        if (2 * i < lnP) {
+          s += lnv4[i][0];
+          q += lnv4[i][1];
+          s += lnv4[i][2];
+          q += lnv4[i][3];
+        }
+      const double ik = 1.0 / 1024.0 * (1024.0f / (float)K);  // 1/K without an fp64 divide
+      const double mu = s * ik;
+      double var = q * ik - mu * mu;
+      if (var < 0.0) var = 0.0;
+      ln_tab[tid] = make_float2((float)mu, rsqrtf((float)var + p.ln_eps));
+    }
+    __syncthreads();
+  }
   if (!kh) {
     if (GEGLU) {
       float gbh[NT / 2 > 0 ? NT / 2 : 1], gbg[NT / 2 > 0 ? NT / 2 : 1];
+      float lch[NT / 2 > 0 ? NT / 2 : 1], lcg[NT / 2 > 0 ? NT / 2 : 1];
 #pragma unroll
       for (int q = 0; q < NT / 2; ++q) {
         const int np = min(n0 + wn * WN + 2 * q * 16 + fr, N - 17);
         gbh[q] = bias ? bias[np] : 0.f;
         gbg[q] = bias ? bias[np + 16] : 0.f;
+        lch[q] = lnf ? ln_cs[min(wn * WN + 2 * q * 16 + fr, BN - 17)] : 0.f;
+        lcg[q] = lnf ? ln_cs[min(wn * WN + 2 * q * 16 + fr, BN - 17) + 16] : 0.f;
       }
 #pragma unroll
-      for (int mi = 0; mi < MT; ++mi)
+      for (int mi = 0; mi < MT; ++mi) {
+        float2 st[LNF ? 4 : 1];  // read ahead of the staging stores (same LDS object)
+        if (LNF) {
+#pragma unroll
+          for (int j = 0; j < (LNF ? 4 : 1); ++j) st[j] = ln_tab[wm * WM + mi * 16 + fg * 4 + j];
+        }
 #pragma unroll
         for (int ni = 0; ni + 1 < NT; ni += 2) {
           const int col = (wn * WN) / 2 + (ni / 2) * 16 + fr;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int row = wm * WM + mi * 16 + fg * 4 + j;
-            const float h = acc[mi][ni][j] * alpha + gbh[ni / 2];
-            const float g = acc[mi][ni + 1][j] * alpha + gbg[ni / 2];
+            float h = acc[mi][ni][j] * alpha, g = acc[mi][ni + 1][j] * alpha;
+            if (LNF) {
+              const float2 t = st[j & (LNF ? 3 : 0)];
+              h = t.y * (h - t.x * lch[ni / 2]);
+              g = t.y * (g - t.x * lcg[ni / 2]);
+            }
+            h += gbh[ni / 2];
+            g += gbg[ni / 2];
             ep[row * LDE + col] = h * gelu_f(g);
           }
         }
+      }
     } else {
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi)
@@ -286,6 +351,8 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   constexpr int TOT = BM * VPR;
   constexpr int ITER = (TOT + NTHR - 1) / NTHR;
   typedef __attribute__((ext_vector_type(8))) TO TO8;
+  const bool lno = LNP && p.ln_out != nullptr;
+  float2* lnslot = (float2*)(smem + LNS_OFF);
   if (vec && m0 + BM <= M && n0o + BNO <= Nout) {
     float v[ITER][8], bv[ITER][8], rv[ITER][8];
     TO8 res[ITER];
@@ -316,6 +383,11 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
         const int r = e / VPR, cv = e - (e / VPR) * VPR;
         const int m = m0 + r, n = n0o + cv * 8;
         if (!GEGLU) {
+          if (lnf) {
+            const float2 st = ln_tab[r];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = st.y * (v[it][i] - st.x * ln_cs[cv * 8 + i]);
+          }
           if (bias) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[it][i] += bv[it][i];
@@ -343,23 +415,56 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
         *(TO8*)(C + (long long)m * p.ldc + n) = o;
+        if (lno) {  // statistics of the values as stored (what the consumer GEMM multiplies)
+          float s = 0.f, q = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float f = (float)o[i];
+            s += f;
+            q += f * f;
+          }
+          lnslot[r * VPR + cv] = make_float2(s, q);
+        }
       }
     }
   } else {  // edge tiles / unaligned operands: scalar, bounds-checked
     for (int e = tid; e < TOT; e += NTHR) {
       const int r = e / VPR, cv = e - (e / VPR) * VPR;
       const int m = m0 + r, n = n0o + cv * 8;
-      if (m >= M || n >= Nout) continue;
-      for (int i = 0; i < 8 && n + i < Nout; ++i) {
-        float x = ep[r * LDE + cv * 8 + i];
-        if (!GEGLU) {
-          if (bias) x += bias[n + i];
-          if (rbias) x += rbias[(long long)(m / p.rows_per_group) * p.rowbias_ld + n + i];
-          x = act_f(x, act);
+      float s = 0.f, q = 0.f;
+      if (m < M && n < Nout) {
+        for (int i = 0; i < 8 && n + i < Nout; ++i) {
+          float x = ep[r * LDE + cv * 8 + i];
+          if (!GEGLU) {
+            if (lnf) {
+              const float2 st = ln_tab[r];
+              x = st.y * (x - st.x * ln_cs[cv * 8 + i]);
+            }
+            if (bias) x += bias[n + i];
+            if (rbias) x += rbias[(long long)(m / p.rows_per_group) * p.rowbias_ld + n + i];
+            x = act_f(x, act);
+          }
+          if (R) x += (float)R[(long long)m * p.ldr + n + i];
+          const TO o = (TO)x;
+          C[(long long)m * p.ldc + n + i] = o;
+          s += (float)o;
+          q += (float)o * (float)o;
         }
-        if (R) x += (float)R[(long long)m * p.ldr + n + i];
-        C[(long long)m * p.ldc + n + i] = (TO)x;
       }
+      if (lno) lnslot[r * VPR + cv] = make_float2(s, q);
+    }
+  }
+  if (lno) {  // per-row partial over this tile's 160 columns, slots summed in column order
+    __syncthreads();
+    if (tid < BM && m0 + tid < M) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int c = 0; c < VPR; ++c) {
+        const float2 v2 = lnslot[tid * VPR + c];
+        s += v2.x;
+        q += v2.y;
+      }
+      ((float2*)p.ln_out)[(long long)(m0 + tid) * (N / 160) + n0 / 160] = make_float2(s, q);
     }
   }
 }
@@ -372,10 +477,17 @@ static int launch_cfg(const fd_gemm_params* p, hipStream_t s, int swz) {
     if (p->act == FD_ACT_GEGLU) return FD_ERR_ARG;
     hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, true, false, TO, KS>), grid, block, 0, s, *p, swz);
   } else if (p->act == FD_ACT_GEGLU) {
-    if constexpr (WN % 32 == 0)
-      hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, true, TO, KS>), grid, block, 0, s, *p, swz);
-    else
+    if constexpr (WN % 32 == 0) {
+      if (p->ln_in)
+        hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, true, TO, KS, true>), grid, block, 0, s, *p,
+                           swz);
+      else
+        hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, true, TO, KS>), grid, block, 0, s, *p, swz);
+    } else {
       return FD_ERR_ARG;
+    }
+  } else if (p->ln_in) {
+    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, false, TO, KS, true>), grid, block, 0, s, *p, swz);
   } else {
     hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM, WN, NS, false, false, TO, KS>), grid, block, 0, s, *p, swz);
   }
@@ -443,6 +555,7 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
     g_swz = env_int("FD_GEMM_SWZ", 1) | (env_int("FD_GEMM_MODE", 0) << 4);
   }
   int cfg = g_cfg >= 0 && g_cfg < CFG_COUNT ? g_cfg : pick_cfg(p);
+  if (p->ln_out) cfg = CFG_64x160;  // LN-fold producer: partials per 160 columns, whatever M (batch-invariant)
   // ring depth: 4 stages (1 WG/CU) pays only on long K when one wave of tiles covers the launch; 2 stages
   // (2-3 co-resident WGs/CU) otherwise (scripts/gemm_sweep.py + in-situ traces)
   const long long tiles = (long long)(p->batch > 0 ? p->batch : 1) * ((p->M + CFG_BM[cfg] - 1) / CFG_BM[cfg]) *
@@ -474,9 +587,15 @@ extern "C" int fd_gemm(const fd_gemm_params* p, void* stream) {
     if (p->stride != 1 && p->stride != 2) return FD_ERR_SHAPE;
     if (p->upsample && (p->stride != 1 || p->pad != 1 || p->Hout < p->Hin || p->Wout < p->Win)) return FD_ERR_SHAPE;
   }
-  const int r8 = fd_gemm8_try(p, stream);
-  if (r8 < 0) return r8;
-  if (r8 == 1) return FD_OK;
+  if (p->ln_out && (p->N % 160 || p->act == FD_ACT_GEGLU || p->batch > 1 || p->conv ||
+                    (p->out_dtype != FD_BF16 && p->out_dtype != FD_F16)))
+    return FD_ERR_SHAPE;
+  if (p->ln_in && (p->K % 320 || p->K > 1280 || p->batch > 1 || p->conv || !p->ln_c)) return FD_ERR_SHAPE;
+  if (!p->ln_out) {
+    const int r8 = fd_gemm8_try(p, stream);
+    if (r8 < 0) return r8;
+    if (r8 == 1) return FD_OK;
+  }
   hipStream_t s = (hipStream_t)stream;
   FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, return dispatch_tiles<T, TO>(p, s)));
 }

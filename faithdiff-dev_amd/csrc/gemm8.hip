@@ -39,7 +39,8 @@ __device__ __forceinline__ void vm_wait() {
 // above) and 64 x 160 over 4 waves (one wave per SIMD, 32 x 80 each: the M = 2048 projections' 256-tile
 // launches, where the previous 4-wave kernel split each K step over two waves and exposed the LDS-read
 // latency in front of every MFMA group).
-template <typename T, int BM, int BN, int NW, int WAVES_M, int NS, bool CONV, bool GEGLU, typename TO>
+template <typename T, int BM, int BN, int NW, int WAVES_M, int NS, bool CONV, bool GEGLU, typename TO,
+          bool LNF = false>
 __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, const int S, const int gm_mode,
                                                         float* __restrict__ slabs, unsigned* __restrict__ counters) {
   typedef typename VecT<T>::v8 V8;
@@ -61,10 +62,16 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   // epilogue staged fp32 [EROWS][BNO+4] in the ring's LDS: the whole tile when it fits, else 128-row halves
   constexpr int EROWS = (BM * LDE * 4 <= NS * STAGE) ? BM : 128;
   constexpr int EPB = EROWS * LDE * 4;
-  constexpr int SMEM = (NS * STAGE > EPB) ? NS * STAGE : EPB;
+  // LN-fold consumer (LNF): (mean, rstd) of the tile's rows and ln_c of its columns after the ring / staging
+  // area, in the same LDS object (a second __shared__ array makes hipcc assume ds_reads may alias the
+  // LDS-DMA targets and drain vmcnt(0) in front of them)
+  constexpr int LNC_OFF = (NS * STAGE > EPB) ? NS * STAGE : EPB;
+  constexpr int SMEM = LNC_OFF + (LNF ? BM * 8 + BN * 4 : 0);
   static_assert(SMEM <= 163840, "LDS");
   static_assert(!GEGLU || (WN % 32 == 0), "GEGLU pairs must not straddle waves");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+  float2* const ln_tab = (float2*)(smem + LNC_OFF);
+  float* const ln_cs = (float*)(smem + LNC_OFF + BM * 8);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -92,6 +99,21 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   }
   const int tile_id = tm * tiles_n + tn;
   const int m0 = tm * BM, n0 = tn * BN;
+  // LN-fold consumer: the producer's (sum, sumsq) partials of this tile's rows and ln_c of its columns,
+  // requested before the first operand stage so their latency is hidden by the K loop (unconditional
+  // 16-B loads, index clamped, lnP even: a conditional load per partial gets sunk into the fold's
+  // branches, one dependent round trip each)
+  const int lnP = p.K / 160;
+  f32x4 lnv4[LNF ? 4 : 1];
+  float lncv = 0.f;
+  if (LNF) {
+    if (tid < BM) {
+      const f32x4* src = (const f32x4*)((const float2*)p.ln_in + (long long)min(m0 + tid, p.M - 1) * lnP);
+#pragma unroll
+      for (int i = 0; i < (LNF ? 4 : 1); ++i) lnv4[i] = src[min(i, lnP / 2 - 1)];
+    }
+    if (tid < BN) lncv = p.ln_c[min(n0 + tid, p.N - 1)];
+  }
   const int nk = K / 64;
   const int kb = (int)((long long)split * nk / S), ke = (int)((long long)(split + 1) * nk / S);
   const int nkl = ke - kb;
@@ -279,6 +301,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   int kt = 0;
   for (; kt < nkl - NS; ++kt) step(true, NS - 2, kt);
   for (; kt < nkl - 1; ++kt) step(false, min(NS - 2, nkl - 2 - kt), kt);
+  constexpr bool lnf = LNF;
   read_frags(buf, 1, a1, b1);
   mma(a0, b0);
   mma(a1, b1);
@@ -412,6 +435,23 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
       gbg[q] = bias ? bias[np + 16] : 0.f;
     }
   }
+  if (LNF && tid < BN) ln_cs[tid] = lncv;
+  if (LNF && tid < BM) {  // (mean, rstd) per row, fp64 fold in a fixed order; read after the first barrier below
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int i = 0; i < (LNF ? 4 : 1); ++i)
+      if (2 * i < lnP) {
+        s += lnv4[i][0];
+        q += lnv4[i][1];
+        s += lnv4[i][2];
+        q += lnv4[i][3];
+      }
+    const double ik = 1.0 / 1024.0 * (1024.0f / (float)K);  // 1/K without an fp64 divide
+    const double mu = s * ik;
+    double var = q * ik - mu * mu;
+    if (var < 0.0) var = 0.0;
+    ln_tab[tid] = make_float2((float)mu, rsqrtf((float)var + p.ln_eps));
+  }
   const bool vec = (Nout % 8 == 0) && (p.ldc % 8 == 0) && ((((unsigned long long)C) & 15) == 0) &&
                    (!R || ((p.ldr % 8 == 0) && ((((unsigned long long)R) & 15) == 0))) &&
                    (GEGLU || !bias || ((((unsigned long long)bias) & 15) == 0)) &&
@@ -426,13 +466,28 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
       for (int mi = 0; mi < MT; ++mi) {
         const int rl = wm * WM + mi * 16 + fg * 4 - half * EROWS;
         if (GEGLU) {
+          // LN-fold operands read into registers ahead of the staging stores (same LDS object: hipcc would
+          // otherwise re-read them after every store)
+          float2 st[LNF ? 4 : 1];
+          float lcn[LNF ? NT : 1];
+          if (LNF) {
+#pragma unroll
+            for (int j = 0; j < (LNF ? 4 : 1); ++j) st[j] = ln_tab[rl + j + half * EROWS];
+#pragma unroll
+            for (int ni = 0; ni < (LNF ? NT : 1); ++ni) lcn[ni] = ln_cs[wn * WN + ni * 16 + fr];
+          }
 #pragma unroll
           for (int ni = 0; ni < NT; ni += 2) {
             const int col = (wn * WN) / 2 + (ni / 2) * 16 + fr;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              const float hv = acc[mi][ni][j] * alpha + gbh[ni / 2];
-              const float g = acc[mi][ni + 1][j] * alpha + gbg[ni / 2];
+              float hv = acc[mi][ni][j] * alpha, g = acc[mi][ni + 1][j] * alpha;
+              if (LNF) {
+                hv = st[j & (LNF ? 3 : 0)].y * (hv - st[j & (LNF ? 3 : 0)].x * lcn[ni % (LNF ? NT : 1)]);
+                g = st[j & (LNF ? 3 : 0)].y * (g - st[j & (LNF ? 3 : 0)].x * lcn[(ni + 1) % (LNF ? NT : 1)]);
+              }
+              hv += gbh[ni / 2];
+              g += gbg[ni / 2];
               ep[(rl + j) * LDE + col] = hv * gelu_f(g);
             }
           }
@@ -476,6 +531,11 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         const int r = e / VPR, cv = e % VPR;
         const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
         if (!GEGLU) {
+          if (lnf) {
+            const float2 st = ln_tab[half * EROWS + r];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = st.y * (v[it][i] - st.x * ln_cs[cv * 8 + i]);
+          }
           if (bias) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[it][i] += bv[it][i];
@@ -513,6 +573,10 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         for (int i = 0; i < 8 && n + i < Nout; ++i) {
           float x = ep[r * LDE + cv * 8 + i];
           if (!GEGLU) {
+            if (lnf) {
+              const float2 st = ln_tab[half * EROWS + r];
+              x = st.y * (x - st.x * ln_cs[cv * 8 + i]);
+            }
             if (bias) x += bias[n + i];
             if (rbias) x += rbias[(long long)(m / p.rows_per_group) * p.rowbias_ld + n + i];
             x = act_f(x, act);
@@ -564,11 +628,19 @@ int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, true, false, TO>), grid, block, 0, s, *p, pl.S,
                        pl.group_m, slabs, cnt);
   } else if (p->act == FD_ACT_GEGLU) {
-    if constexpr ((BN / (NW / WAVES_M)) % 32 == 0)
-      hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, true, TO>), grid, block, 0, s, *p, pl.S,
-                         pl.group_m, slabs, cnt);
-    else
+    if constexpr ((BN / (NW / WAVES_M)) % 32 == 0) {
+      if (p->ln_in)
+        hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, true, TO, true>), grid, block, 0, s, *p,
+                           pl.S, pl.group_m, slabs, cnt);
+      else
+        hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, true, TO>), grid, block, 0, s, *p, pl.S,
+                           pl.group_m, slabs, cnt);
+    } else {
       return FD_ERR_ARG;
+    }
+  } else if (p->ln_in) {
+    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO, true>), grid, block, 0, s, *p, pl.S,
+                       pl.group_m, slabs, cnt);
   } else {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO>), grid, block, 0, s, *p, pl.S,
                        pl.group_m, slabs, cnt);

@@ -34,6 +34,7 @@ class GemmParams(ctypes.Structure):
         ("Hout", c_int), ("Wout", c_int), ("stride", c_int), ("pad", c_int), ("upsample", c_int),
         ("A2", c_vp), ("C1", c_int),
         ("m_ref", c_int), ("ws", c_vp), ("ws_bytes", c_ll),
+        ("ln_out", c_vp), ("ln_in", c_vp), ("ln_c", c_vp), ("ln_eps", c_f),
     ]
 
 

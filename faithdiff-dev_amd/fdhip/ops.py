@@ -127,8 +127,11 @@ def _launch_gemm(p, what):
 
 def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=1, alpha=1.0, act="none",
          out_dtype=None, batch=1, M=None, N=None, K=None, lda=None, ldw=None, ldc=None, ldr=None,
-         stride_a=0, stride_w=0, stride_c=0, stride_r=0):
-    """out[M, N (N/2 for geglu)] = epi(alpha * a[M, K] @ w[N, K]^T); strides default to the tensors'."""
+         stride_a=0, stride_w=0, stride_c=0, stride_r=0, ln_out=None, ln_in=None, ln_c=None, ln_eps=1e-5):
+    """out[M, N (N/2 for geglu)] = epi(alpha * a[M, K] @ w[N, K]^T); strides default to the tensors'.
+    ln_out: fp32 [M, N/160, 2] -- also write per-row (sum, sumsq) partials of the stored output (LayerNorm
+    producer).  ln_in / ln_c: fold LayerNorm(a) into this GEMM (w = W * gamma, ln_c = rowsum(w), bias =
+    W . beta + b; see fold_layer_norm)."""
     K = a.shape[-1] if K is None else K
     N = w.shape[-2] if N is None else N
     ldw = w.stride(-2) if ldw is None else ldw
@@ -156,9 +159,26 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
     p.act = L.ACT[act]
     p.dtype = L.dtype_code(a.dtype)
     p.out_dtype = L.dtype_code(odt)
+    if ln_out is not None:
+        p.ln_out = ln_out.data_ptr()
+    if ln_in is not None:
+        p.ln_in, p.ln_c, p.ln_eps = ln_in.data_ptr(), ln_c.data_ptr(), ln_eps
     _attach_ws(p, a.device)
     _launch_gemm(p, "fd_gemm")
     return out
+
+
+def fold_layer_norm(w, gamma, beta, bias=None, dtype=torch.bfloat16):
+    """LayerNorm(x; gamma, beta) @ w^T + bias == rstd * (x @ w'^T - mean * c) + d  with
+    w' = w * gamma (per input column, rounded to the GEMM dtype), c = rowsum(w') of the rounded values and
+    d = w @ beta + bias (fp64).  Returns (w', c, d) for gemm(..., ln_in=..., ln_c=c, bias=d)."""
+    w64 = w.double()
+    wp = (w64 * gamma.double()[None, :]).to(dtype)
+    c = wp.double().sum(1).float()
+    d = w64 @ beta.double()
+    if bias is not None:
+        d = d + bias.double()
+    return wp.contiguous(), c.contiguous(), d.float().contiguous()
 
 
 def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C1=None, out=None, rowbias=None,

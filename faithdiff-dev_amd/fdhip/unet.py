@@ -13,9 +13,16 @@ MI355X-specific structure (not a translation of the reference's module graph):
     transformer blocks are ONE GEMM per forward ([ncfg*77, 2048] x [166400, 2048]^T), and one K/V pair
     [neg, pos] serves every tile of a batched forward (kv_mod = CFG width);
   * the up-block skip concat is folded into the conv1 gather (two-source implicit GEMM) after the
-    GroupNorm reads the materialised concat.
+    GroupNorm reads the materialised concat;
+  * the transformer blocks' LayerNorms (norm1/2/3) are folded into the GEMM pair around them: the
+    residual-stream GEMM (proj_in, attn out-projections, ff out) also writes per-row (sum, sumsq)
+    partials, and the next projection runs on the raw stream with W * gamma, finishing
+    rstd * (acc - mean * rowsum(W * gamma)) + W . beta + b in its epilogue (no LayerNorm launches; FD_LN_FOLD=0
+    restores them).
 Rows are [tile0 uncond, tile0 cond, tile1 uncond, ...]: several TLC tiles can share one forward.
 """
+import os
+
 import torch
 
 from . import arch
@@ -62,11 +69,30 @@ class HipUNet:
                            Fp(p + ".conv_shortcut.bias"))
             return r
 
+        self.ln_fold = os.environ.get("FD_LN_FOLD", "1") != "0"
+
+        def fold(w, n, bias=None):  # (W * gamma, rowsum, W . beta + b) on the device
+            dev = lambda t: t.to(self.device)  # noqa: E731
+            return ops.fold_layer_norm(dev(w), dev(sd[n + ".weight"]), dev(sd[n + ".bias"]),
+                                       None if bias is None else dev(bias), dtype)
+
         def t2d(p, c, layers):
             blocks = []
             for i in range(layers):
                 b = f"{p}.transformer_blocks.{i}"
                 ffw, ffb = ops.pack_geglu(sd[b + ".ff.net.0.proj.weight"], sd[b + ".ff.net.0.proj.bias"])
+                if self.ln_fold:
+                    blocks.append(dict(
+                        qkv_f=fold(torch.cat([sd[f"{b}.attn1.to_{n}.weight"] for n in "qkv"], 0), b + ".norm1"),
+                        o1=(W(b + ".attn1.to_out.0.weight"), Fp(b + ".attn1.to_out.0.bias")),
+                        q2_f=fold(sd[b + ".attn2.to_q.weight"], b + ".norm2"),
+                        kv2=_dev(torch.cat([sd[b + ".attn2.to_k.weight"], sd[b + ".attn2.to_v.weight"]], 0),
+                                 self.device, dtype),
+                        o2=(W(b + ".attn2.to_out.0.weight"), Fp(b + ".attn2.to_out.0.bias")),
+                        ff1_f=fold(ffw, b + ".norm3", ffb),
+                        ff2=(W(b + ".ff.net.2.weight"), Fp(b + ".ff.net.2.bias")),
+                    ))
+                    continue
                 blocks.append(dict(
                     n1=(Fp(b + ".norm1.weight"), Fp(b + ".norm1.bias")),
                     qkv=_dev(torch.cat([sd[f"{b}.attn1.to_{n}.weight"] for n in "qkv"], 0), self.device, dtype),
@@ -186,6 +212,8 @@ class HipUNet:
         C, heads, HW = t["c"], t["heads"], H * Wd
         M = B * HW
         h = ops.group_norm(x, *t["norm"], B, HW, C, 32, 1e-6, silu=False)
+        if self.ln_fold:
+            return self._t2d_folded(t, x, h, B, H, Wd)
         h = ops.gemm(h, t["pin"][0], bias=t["pin"][1])
         qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
         att = torch.empty((M, C), dtype=self.dtype, device=self.device)
@@ -206,6 +234,34 @@ class HipUNet:
             ops.layer_norm(h, *b["n3"], 1e-5, out=n)
             ff = ops.gemm(n, b["ff1"][0], bias=b["ff1"][1], act="geglu")
             ops.gemm(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
+        return ops.gemm(h, t["pout"][0], bias=t["pout"][1], residual=x)
+
+    def _t2d_folded(self, t, x, hn, B, H, Wd):
+        """_t2d with norm1/2/3 folded into the GEMMs (fd_gemm_params.ln_out / ln_in): `st` holds the
+        per-row (sum, sumsq) partials of the current residual stream h, per 160 columns."""
+        C, heads, HW = t["c"], t["heads"], H * Wd
+        M = B * HW
+        st = torch.empty((M, C // 160, 2), dtype=torch.float32, device=self.device)
+        h = ops.gemm(hn, t["pin"][0], bias=t["pin"][1], ln_out=st)
+        qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
+        att = torch.empty((M, C), dtype=self.dtype, device=self.device)
+        nb = len(t["blocks"])
+        for i, b in enumerate(t["blocks"]):
+            w, c, d = b["qkv_f"]
+            ops.gemm(h, w, bias=d, out=qkv, ln_in=st, ln_c=c)
+            ops.flash_attn(qkv, qkv[:, C:], qkv[:, 2 * C:], att, B, heads, HW, HW, 3 * C, 3 * C, 3 * C, C,
+                           HW * 3 * C, HW * 3 * C, HW * 3 * C, HW * C, kv_mod=0, scale=0.125)
+            ops.gemm(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h, ln_out=st)
+            w, c, d = b["q2_f"]
+            ops.gemm(h, w, bias=d, out=qkv[:, :C], ldc=3 * C, ln_in=st, ln_c=c)
+            kv = self._kv[:, b["kv_off"]:]
+            Lk, ldkv = self.Lk, self.kv_total
+            ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, ldkv, ldkv, C,
+                           HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self.ncfg, scale=0.125)
+            ops.gemm(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h, ln_out=st)
+            w, c, d = b["ff1_f"]
+            ff = ops.gemm(h, w, bias=d, act="geglu", ln_in=st, ln_c=c)
+            ops.gemm(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h, ln_out=st if i + 1 < nb else None)
         return ops.gemm(h, t["pout"][0], bias=t["pout"][1], residual=x)
 
     def _extras(self, x0, cond, B, H, Wd):

@@ -80,6 +80,17 @@ typedef struct fd_gemm_params {
   int m_ref;
   void* ws;
   long long ws_bytes;
+  /* LayerNorm folded across a GEMM pair (Transformer blocks' norm1/2/3, diffusers BasicTransformerBlock;
+   * replaces the separate LayerNorm launch).  Producer (ln_out != NULL; N % 160 == 0, no GEGLU, batch 1):
+   * also writes, per output row m and 160-column group g, (sum, sum of squares) of the STORED outputs
+   * to ln_out[m * (N / 160) + g] (float2).  Consumer (ln_in != NULL; K % 320 == 0, K <= 1280, batch 1):
+   * A is the producer's raw output x; B holds W' = W * gamma (per k), ln_c[n] = sum_k W'[n][k], bias =
+   * W . beta + b; the epilogue computes rstd_m * (acc - mean_m * ln_c[n]) + bias[n] = LN(x) . W^T + b with
+   * (mean_m, rstd_m) from the producer's partials (eps ln_eps), before the activation / GEGLU. */
+  float* ln_out;
+  const float* ln_in;
+  const float* ln_c;
+  float ln_eps;
 } fd_gemm_params;
 
 int fd_gemm(const fd_gemm_params* p, void* stream);
