@@ -656,7 +656,7 @@ int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
 // the 4-wave kernel sums each K step's two halves in separate waves, these kernels in one accumulator,
 // and any tile shape of the same kernel family gives the same k order.
 static int plan8(const fd_gemm_params* p, Plan8* pl) {
-  static int enabled = -1, force_s = 0, force_gm = 0, r4 = 1, pair128 = 0, r4_ns = 3, b4 = 0;
+  static int enabled = -1, force_s = 0, force_gm = 0, r4 = 1, pair128 = 0, r4_ns = 3, b4 = 0, w160 = 1;
   if (enabled < 0) {
     enabled = env_i("FD_GEMM8", 1);
     force_s = env_i("FD_GEMM8_S", 0);
@@ -667,6 +667,7 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     pair128 = env_i("FD_GEMM_P128", 0);
     r4_ns = env_i("FD_GEMM_R4_NS", 3);
     b4 = env_i("FD_GEMM_B4", 0);
+    w160 = env_i("FD_GEMM8_W160", 1);
   }
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if (!enabled || p->batch > 1 || p->K < 128) return 0;
@@ -679,6 +680,16 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
   q.waves_m = 4;
   q.ns = 3;
   q.S = (m_ref >= 256 && p->N >= 128) ? (force_s > 0 ? force_s : choose_split(m_ref, p->N, p->K, q.bn)) : 0;
+  if (q.S == 1 && w160 && p->act == FD_ACT_GEGLU && p->N % 160 == 0 && !p->conv) {
+    // 256 x 160 tiles (8 waves of 32 x 160) when they need fewer rounds of 256 CUs: the GEGLU projections
+    // (2048 x 10240: 640 -> 512 tiles, 3 -> 2 rounds; 8192 x 5120: 5 -> 4)
+    const long long tm = (m_ref + 255) / 256;
+    const long long r128 = (tm * (p->N / 128) + 255) / 256, r160 = (tm * (p->N / 160) + 255) / 256;
+    if (r160 < r128) {
+      q.bn = 160;
+      q.waves_m = 8;
+    }
+  }
   if (q.S <= 0) {
     const long long tiles_ref = (long long)((m_ref + 63) / 64) * ((p->N + 159) / 160);
     const long long tiles128 = (long long)((m_ref + 127) / 128) * ((p->N + 159) / 160);
@@ -753,7 +764,9 @@ extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream) {
   int rc;
 #define FD_G8(BM_, BN_, NW_, WM_, NS_) \
   FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, rc = (launch8<T, TO, BM_, BN_, NW_, WM_, NS_>(p, pl, s))))
-  if (pl.bm == 256) {
+  if (pl.bm == 256 && pl.bn == 160) {
+    FD_G8(256, 160, 8, 8, 3);
+  } else if (pl.bm == 256) {
     FD_G8(256, 128, 8, 4, 3);
   } else if (pl.bm == 128) {
     FD_G8(128, 160, 4, 2, 3);
