@@ -424,7 +424,9 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   float* ep = (float*)smem;
   constexpr int VPR = BNO / 8;
   // row-phase iterations whose loads are issued together
-  constexpr int ITER = (EROWS * VPR) % (NTHR * 4) == 0 ? 4 : (EROWS * VPR) % (NTHR * 5) == 0 ? 5 : 1;
+  // (1 for the 256 x 160 plain / conv tiles: five batched iterations push them past 256 VGPRs)
+  constexpr int ITER = (BN == 160 && BM == 256 && !GEGLU) ? 1
+                       : (EROWS * VPR) % (NTHR * 4) == 0 ? 4 : (EROWS * VPR) % (NTHR * 5) == 0 ? 5 : 1;
   static_assert(EROWS * VPR % (NTHR * ITER) == 0, "epilogue iterations");
   float gbh[GEGLU ? NT / 2 : 1], gbg[GEGLU ? NT / 2 : 1];
   if (GEGLU) {
@@ -667,7 +669,7 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     pair128 = env_i("FD_GEMM_P128", 0);
     r4_ns = env_i("FD_GEMM_R4_NS", 3);
     b4 = env_i("FD_GEMM_B4", 0);
-    w160 = env_i("FD_GEMM8_W160", 1);
+    w160 = env_i("FD_GEMM8_W160", 3);  // bit 0: 256 x 160 tiles where faster; bit 1: also take N = 320 from the 4-wave kernel
   }
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if (!enabled || p->batch > 1 || p->K < 128) return 0;
@@ -680,14 +682,21 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
   q.waves_m = 4;
   q.ns = 3;
   q.S = (m_ref >= 256 && p->N >= 128) ? (force_s > 0 ? force_s : choose_split(m_ref, p->N, p->K, q.bn)) : 0;
-  if (q.S == 1 && w160 && p->act == FD_ACT_GEGLU && p->N % 160 == 0 && !p->conv) {
-    // 256 x 160 tiles (8 waves of 32 x 160) when they need fewer rounds of 256 CUs: the GEGLU projections
-    // (2048 x 10240: 640 -> 512 tiles, 3 -> 2 rounds; 8192 x 5120: 5 -> 4)
+  if (w160 && m_ref >= 256 && p->N % 160 == 0 && force_s <= 0) {
+    // 256 x 160 tiles (8 waves of 32 x 160) when they finish in less time on 256 CUs: time ~ rounds x
+    // (columns per workgroup) / S.  2048 x 10240 GEGLU: 640 -> 512 tiles (3 -> 2 rounds); 8192 x 1280 conv:
+    // 320 -> 256 tiles; 8192 x 640 long-K conv: 160 tiles S = 1 -> 128 tiles S = 2; N = 320 at 128^2.
     const long long tm = (m_ref + 255) / 256;
-    const long long r128 = (tm * (p->N / 128) + 255) / 256, r160 = (tm * (p->N / 160) + 255) / 256;
-    if (r160 < r128) {
-      q.bn = 160;
-      q.waves_m = 8;
+    const int s160 = choose_split(m_ref, p->N, p->K, 160);
+    if (s160 > 0) {
+      const double t160 = (double)((tm * (p->N / 160) * s160 + 255) / 256) * 160.0 / s160;
+      const double t128 = q.S > 0 ? (double)((tm * ((p->N + 127) / 128) * q.S + 255) / 256) * 128.0 / q.S : 1e30;
+      const bool narrow = q.S <= 0 && !(w160 & 2);  // the 4-wave kernel holds N = 320 unless FD_GEMM8_W160 & 2
+      if (!narrow && t160 < 0.9 * t128) {
+        q.bn = 160;
+        q.waves_m = 8;
+        q.S = s160;
+      }
     }
   }
   if (q.S <= 0) {

@@ -90,3 +90,26 @@ def test_conv_split_and_batching():
     xr = x[:nimg * H * W].float().reshape(nimg, H, W, Cin).permute(0, 3, 1, 2)
     ref = F.conv2d(xr, wt.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, Cout)
     assert rel_l2(one, ref) < 6e-3
+
+
+@pytest.mark.parametrize("H,W,Cin,Cout,up", [(32, 32, 1280, 1280, True),    # 8192 x 1280 upsample conv: 256 x 160
+                                             (64, 64, 1920, 640, False),    # 8192 x 640, K = 17280: 160 wide, S = 2
+                                             (64, 64, 320, 320, False)])    # N = 320 (W160 & 2 only)
+def test_conv_160_wide_tiles(H, W, Cin, Cout, up):
+    """256 x 160 tiles (gemm8 planner, FD_GEMM8_W160): conv vs fp32, tile batching bitwise."""
+    from fdhip import ops
+    nimg = 2
+    x = rnd(2 * nimg * H * W, Cin)
+    wt = (torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)).to(torch.bfloat16)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    wp = ops.pack_conv3x3(wt)
+    with ops.tile_groups(2):
+        big = ops.conv3x3(x, wp, b, 2 * nimg, H, W, upsample=up)
+    one = ops.conv3x3(x[:nimg * H * W], wp, b, nimg, H, W, upsample=up)
+    Ho = 2 * H if up else H
+    assert torch.equal(big[:nimg * Ho * Ho], one)
+    xr = x[:nimg * H * W].float().reshape(nimg, H, W, Cin).permute(0, 3, 1, 2)
+    if up:
+        xr = F.interpolate(xr, scale_factor=2, mode="nearest")
+    ref = F.conv2d(xr, wt.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, Cout)
+    assert rel_l2(one, ref) < 6e-3, rel_l2(one, ref)
