@@ -297,6 +297,13 @@ class HipUNet:
         ops.unary(emb, semb, "silu")
         return ops.gemm(semb, self.temb_w, bias=self.temb_b, out_dtype=torch.float32)  # [B, sum C_out]
 
+    def _side_stream(self):
+        if os.environ.get("FD_SIDE_STREAM", "0") == "0":
+            return None
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
     def forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True):
         """x: NHWC [B*H*W, 4] (dtype); t: fp32 [B]; time_ids fp32 [B, 6]; text_embeds fp32 [B, 1280];
         cond: NHWC [B*H*W, 512] image latents (dtype) or None.  Returns eps NHWC [B*H*W, 4] (dtype)."""
@@ -306,8 +313,23 @@ class HipUNet:
             return self._forward(x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample)
 
     def _forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample):
-        temb = self.embeddings(t, time_ids, text_embeds, B)
-        self._kv = ops.gemm(self.ctx, self.kv_w)  # [ncfg*77, sum 2C]: every attn2 K/V of this forward
+        # The time / add embeddings (six M = 2 launches) and the attn2 K/V projection of the prompt for all 70
+        # blocks depend on nothing the input path computes: they run on a second stream beside conv_in and
+        # the FaithDiff extras (a fork / join inside the captured graph).  Neither uses split-K, so the two
+        # streams never share the GEMM workspace.  Opt-in (FD_SIDE_STREAM=1): measured 0.39 ms/step SLOWER at
+        # C2 -- the K/V GEMM's 2600 workgroups compete with the extras' full-chip convs.
+        cur = torch.cuda.current_stream(self.device)
+        side = self._side_stream()
+        if side is not None:
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                temb = self.embeddings(t, time_ids, text_embeds, B)
+                self._kv = ops.gemm(self.ctx, self.kv_w)
+            temb.record_stream(cur)
+            self._kv.record_stream(cur)
+        else:
+            temb = self.embeddings(t, time_ids, text_embeds, B)
+            self._kv = ops.gemm(self.ctx, self.kv_w)  # [ncfg*77, sum 2C]: every attn2 K/V of this forward
         x0 = ops.conv_direct(x, *self.conv_in, B, H, Wd, 4, 3, 1, 1, out_dtype=self.dtype)
         if cond is not None and self.has_extras:
             feat = self._extras(x0, cond, B, H, Wd)
@@ -315,6 +337,8 @@ class HipUNet:
                 x0 = ops.gemm(feat, self.scp[0], bias=self.scp[1], residual=x0)
             else:
                 x0 = ops.gemm(feat, self.scp[0], bias=self.scp[1])
+        if side is not None:
+            cur.wait_stream(side)
         skips = [(x0, 320, H, Wd)]
         h, hh, ww = x0, H, Wd
         for i, blk in enumerate(self.down):
