@@ -95,6 +95,24 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   int tm, tn;
   tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, swz, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
+  // residual prefetch (64 x 160 tiles, one workgroup per CU for the M = 2048 projections): the epilogue's
+  // residual rows are requested before the first operand stage, so no memory round trip is left between
+  // the last MFMA and the stores
+  constexpr bool PREF = (BM == 64 && BN == 160 && !GEGLU);
+  constexpr int PF_VPR = BN / 8, PF_TOT = BM * PF_VPR, PF_ITER = (PF_TOT + 256 * KS - 1) / (256 * KS);
+  typedef __attribute__((ext_vector_type(8))) TO TO8P;
+  TO8P res_pf[PREF ? PF_ITER : 1];
+  const bool pf = PREF && p.residual && (p.ldr % 8 == 0) && ((((unsigned long long)p.residual) & 15) == 0) &&
+                  m0 + BM <= p.M && n0 + BN <= p.N;
+  if (PREF && pf) {
+    const TO* Rp = (const TO*)p.residual + (long long)blockIdx.z * p.strideR;
+#pragma unroll
+    for (int it = 0; it < (PREF ? PF_ITER : 1); ++it) {
+      const int e = threadIdx.x + it * 256 * KS;
+      if (PF_TOT % (256 * KS) == 0 || e < PF_TOT)
+        res_pf[it] = *(const TO8P*)(Rp + (long long)(m0 + e / PF_VPR) * p.ldr + n0 + (e % PF_VPR) * 8);
+    }
+  }
   // LN-fold consumer: the producer's (sum, sumsq) partials of this tile's rows and ln_c of its columns,
   // requested before the first operand stage so their latency is hidden by the K loop (unconditional
   // 16-B loads, index clamped, lnP even: a conditional load per partial gets sunk into the fold's
@@ -373,7 +391,10 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
           *(f32x4*)&rv[it][0] = *(const f32x4*)rb;
           *(f32x4*)&rv[it][4] = *(const f32x4*)(rb + 4);
         }
-        if (R) res[it] = *(const TO8*)(R + (long long)m * p.ldr + n);
+        if (R) {
+          if (PREF && pf) res[it] = __builtin_bit_cast(TO8, res_pf[PREF ? it : 0]);
+          else res[it] = *(const TO8*)(R + (long long)m * p.ldr + n);
+        }
       }
     }
 #pragma unroll
