@@ -1,0 +1,182 @@
+// OCP e4m3 GEMM on the gfx950 block-scaled MFMA (v_mfma_scale_f32_16x16x128_f8f6f4) -- the fp8 leg of
+// the reference's quantize_8bit (utils/system.py:13-32) stores every UNet weight
+// as unscaled float8_e4m3fn; here those bytes ARE the B operand (no widening), and the activations are
+// quantized per row to e4m3 with an fp32 scale (fd_quant_rows_e4m3), so both operands run on the fp8
+// matrix pipe at 2x the bf16 rate with half the operand bytes.
+//
+//   C[m][n] = out( a_scale[m] * w_scale * sum_k A8[m][k] * W8[n][k] + bias[n] + residual[m][n] )
+//
+// Tiles: 128x128 per 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA 16x16 tiles), K-step 128 bytes.
+// Operands go global -> registers (next K-step prefetched while the MFMAs run) -> LDS (144-B row pitch:
+// the 16 rows one ds_read_b128 phase touches land on 16 disjoint 4-bank groups) -> fragments.
+// MFMA operand map (16x16x128, 8-bit): lane l holds row (l & 15), k = 32*(l >> 4) + j, j = 0..31,
+// i.e. 32 contiguous bytes of one row; C/D: col = l & 15, row = 4*(l >> 4) + r.
+#include "fd_common.h"
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(2))) int i32x2;
+
+namespace {
+constexpr int F8_BM = 128, F8_BN = 128, F8_BK = 128;
+constexpr int F8_PITCH = F8_BK + 16;
+constexpr int F8_NT = 256;
+
+__device__ __forceinline__ f32x4 mfma_e4m3(const i32x8& a, const i32x8& b, f32x4 c) {
+  // cbsz = blgp = 0 -> both operands e4m3; E8M0 block scales 127 = 2^0 (per-row scaling happens in the epilogue)
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+// 128 rows x 128 bytes of a row-major [rows][ld] e4m3 matrix -> 4 x 16 B per thread, zero outside.
+__device__ __forceinline__ void f8_load_tile(const uint8_t* __restrict__ base, long long ld, int r0, int rows,
+                                             int k0, int K, u32x4 (&r)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = threadIdx.x + i * F8_NT;
+    const int row = c >> 3, kc = k0 + (c & 7) * 16;
+    if (r0 + row < rows && kc < K)
+      r[i] = *(const u32x4*)(base + (long long)(r0 + row) * ld + kc);
+    else
+      r[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
+__device__ __forceinline__ void f8_store_tile(uint8_t* lds, const u32x4 (&r)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = threadIdx.x + i * F8_NT;
+    *(u32x4*)(lds + (c >> 3) * F8_PITCH + (c & 7) * 16) = r[i];
+  }
+}
+
+__device__ __forceinline__ i32x8 f8_frag(const uint8_t* lds, int row, int lane) {
+  const uint8_t* p = lds + row * F8_PITCH + (lane >> 4) * 32;
+  const u32x4 lo = *(const u32x4*)p, hi = *(const u32x4*)(p + 16);
+  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+template <typename TO>
+__global__ __launch_bounds__(F8_NT) void gemm_e4m3_kernel(const uint8_t* __restrict__ A, long long lda,
+                                                           const float* __restrict__ a_scale,
+                                                           const uint8_t* __restrict__ W, long long ldw,
+                                                           float w_scale, TO* __restrict__ C, long long ldc, int M,
+                                                           int N, int K, const float* __restrict__ bias,
+                                                           const TO* __restrict__ R, long long ldr) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_a[F8_BM * F8_PITCH];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_b[F8_BN * F8_PITCH];
+  const int tn = (N + F8_BN - 1) / F8_BN, tm = (M + F8_BM - 1) / F8_BM;
+  const int b = xcd_remap(blockIdx.x, tn * tm);  // neighbouring tiles (same A row panel) share one XCD's L2
+  const int m0 = (b / tn) * F8_BM, n0 = (b % tn) * F8_BN;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[4], rb[4];
+  const int nk = (K + F8_BK - 1) / F8_BK;
+  f8_load_tile(A, lda, m0, M, 0, K, ra);
+  f8_load_tile(W, ldw, n0, N, 0, K, rb);
+  for (int kt = 0; kt < nk; ++kt) {
+    __syncthreads();  // every wave finished reading the previous K-step's fragments
+    f8_store_tile(lds_a, ra);
+    f8_store_tile(lds_b, rb);
+    __syncthreads();
+    if (kt + 1 < nk) {  // next K-step's operands in flight under this step's MFMAs
+      f8_load_tile(A, lda, m0, M, (kt + 1) * F8_BK, K, ra);
+      f8_load_tile(W, ldw, n0, N, (kt + 1) * F8_BK, K, rb);
+    }
+    i32x8 fa[4], fb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = f8_frag(lds_a, wm + i * 16 + (lane & 15), lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = f8_frag(lds_b, wn + j * 16 + (lane & 15), lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma_e4m3(fa[i], fb[j], acc[i][j]);
+  }
+
+  // epilogue: per-row activation scale x weight scale, bias, residual; 16 lanes store 16 adjacent columns
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+      if (m >= M) continue;
+      const float s = a_scale[m] * w_scale;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn + j * 16 + (lane & 15);
+        if (n >= N) continue;
+        float v = acc[i][j][r] * s;
+        if (bias) v += bias[n];
+        if (R) v += (float)R[(long long)m * ldr + n];
+        C[(long long)m * ldc + n] = (TO)v;
+      }
+    }
+  }
+}
+
+// One workgroup per row: amax over the row, q = RNE_e4m3(x * 448 / amax), scale = amax / 448.
+template <typename T>
+__global__ __launch_bounds__(256) void quant_rows_e4m3_kernel(const T* __restrict__ x, long long ldx,
+                                                              uint8_t* __restrict__ q, long long ldq,
+                                                              float* __restrict__ scale, int K) {
+  typedef typename VecT<T>::v8 V8;
+  __shared__ float red[4];
+  const long long row = blockIdx.x;
+  const T* xr = x + row * ldx;
+  float amax = 0.f;
+  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+    const V8 v = *(const V8*)(xr + k);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf((float)v[j]));
+  }
+  amax = wave_max(amax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  // correctly rounded divisions (hipcc's default f32 '/' is not), so the scale is exactly amax / 448 in fp32
+  const float inv = amax > 0.f ? __fdiv_rn(448.0f, amax) : 0.f;
+  if (threadIdx.x == 0) scale[row] = __fdiv_rn(amax, 448.0f);
+  uint8_t* qr = q + row * ldq;
+  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+    const V8 v = *(const V8*)(xr + k);
+    int lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[0] * inv, (float)v[1] * inv, 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[2] * inv, (float)v[3] * inv, lo, true);
+    int hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[4] * inv, (float)v[5] * inv, 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[6] * inv, (float)v[7] * inv, hi, true);
+    *(i32x2*)(qr + k) = i32x2{lo, hi};
+  }
+}
+}  // namespace
+
+extern "C" int fd_quant_rows_e4m3(const void* x, long long ldx, void* q, long long ldq, float* scale, int M, int K,
+                                  int dtype, void* stream) {
+  if (!x || !q || !scale) return FD_ERR_ARG;
+  if (M <= 0 || K <= 0 || (K % 16) || (ldx % 8) || (ldq % 16) || ldx < K || ldq < K) return FD_ERR_SHAPE;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(quant_rows_e4m3_kernel<T>, dim3(M), dim3(256), 0, (hipStream_t)stream,
+                                          (const T*)x, ldx, (uint8_t*)q, ldq, scale, K));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, const void* W, long long ldw,
+                            float w_scale, void* C, long long ldc, int M, int N, int K, const float* bias,
+                            const void* residual, long long ldr, int out_dtype, void* stream) {
+  if (!A || !a_scale || !W || !C) return FD_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || (K % 16) || (lda % 16) || (ldw % 16) || lda < K || ldw < K || ldc < N)
+    return FD_ERR_SHAPE;
+  if (residual && ldr < N) return FD_ERR_SHAPE;
+  if (residual && out_dtype == FD_F32) return FD_ERR_DTYPE;
+  const int tiles = ((M + F8_BM - 1) / F8_BM) * ((N + F8_BN - 1) / F8_BN);
+  FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL(gemm_e4m3_kernel<TO>, dim3(tiles), dim3(F8_NT), 0,
+                                              (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
+                                              (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias,
+                                              (const TO*)residual, ldr));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}

@@ -168,6 +168,47 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
     return out
 
 
+def pack_e4m3(w):
+    """Weights -> OCP e4m3 bytes [N][K] (uint8) exactly as utils/system.py:20 (``.to(torch.float8_e4m3fn)``:
+    unscaled, RNE, no saturation), for gemm_e4m3(w_scale=1)."""
+    return w.to(torch.float8_e4m3fn).view(torch.uint8).contiguous()
+
+
+def quant_rows_e4m3(x, q=None, scale=None, M=None, K=None, ldx=None):
+    """x [M, K] bf16/f16 -> (q uint8 [M, K] e4m3, scale fp32 [M]) with x ~= q * scale per row."""
+    K = x.shape[-1] if K is None else K
+    M = x.numel() // x.shape[-1] if M is None else M
+    ldx = x.stride(-2) if ldx is None else ldx
+    if q is None:
+        q = torch.empty((M, K), dtype=torch.uint8, device=x.device)
+    if scale is None:
+        scale = torch.empty((M,), dtype=torch.float32, device=x.device)
+    L.check(L.load().fd_quant_rows_e4m3(L.ptr(x), ldx, L.ptr(q), q.stride(0), L.ptr(scale), M, K,
+                                        L.dtype_code(x.dtype), L.stream()), "fd_quant_rows_e4m3")
+    return q, scale
+
+
+def gemm_e4m3(a8, a_scale, w8, out=None, bias=None, residual=None, w_scale=1.0, out_dtype=torch.bfloat16):
+    """out[M, N] = a_scale[m] * w_scale * (a8[M, K] @ w8[N, K]^T) + bias + residual on the fp8 MFMA."""
+    M, K = a8.shape
+    N = w8.shape[0]
+    if w8.shape[1] != K:
+        raise ValueError(f"gemm_e4m3: K mismatch {a8.shape} x {w8.shape}")
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=a8.device)
+    rc = L.load().fd_gemm_e4m3(L.ptr(a8), a8.stride(0), L.ptr(a_scale), L.ptr(w8), w8.stride(0), w_scale, L.ptr(out),
+                               out.stride(0), M, N, K, L.ptr(bias), L.ptr(residual),
+                               0 if residual is None else residual.stride(0), L.dtype_code(out.dtype), L.stream())
+    L.check(rc, "fd_gemm_e4m3")
+    return out
+
+
+def linear_e4m3(x, w8, bias=None, residual=None):
+    """nn.Linear of a quantize_8bit UNet on the fp8 MFMA: per-row e4m3 activations x e4m3 weight bytes."""
+    q, s = quant_rows_e4m3(x)
+    return gemm_e4m3(q, s, w8, bias=bias, residual=residual, out_dtype=x.dtype)
+
+
 def fold_layer_norm(w, gamma, beta, bias=None, dtype=torch.bfloat16):
     """LayerNorm(x; gamma, beta) @ w^T + bias == rstd * (x @ w'^T - mean * c) + d  with
     w' = w * gamma (per input column, rounded to the GEMM dtype), c = rowsum(w') of the rounded values and

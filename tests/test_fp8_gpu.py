@@ -1,0 +1,119 @@
+"""fp8 (OCP e4m3) leg of SURVEY §8 a18 / config C4: fd_quant_rows_e4m3 + fd_gemm_e4m3 on the block-scaled MFMA.
+
+Bars (stated per test):
+  * operand map / tails: exact integer data (representable in e4m3) -> bit-exact fp32 result;
+  * quantization: bytes and scales bit-exact vs torch's own float8_e4m3fn cast of x * 448/amax (RNE);
+  * GEMM on quantized operands vs fp32 matmul of the SAME dequantized operands: rel-L2 <= 1e-5 (fp32 out);
+  * against the unquantized bf16-activation product (the reference computes fp16 activations x widened e4m3
+    weights, pipeline:1349): rel-L2 <= 4e-2 -- the cost of e4m3 activations (3 mantissa bits), stated here.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _dev():
+    from fdhip import lib
+    lib.require_device()
+
+
+def rel_l2(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def e4m3(x):
+    return x.to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+def widen(q):
+    return q.view(torch.float8_e4m3fn).float()
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (200, 72, 320), (77, 1280, 2048), (16, 16, 16),
+                                   (2048, 1280, 1280), (333, 640, 5120)])
+def test_gemm_e4m3_exact_integers(M, N, K):
+    """Asymmetric small-integer operands: every product and partial sum is exact in fp32, so any error in
+    the 16x16x128 lane map, the K / M / N tails or the epilogue shows as a mismatch."""
+    from fdhip import ops
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    a = torch.randint(-6, 7, (M, K), generator=g).float()
+    w = torch.randint(-4, 5, (N, K), generator=g).float() * 0.5
+    a8, w8 = e4m3(a).to(DEV), e4m3(w).to(DEV)
+    ones = torch.ones(M, device=DEV)
+    got = ops.gemm_e4m3(a8, ones, w8, out_dtype=torch.float32).cpu()
+    want = a.double() @ w.double().T
+    assert torch.equal(got.double(), want)
+
+
+def test_gemm_e4m3_scales_bias_residual():
+    from fdhip import ops
+    M, N, K = 300, 200, 640
+    g = torch.Generator().manual_seed(5)
+    a = torch.randint(-6, 7, (M, K), generator=g).float()
+    w = torch.randint(-4, 5, (N, K), generator=g).float()
+    sa = torch.rand(M, generator=g) + 0.5
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g).to(torch.bfloat16)
+    got = ops.gemm_e4m3(e4m3(a).to(DEV), sa.to(DEV), e4m3(w).to(DEV), bias=bias.to(DEV), residual=res.to(DEV),
+                        w_scale=0.25, out_dtype=torch.bfloat16).cpu()
+    want = (a.double() @ w.double().T) * sa.double()[:, None] * 0.25 + bias.double() + res.double()
+    assert rel_l2(got, want) < 4e-3  # one bf16 rounding on store
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,K", [(1, 16), (77, 2048), (2048, 1280), (513, 5120)])
+def test_quant_rows_e4m3_bitexact(dtype, M, K):
+    from fdhip import ops
+    x = (torch.randn(M, K, device=DEV) * torch.logspace(-3, 2, M, device=DEV)[:, None]).to(dtype)
+    x[0, : min(K, 8)] = 0  # zeros and a partly-zero row
+    q, s = ops.quant_rows_e4m3(x)
+    # correctly rounded fp32 divisions, computed on the host (torch's device division by a scalar multiplies
+    # by the reciprocal, which is not what the kernel defines)
+    xc = x.float().cpu()
+    amax = xc.abs().amax(1).double()
+    inv = torch.where(amax > 0, 448.0 / amax, torch.zeros_like(amax)).float()
+    want_q = e4m3(xc * inv[:, None])
+    assert torch.equal(s.cpu(), (amax / 448.0).float())
+    assert torch.equal(q.cpu(), want_q)
+
+
+def test_quant_rows_zero_row():
+    from fdhip import ops
+    x = torch.zeros(3, 64, dtype=torch.bfloat16, device=DEV)
+    q, s = ops.quant_rows_e4m3(x)
+    assert torch.all(q == 0) and torch.all(s == 0)
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 1280, 1280), (8192, 640, 640), (2048, 5120, 1280), (2048, 1280, 5120),
+                                   (77, 1280, 2048)])
+def test_linear_e4m3_vs_dequantized_and_unquantized(M, N, K):
+    from fdhip import arch, ops
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV) * K ** -0.5
+    b = torch.randn(N, device=DEV) * 0.1
+    w8 = ops.pack_e4m3(w)
+    # the weights are the reference's quantize_8bit values (arch.quantize_e4m3), unscaled
+    assert torch.equal(widen(w8), arch.quantize_e4m3({"w": w})["w"])
+    q, s = ops.quant_rows_e4m3(x)
+    got32 = ops.gemm_e4m3(q, s, w8, bias=b, out_dtype=torch.float32)
+    deq = widen(q).double() * s.double()[:, None]
+    want_deq = deq @ widen(w8).double().T + b.double()
+    assert rel_l2(got32, want_deq) < 1e-5
+    got = ops.linear_e4m3(x, w8, bias=b)
+    assert got.dtype == torch.bfloat16
+    want_ref = x.double() @ widen(w8).double().T + b.double()  # fp16/bf16 activations x widened e4m3 weights
+    assert rel_l2(got, want_ref) < 4e-2
+
+
+def test_gemm_e4m3_rejects_bad_shapes():
+    from fdhip import ops
+    a8 = torch.zeros(64, 24, dtype=torch.uint8, device=DEV)  # K % 16 != 0
+    with pytest.raises(RuntimeError):
+        ops.gemm_e4m3(a8, torch.ones(64, device=DEV), torch.zeros(32, 24, dtype=torch.uint8, device=DEV))
+    with pytest.raises(ValueError):
+        ops.gemm_e4m3(torch.zeros(64, 32, dtype=torch.uint8, device=DEV), torch.ones(64, device=DEV),
+                      torch.zeros(32, 48, dtype=torch.uint8, device=DEV))
