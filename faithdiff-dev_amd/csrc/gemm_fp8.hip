@@ -6,8 +6,9 @@
 //
 //   C[m][n] = out( a_scale[m] * w_scale * sum_k A8[m][k] * W8[n][k] + bias[n] + residual[m][n] )
 //
-// Tiles: 128x128 per 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA 16x16 tiles), K-step 128 bytes.
-// Operands go global -> registers (next K-step prefetched while the MFMAs run) -> LDS (144-B row pitch:
+// Tiles: 128x128 (or 64x128 when 128-row tiles cannot fill 256 CUs) per 256-thread workgroup, 2x2 waves,
+// K-step 128 bytes.  Operands go global -> registers (next K-step prefetched while the MFMAs run) -> double-
+// buffered LDS (144-B row pitch:
 // the 16 rows one ds_read_b128 phase touches land on 16 disjoint 4-bank groups) -> fragments.
 // MFMA operand map (16x16x128, 8-bit): lane l holds row (l & 15), k = 32*(l >> 4) + j, j = 0..31,
 // i.e. 32 contiguous bytes of one row; C/D: col = l & 15, row = 4*(l >> 4) + r.
@@ -17,7 +18,7 @@ typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(2))) int i32x2;
 
 namespace {
-constexpr int F8_BM = 128, F8_BN = 128, F8_BK = 128;
+constexpr int F8_BN = 128, F8_BK = 128;
 constexpr int F8_PITCH = F8_BK + 16;
 constexpr int F8_NT = 256;
 
@@ -26,11 +27,12 @@ __device__ __forceinline__ f32x4 mfma_e4m3(const i32x8& a, const i32x8& b, f32x4
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
 
-// 128 rows x 128 bytes of a row-major [rows][ld] e4m3 matrix -> 4 x 16 B per thread, zero outside.
+// ROWS x 128 bytes of a row-major [rows][ld] e4m3 matrix -> ROWS/32 x 16 B per thread, zero outside.
+template <int ROWS>
 __device__ __forceinline__ void f8_load_tile(const uint8_t* __restrict__ base, long long ld, int r0, int rows,
-                                             int k0, int K, u32x4 (&r)[4]) {
+                                             int k0, int K, u32x4 (&r)[ROWS / 32]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < ROWS / 32; ++i) {
     const int c = threadIdx.x + i * F8_NT;
     const int row = c >> 3, kc = k0 + (c & 7) * 16;
     if (r0 + row < rows && kc < K)
@@ -40,9 +42,10 @@ __device__ __forceinline__ void f8_load_tile(const uint8_t* __restrict__ base, l
   }
 }
 
-__device__ __forceinline__ void f8_store_tile(uint8_t* lds, const u32x4 (&r)[4]) {
+template <int ROWS>
+__device__ __forceinline__ void f8_store_tile(uint8_t* lds, const u32x4 (&r)[ROWS / 32]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < ROWS / 32; ++i) {
     const int c = threadIdx.x + i * F8_NT;
     *(u32x4*)(lds + (c >> 3) * F8_PITCH + (c & 7) * 16) = r[i];
   }
@@ -54,54 +57,64 @@ __device__ __forceinline__ i32x8 f8_frag(const uint8_t* lds, int row, int lane) 
   return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
 }
 
-template <typename TO>
+// BM x 128 tile per workgroup: 2x2 waves of (BM/2) x 64.  LDS is double-buffered: K-step kt+1's operands
+// are loaded to registers before kt's MFMAs and written to the other buffer after them, so one barrier per
+// K-step orders both the reads of buffer kt and the writes of buffer kt+1.
+template <typename TO, int BM>
 __global__ __launch_bounds__(F8_NT) void gemm_e4m3_kernel(const uint8_t* __restrict__ A, long long lda,
                                                            const float* __restrict__ a_scale,
                                                            const uint8_t* __restrict__ W, long long ldw,
                                                            float w_scale, TO* __restrict__ C, long long ldc, int M,
                                                            int N, int K, const float* __restrict__ bias,
                                                            const TO* __restrict__ R, long long ldr) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds_a[F8_BM * F8_PITCH];
-  __shared__ __attribute__((aligned(16))) uint8_t lds_b[F8_BN * F8_PITCH];
-  const int tn = (N + F8_BN - 1) / F8_BN, tm = (M + F8_BM - 1) / F8_BM;
+  constexpr int MI = BM / 32;  // 16-row MFMA tiles per wave
+  __shared__ __attribute__((aligned(16))) uint8_t lds_a[2][BM * F8_PITCH];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_b[2][F8_BN * F8_PITCH];
+  const int tn = (N + F8_BN - 1) / F8_BN, tm = (M + BM - 1) / BM;
   const int b = xcd_remap(blockIdx.x, tn * tm);  // neighbouring tiles (same A row panel) share one XCD's L2
-  const int m0 = (b / tn) * F8_BM, n0 = (b % tn) * F8_BN;
+  const int m0 = (b / tn) * BM, n0 = (b % tn) * F8_BN;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+  const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * 64;
 
-  f32x4 acc[4][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra[4], rb[4];
+  u32x4 ra[BM / 32], rb[F8_BN / 32];
   const int nk = (K + F8_BK - 1) / F8_BK;
-  f8_load_tile(A, lda, m0, M, 0, K, ra);
-  f8_load_tile(W, ldw, n0, N, 0, K, rb);
+  f8_load_tile<BM>(A, lda, m0, M, 0, K, ra);
+  f8_load_tile<F8_BN>(W, ldw, n0, N, 0, K, rb);
+  f8_store_tile<BM>(lds_a[0], ra);
+  f8_store_tile<F8_BN>(lds_b[0], rb);
+  __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    __syncthreads();  // every wave finished reading the previous K-step's fragments
-    f8_store_tile(lds_a, ra);
-    f8_store_tile(lds_b, rb);
-    __syncthreads();
-    if (kt + 1 < nk) {  // next K-step's operands in flight under this step's MFMAs
-      f8_load_tile(A, lda, m0, M, (kt + 1) * F8_BK, K, ra);
-      f8_load_tile(W, ldw, n0, N, (kt + 1) * F8_BK, K, rb);
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {  // next K-step's operands in flight under this step's MFMAs
+      f8_load_tile<BM>(A, lda, m0, M, (kt + 1) * F8_BK, K, ra);
+      f8_load_tile<F8_BN>(W, ldw, n0, N, (kt + 1) * F8_BK, K, rb);
     }
-    i32x8 fa[4], fb[4];
+    i32x8 fa[MI], fb[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = f8_frag(lds_a, wm + i * 16 + (lane & 15), lane);
+    for (int i = 0; i < MI; ++i) fa[i] = f8_frag(lds_a[cur], wm + i * 16 + (lane & 15), lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = f8_frag(lds_b, wn + j * 16 + (lane & 15), lane);
+    for (int j = 0; j < 4; ++j) fb[j] = f8_frag(lds_b[cur], wn + j * 16 + (lane & 15), lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma_e4m3(fa[i], fb[j], acc[i][j]);
+    if (more) {
+      f8_store_tile<BM>(lds_a[cur ^ 1], ra);
+      f8_store_tile<F8_BN>(lds_b[cur ^ 1], rb);
+    }
+    __syncthreads();
   }
 
   // epilogue: per-row activation scale x weight scale, bias, residual; 16 lanes store 16 adjacent columns
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < MI; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
@@ -172,11 +185,15 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
     return FD_ERR_SHAPE;
   if (residual && ldr < N) return FD_ERR_SHAPE;
   if (residual && out_dtype == FD_F32) return FD_ERR_DTYPE;
-  const int tiles = ((M + F8_BM - 1) / F8_BM) * ((N + F8_BN - 1) / F8_BN);
-  FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL(gemm_e4m3_kernel<TO>, dim3(tiles), dim3(F8_NT), 0,
-                                              (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
-                                              (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias,
-                                              (const TO*)residual, ldr));
+  // 64-row tiles when 128-row tiles leave CUs idle (fewer than 256 workgroups, e.g. the M = 2048 projections)
+  const int tn = (N + F8_BN - 1) / F8_BN, t128 = ((M + 127) / 128) * tn;
+  const bool small = t128 < 256;
+  const int tiles = small ? ((M + 63) / 64) * tn : t128;
+  FD_DISPATCH_O(out_dtype, {
+    auto kern = small ? gemm_e4m3_kernel<TO, 64> : gemm_e4m3_kernel<TO, 128>;
+    hipLaunchKernelGGL(kern, dim3(tiles), dim3(F8_NT), 0, (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
+                       (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr);
+  });
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

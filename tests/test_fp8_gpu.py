@@ -34,7 +34,7 @@ def widen(q):
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 128), (200, 72, 320), (77, 1280, 2048), (16, 16, 16),
-                                   (2048, 1280, 1280), (333, 640, 5120)])
+                                   (2048, 1280, 1280), (333, 640, 5120), (4100, 1030, 272), (8192, 640, 640)])
 def test_gemm_e4m3_exact_integers(M, N, K):
     """Asymmetric small-integer operands: every product and partial sum is exact in fp32, so any error in
     the 16x16x128 lane map, the K / M / N tails or the epilogue shows as a mismatch."""
