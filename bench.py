@@ -94,6 +94,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--size", type=int, default=1024, help="image side (latent = size/8)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="use_fp8 model (quantize_8bit weights; transformer Linears "
+                                                       "on the e4m3 MFMA): the C4 arithmetic on the C2 tile")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vae", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof windows)")
@@ -113,12 +115,14 @@ def setup_dist(n):
     return world, rank, local
 
 
-def build(size, seed):
+def build(size, seed, fp8=False):
     from fdhip import arch
     from fdhip.unet import HipUNet
     dev = torch.device("cuda", torch.cuda.current_device())
     sd = arch.random_init(arch.unet_param_shapes(True), seed=seed, device=dev)
-    unet = HipUNet(sd, dev, torch.bfloat16)
+    if fp8:
+        sd = arch.quantize_e4m3(sd)
+    unet = HipUNet(sd, dev, torch.bfloat16, fp8_mfma=fp8)
     del sd
     return unet
 
@@ -165,7 +169,7 @@ def main():
     h = w = args.size // 8
     k = min(128, h)
     cfg, B = 2, 2
-    unet = build(args.size, seed=0)
+    unet = build(args.size, seed=0, fp8=args.fp8)
 
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     canvas = torch.randn((4, h, w), generator=g, device=dev) * 11.0
@@ -283,7 +287,7 @@ def main():
     gemm_tf = fl_g / (ms_g / 1e3) / 1e12
     tr = load_traffic()
     traffic = None
-    if tr and tr.get("workload") == f"C2 {args.size}":
+    if tr and tr.get("workload") == f"C2 {args.size}" and not args.fp8:
         traffic = tr["hbm_bytes_per_forward"]
     n_a, fl_a, _, ms_a = kstats["flash_attn"]
     attn_tf = fl_a / (ms_a / 1e3) / 1e12
@@ -297,9 +301,10 @@ def main():
         "metric": "denoise steps/sec @1024px 20-step + VAE decode ms",
         "value": round(value, 4), "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "bf16", "data": "synthetic (seeded random-init SDXL+FaithDiff weights, random latents/conditions)",
+        "dtype": "fp8-e4m3+bf16" if args.fp8 else "bf16", "data": "synthetic (seeded random-init SDXL+FaithDiff weights, random latents/conditions)",
         "config": {"workload": f"C2: {args.size}x{args.size} single TLC tile, CFG batch 2, Euler step + blend, "
-                               f"UNet bf16 (hipGraph={graph is not None}), VAE fp16",
+                               f"UNet {'use_fp8: transformer Linears e4m3 MFMA, convs bf16' if args.fp8 else 'bf16'} "
+                               f"(hipGraph={graph is not None}), VAE fp16",
                    "model": "SDXL UNet + FaithDiff extras (2.58B params)", "global_batch": 2 * world,
                    "latent": [h, w], "parallelism": f"replicas x{world}"},
         "vae_decode_ms": None if vae_ms is None else round(vae_ms, 2),

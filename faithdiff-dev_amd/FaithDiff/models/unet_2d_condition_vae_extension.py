@@ -162,7 +162,10 @@ class UNet2DConditionModel:
             cdt = torch.bfloat16 if self._dtype in (torch.float32, torch.bfloat16, torch.float8_e4m3fn) \
                 else self._dtype
             sd = arch.quantize_e4m3(self._sd) if self._fp8 else self._sd
-            self._hip = HipUNet(sd, self._device, cdt)
+            # the quantized model's transformer Linears run on the e4m3 MFMA (FD_FP8_MFMA=0: 16-bit MFMA on the
+            # widened e4m3 values, i.e. exactly the reference's autocast arithmetic)
+            fp8_mfma = self._fp8 and os.environ.get("FD_FP8_MFMA", "1") != "0"
+            self._hip = HipUNet(sd, self._device, cdt, fp8_mfma=fp8_mfma)
         return self._hip
 
     def release_host_weights(self):

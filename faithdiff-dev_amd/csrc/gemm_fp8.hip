@@ -4,7 +4,8 @@
 // quantized per row to e4m3 with an fp32 scale (fd_quant_rows_e4m3), so both operands run on the fp8
 // matrix pipe at 2x the bf16 rate with half the operand bytes.
 //
-//   C[m][n] = out( a_scale[m] * w_scale * sum_k A8[m][k] * W8[n][k] + bias[n] + residual[m][n] )
+//   C[m][n] = out( act(a_scale[m] * w_scale * sum_k A8[m][k] * W8[n][k] + bias[n]) + residual[m][n] )
+//   (act = SiLU / GELU / QuickGELU, or GEGLU over packed [hidden | gate] row groups -> N/2 columns)
 //
 // Tiles: 128x128 (or 64x128 when 128-row tiles cannot fill 256 CUs) per 256-thread workgroup, 2x2 waves,
 // K-step 128 bytes.  Operands go global -> registers (next K-step prefetched while the MFMAs run) -> double-
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(F8_NT) void gemm_e4m3_kernel(const uint8_t* __restr
                                                            const uint8_t* __restrict__ W, long long ldw,
                                                            float w_scale, TO* __restrict__ C, long long ldc, int M,
                                                            int N, int K, const float* __restrict__ bias,
-                                                           const TO* __restrict__ R, long long ldr) {
+                                                           const TO* __restrict__ R, long long ldr, int act) {
   constexpr int MI = BM / 32;  // 16-row MFMA tiles per wave
   __shared__ __attribute__((aligned(16))) uint8_t lds_a[2][BM * F8_PITCH];
   __shared__ __attribute__((aligned(16))) uint8_t lds_b[2][F8_BN * F8_PITCH];
@@ -112,7 +113,9 @@ __global__ __launch_bounds__(F8_NT) void gemm_e4m3_kernel(const uint8_t* __restr
     __syncthreads();
   }
 
-  // epilogue: per-row activation scale x weight scale, bias, residual; 16 lanes store 16 adjacent columns
+  // epilogue: per-row activation scale x weight scale, bias, residual; 16 lanes store 16 adjacent columns.
+  // GEGLU: W rows are packed [16 hidden | 16 gate] per 32 (ops.pack_geglu), so a wave's column tiles j = 0,1
+  // and 2,3 are the hidden / gate halves of output columns ((n0 + wn) / 32 + j / 2) * 16 + (lane & 15).
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -120,12 +123,27 @@ __global__ __launch_bounds__(F8_NT) void gemm_e4m3_kernel(const uint8_t* __restr
       const int m = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
       if (m >= M) continue;
       const float s = a_scale[m] * w_scale;
+      if (act == FD_ACT_GEGLU) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const int nh = n0 + wn + g * 32 + (lane & 15);
+          if (nh >= N) continue;
+          float hv = acc[i][2 * g][r] * s, gv = acc[i][2 * g + 1][r] * s;
+          if (bias) hv += bias[nh], gv += bias[nh + 16];
+          const int o = ((n0 + wn) / 32 + g) * 16 + (lane & 15);
+          float v = hv * gelu_f(gv);
+          if (R) v += (float)R[(long long)m * ldr + o];
+          C[(long long)m * ldc + o] = (TO)v;
+        }
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = n0 + wn + j * 16 + (lane & 15);
         if (n >= N) continue;
         float v = acc[i][j][r] * s;
         if (bias) v += bias[n];
+        if (act != FD_ACT_NONE) v = act_f(v, act);
         if (R) v += (float)R[(long long)m * ldr + n];
         C[(long long)m * ldc + n] = (TO)v;
       }
@@ -179,11 +197,14 @@ extern "C" int fd_quant_rows_e4m3(const void* x, long long ldx, void* q, long lo
 
 extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, const void* W, long long ldw,
                             float w_scale, void* C, long long ldc, int M, int N, int K, const float* bias,
-                            const void* residual, long long ldr, int out_dtype, void* stream) {
+                            const void* residual, long long ldr, int act, int out_dtype, void* stream) {
   if (!A || !a_scale || !W || !C) return FD_ERR_ARG;
-  if (M <= 0 || N <= 0 || K <= 0 || (K % 16) || (lda % 16) || (ldw % 16) || lda < K || ldw < K || ldc < N)
+  if (act < FD_ACT_NONE || act > FD_ACT_GEGLU) return FD_ERR_ARG;
+  const int nout = act == FD_ACT_GEGLU ? N / 2 : N;
+  if (M <= 0 || N <= 0 || K <= 0 || (K % 16) || (lda % 16) || (ldw % 16) || lda < K || ldw < K || ldc < nout)
     return FD_ERR_SHAPE;
-  if (residual && ldr < N) return FD_ERR_SHAPE;
+  if (act == FD_ACT_GEGLU && (N % 32)) return FD_ERR_SHAPE;
+  if (residual && ldr < nout) return FD_ERR_SHAPE;
   if (residual && out_dtype == FD_F32) return FD_ERR_DTYPE;
   // 64-row tiles when 128-row tiles leave CUs idle (fewer than 256 workgroups, e.g. the M = 2048 projections)
   const int tn = (N + F8_BN - 1) / F8_BN, t128 = ((M + 127) / 128) * tn;
@@ -192,7 +213,7 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
   FD_DISPATCH_O(out_dtype, {
     auto kern = small ? gemm_e4m3_kernel<TO, 64> : gemm_e4m3_kernel<TO, 128>;
     hipLaunchKernelGGL(kern, dim3(tiles), dim3(F8_NT), 0, (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
-                       (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr);
+                       (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr, act);
   });
   FD_LAUNCH_CHECK();
   return FD_OK;

@@ -188,25 +188,27 @@ def quant_rows_e4m3(x, q=None, scale=None, M=None, K=None, ldx=None):
     return q, scale
 
 
-def gemm_e4m3(a8, a_scale, w8, out=None, bias=None, residual=None, w_scale=1.0, out_dtype=torch.bfloat16):
-    """out[M, N] = a_scale[m] * w_scale * (a8[M, K] @ w8[N, K]^T) + bias + residual on the fp8 MFMA."""
+def gemm_e4m3(a8, a_scale, w8, out=None, bias=None, residual=None, w_scale=1.0, act="none", out_dtype=torch.bfloat16):
+    """out[M, N (N/2 for geglu)] = act(a_scale[m] * w_scale * (a8[M, K] @ w8[N, K]^T) + bias) + residual on the
+    fp8 MFMA (geglu: w8 / bias packed by pack_geglu)."""
     M, K = a8.shape
     N = w8.shape[0]
     if w8.shape[1] != K:
         raise ValueError(f"gemm_e4m3: K mismatch {a8.shape} x {w8.shape}")
+    nout = N // 2 if act == "geglu" else N
     if out is None:
-        out = torch.empty((M, N), dtype=out_dtype, device=a8.device)
-    rc = L.load().fd_gemm_e4m3(L.ptr(a8), a8.stride(0), L.ptr(a_scale), L.ptr(w8), w8.stride(0), w_scale, L.ptr(out),
-                               out.stride(0), M, N, K, L.ptr(bias), L.ptr(residual),
-                               0 if residual is None else residual.stride(0), L.dtype_code(out.dtype), L.stream())
-    L.check(rc, "fd_gemm_e4m3")
+        out = torch.empty((M, nout), dtype=out_dtype, device=a8.device)
+    args = (L.ptr(a8), a8.stride(0), L.ptr(a_scale), L.ptr(w8), w8.stride(0), w_scale, L.ptr(out), out.stride(0),
+            M, N, K, L.ptr(bias), L.ptr(residual), 0 if residual is None else residual.stride(0), L.ACT[act],
+            L.dtype_code(out.dtype), L.stream())
+    _timed("gemm_e4m3", 2.0 * M * N * K, 0.0, lambda: L.check(L.load().fd_gemm_e4m3(*args), "fd_gemm_e4m3"))
     return out
 
 
-def linear_e4m3(x, w8, bias=None, residual=None):
+def linear_e4m3(x, w8, bias=None, residual=None, act="none", out=None):
     """nn.Linear of a quantize_8bit UNet on the fp8 MFMA: per-row e4m3 activations x e4m3 weight bytes."""
     q, s = quant_rows_e4m3(x)
-    return gemm_e4m3(q, s, w8, bias=bias, residual=residual, out_dtype=x.dtype)
+    return gemm_e4m3(q, s, w8, out=out, bias=bias, residual=residual, act=act, out_dtype=x.dtype)
 
 
 def fold_layer_norm(w, gamma, beta, bias=None, dtype=torch.bfloat16):

@@ -35,8 +35,14 @@ def _dev(t, device, dtype):
 
 
 class HipUNet:
-    def __init__(self, sd, device="cuda", dtype=torch.bfloat16):
+    def __init__(self, sd, device="cuda", dtype=torch.bfloat16, fp8_mfma=False):
+        """fp8_mfma: the transformer Linears (proj_in/out, QKV, attention out-projections, GEGLU, ff out) run
+        on the e4m3 MFMA (fd_gemm_e4m3) with the weights as e4m3 bytes and activations quantized per row --
+        the use_fp8 / quantize_8bit model.  Meant for weights already rounded by
+        arch.quantize_e4m3 (then the byte packing is exact); convolutions stay on the 16-bit MFMA, and the
+        separate LayerNorm path is used (the fold needs W * gamma, which is not an e4m3 weight)."""
         L.require_device()
+        self.fp8_mfma = bool(fp8_mfma)
         self.device, self.dtype = torch.device(device), dtype
         f32 = torch.float32
         W = lambda k: _dev(sd[k], self.device, dtype)  # noqa: E731
@@ -69,7 +75,10 @@ class HipUNet:
                            Fp(p + ".conv_shortcut.bias"))
             return r
 
-        self.ln_fold = os.environ.get("FD_LN_FOLD", "1") != "0"
+        self.ln_fold = os.environ.get("FD_LN_FOLD", "1") != "0" and not self.fp8_mfma
+        # transformer Linear weights: e4m3 bytes for the fp8 MFMA, else the compute dtype
+        LW = (lambda t: ops.pack_e4m3(t.to(self.device))) if self.fp8_mfma else \
+            (lambda t: _dev(t, self.device, dtype))  # noqa: E731
 
         def fold(w, n, bias=None):  # (W * gamma, rowsum, W . beta + b) on the device
             dev = lambda t: t.to(self.device)  # noqa: E731
@@ -95,20 +104,20 @@ class HipUNet:
                     continue
                 blocks.append(dict(
                     n1=(Fp(b + ".norm1.weight"), Fp(b + ".norm1.bias")),
-                    qkv=_dev(torch.cat([sd[f"{b}.attn1.to_{n}.weight"] for n in "qkv"], 0), self.device, dtype),
-                    o1=(W(b + ".attn1.to_out.0.weight"), Fp(b + ".attn1.to_out.0.bias")),
+                    qkv=LW(torch.cat([sd[f"{b}.attn1.to_{n}.weight"] for n in "qkv"], 0)),
+                    o1=(LW(sd[b + ".attn1.to_out.0.weight"]), Fp(b + ".attn1.to_out.0.bias")),
                     n2=(Fp(b + ".norm2.weight"), Fp(b + ".norm2.bias")),
-                    q2=W(b + ".attn2.to_q.weight"),
+                    q2=LW(sd[b + ".attn2.to_q.weight"]),
                     kv2=_dev(torch.cat([sd[b + ".attn2.to_k.weight"], sd[b + ".attn2.to_v.weight"]], 0), self.device,
                              dtype),
-                    o2=(W(b + ".attn2.to_out.0.weight"), Fp(b + ".attn2.to_out.0.bias")),
+                    o2=(LW(sd[b + ".attn2.to_out.0.weight"]), Fp(b + ".attn2.to_out.0.bias")),
                     n3=(Fp(b + ".norm3.weight"), Fp(b + ".norm3.bias")),
-                    ff1=(_dev(ffw, self.device, dtype), _dev(ffb, self.device, f32)),
-                    ff2=(W(b + ".ff.net.2.weight"), Fp(b + ".ff.net.2.bias")),
+                    ff1=(LW(ffw), _dev(ffb, self.device, f32)),
+                    ff2=(LW(sd[b + ".ff.net.2.weight"]), Fp(b + ".ff.net.2.bias")),
                 ))
             return dict(c=c, heads=c // 64, norm=(Fp(p + ".norm.weight"), Fp(p + ".norm.bias")),
-                        pin=(W(p + ".proj_in.weight"), Fp(p + ".proj_in.bias")),
-                        pout=(W(p + ".proj_out.weight"), Fp(p + ".proj_out.bias")), blocks=blocks)
+                        pin=(LW(sd[p + ".proj_in.weight"]), Fp(p + ".proj_in.bias")),
+                        pout=(LW(sd[p + ".proj_out.weight"]), Fp(p + ".proj_out.bias")), blocks=blocks)
 
         C, Lr = arch.UNET_CH, arch.UNET_LAYERS
         self.down = []
@@ -214,27 +223,35 @@ class HipUNet:
         h = ops.group_norm(x, *t["norm"], B, HW, C, 32, 1e-6, silu=False)
         if self.ln_fold:
             return self._t2d_folded(t, x, h, B, H, Wd)
-        h = ops.gemm(h, t["pin"][0], bias=t["pin"][1])
+        lin = self._lin
+        h = lin(h, t["pin"][0], bias=t["pin"][1])
         qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
         att = torch.empty((M, C), dtype=self.dtype, device=self.device)
         n = torch.empty((M, C), dtype=self.dtype, device=self.device)
         for b in t["blocks"]:
             ops.layer_norm(h, *b["n1"], 1e-5, out=n)
-            ops.gemm(n, b["qkv"], out=qkv)
+            lin(n, b["qkv"], out=qkv)
             ops.flash_attn(qkv, qkv[:, C:], qkv[:, 2 * C:], att, B, heads, HW, HW, 3 * C, 3 * C, 3 * C, C,
                            HW * 3 * C, HW * 3 * C, HW * 3 * C, HW * C, kv_mod=0, scale=0.125)
-            ops.gemm(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
+            lin(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
             ops.layer_norm(h, *b["n2"], 1e-5, out=n)
-            q = ops.gemm(n, b["q2"], out=qkv[:, :C], ldc=3 * C)
+            q = lin(n, b["q2"], out=qkv[:, :C])  # row stride 3C (the view's)
             kv = self._kv[:, b["kv_off"]:]  # [ncfg*77, ...] view; K at +0, V at +C, row stride kv_total
             Lk, ldkv = self.Lk, self.kv_total
             ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, ldkv, ldkv, C,
                            HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self.ncfg, scale=0.125)
-            ops.gemm(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
+            lin(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
             ops.layer_norm(h, *b["n3"], 1e-5, out=n)
-            ff = ops.gemm(n, b["ff1"][0], bias=b["ff1"][1], act="geglu")
-            ops.gemm(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
-        return ops.gemm(h, t["pout"][0], bias=t["pout"][1], residual=x)
+            ff = lin(n, b["ff1"][0], bias=b["ff1"][1], act="geglu")
+            lin(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
+        return lin(h, t["pout"][0], bias=t["pout"][1], residual=x)
+
+    def _lin(self, x, w, bias=None, residual=None, out=None, act="none"):
+        """A transformer Linear: fd_gemm (16-bit MFMA) or, for the fp8 model, fd_quant_rows_e4m3 + fd_gemm_e4m3."""
+        if self.fp8_mfma:
+            return ops.linear_e4m3(x, w, bias=bias, residual=residual, act=act, out=out)
+        return ops.gemm(x, w, bias=bias, residual=residual, out=out, act=act,
+                        ldc=None if out is None else out.stride(0))
 
     def _t2d_folded(self, t, x, hn, B, H, Wd):
         """_t2d with norm1/2/3 folded into the GEMMs (fd_gemm_params.ln_out / ln_in): `st` holds the

@@ -117,7 +117,8 @@ int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta,
 
 /* ---------------------------------------------------------------------------------------------
  * fp8 (OCP e4m3) GEMM on the block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales):
- *   C[m][n] = out( a_scale[m] * w_scale * sum_k A8[m][k] * W8[n][k] + bias[n] + residual[m][n] )
+ *   C[m][n] = out( act(a_scale[m] * w_scale * sum_k A8[m][k] * W8[n][k] + bias[n]) + residual[m][n] )
+ * act: FD_ACT_* as fd_gemm (GEGLU: W rows packed [16 hidden | 16 gate] per 32, N % 32 == 0, N/2 output columns).
  * A8 [M][lda] e4m3 activations with per-row fp32 scales from fd_quant_rows_e4m3; W8 [N][ldw] e4m3 weights
  * (the reference's unscaled quantize_8bit bytes, utils/system.py:13-32, w_scale = 1).  Out dtype bf16 / f16 /
  * f32 (residual, if given, in the out dtype; not with f32).  Requires K % 16 == 0, lda % 16 == 0, ldw % 16 == 0.
@@ -125,7 +126,7 @@ int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta,
  *   quantized UNet (pipeline_FaithDiff_tlc.py:1349 autocast, utils/system.py:20 .to(float8_e4m3fn)). */
 int fd_gemm_e4m3(const void* A8, long long lda, const float* a_scale, const void* W8, long long ldw, float w_scale,
                  void* C, long long ldc, int M, int N, int K, const float* bias, const void* residual, long long ldr,
-                 int out_dtype, void* stream);
+                 int act, int out_dtype, void* stream);
 
 /* Per-row e4m3 quantization of x[M][K] (row stride ldx, bf16 / f16): scale[m] = amax_m / 448,
  * q[m][k] = e4m3_RNE(x[m][k] * 448 / amax_m) into q (row stride ldq bytes).  Requires K % 16 == 0,
