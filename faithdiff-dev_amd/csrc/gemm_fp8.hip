@@ -8,11 +8,13 @@
 //   (act = SiLU / GELU / QuickGELU, or GEGLU over packed [hidden | gate] row groups -> N/2 columns)
 //
 // Tiles: 128x128 (or 64x128 when 128-row tiles cannot fill 256 CUs) per 256-thread workgroup, 2x2 waves,
-// K-step 128 bytes.  Operands go global -> registers (next K-step prefetched while the MFMAs run) -> double-
-// buffered LDS (144-B row pitch:
+// K-step 128 bytes.  K % 128 == 0: operands go global -> LDS by DMA into a 2/3-stage ring (gemm_e4m3_dma_kernel).
+// Ragged K: global -> registers (next K-step prefetched while the MFMAs run) -> double-buffered LDS (144-B pitch:
 // the 16 rows one ds_read_b128 phase touches land on 16 disjoint 4-bank groups) -> fragments.
 // MFMA operand map (16x16x128, 8-bit): lane l holds row (l & 15), k = 32*(l >> 4) + j, j = 0..31,
 // i.e. 32 contiguous bytes of one row; C/D: col = l & 15, row = 4*(l >> 4) + r.
+#include <stdlib.h>
+
 #include "fd_common.h"
 
 typedef __attribute__((ext_vector_type(8))) int i32x8;
@@ -56,6 +58,50 @@ __device__ __forceinline__ i32x8 f8_frag(const uint8_t* lds, int row, int lane) 
   const uint8_t* p = lds + row * F8_PITCH + (lane >> 4) * 32;
   const u32x4 lo = *(const u32x4*)p, hi = *(const u32x4*)(p + 16);
   return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+// Epilogue shared by both e4m3 kernels: acc[i][j] = C[m0 + wm + 16 i + 4 (lane >> 4) + r][n0 + wn + 16 j + (lane & 15)].
+template <typename TO, int MI>
+__device__ __forceinline__ void f8_epilogue(const f32x4 (&acc)[MI][4], int m0, int n0, int wm, int wn, int lane,
+                                            const float* __restrict__ a_scale, float w_scale, TO* __restrict__ C,
+                                            long long ldc, int M, int N, const float* __restrict__ bias,
+                                            const TO* __restrict__ R, long long ldr, int act) {
+  // epilogue: per-row activation scale x weight scale, bias, residual; 16 lanes store 16 adjacent columns.
+  // GEGLU: W rows are packed [16 hidden | 16 gate] per 32 (ops.pack_geglu), so a wave's column tiles j = 0,1
+  // and 2,3 are the hidden / gate halves of output columns ((n0 + wn) / 32 + j / 2) * 16 + (lane & 15).
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+      if (m >= M) continue;
+      const float s = a_scale[m] * w_scale;
+      if (act == FD_ACT_GEGLU) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const int nh = n0 + wn + g * 32 + (lane & 15);
+          if (nh >= N) continue;
+          float hv = acc[i][2 * g][r] * s, gv = acc[i][2 * g + 1][r] * s;
+          if (bias) hv += bias[nh], gv += bias[nh + 16];
+          const int o = ((n0 + wn) / 32 + g) * 16 + (lane & 15);
+          float v = hv * gelu_f(gv);
+          if (R) v += (float)R[(long long)m * ldr + o];
+          C[(long long)m * ldc + o] = (TO)v;
+        }
+        continue;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn + j * 16 + (lane & 15);
+        if (n >= N) continue;
+        float v = acc[i][j][r] * s;
+        if (bias) v += bias[n];
+        if (act != FD_ACT_NONE) v = act_f(v, act);
+        if (R) v += (float)R[(long long)m * ldr + n];
+        C[(long long)m * ldc + n] = (TO)v;
+      }
+    }
+  }
 }
 
 // BM x 128 tile per workgroup: 2x2 waves of (BM/2) x 64.  LDS is double-buffered: K-step kt+1's operands
@@ -113,42 +159,105 @@ __global__ __launch_bounds__(F8_NT) void gemm_e4m3_kernel(const uint8_t* __restr
     __syncthreads();
   }
 
-  // epilogue: per-row activation scale x weight scale, bias, residual; 16 lanes store 16 adjacent columns.
-  // GEGLU: W rows are packed [16 hidden | 16 gate] per 32 (ops.pack_geglu), so a wave's column tiles j = 0,1
-  // and 2,3 are the hidden / gate halves of output columns ((n0 + wn) / 32 + j / 2) * 16 + (lane & 15).
+  f8_epilogue<TO, MI>(acc, m0, n0, wm, wn, lane, a_scale, w_scale, C, ldc, M, N, bias, R, ldr, act);
+}
+
+template <int N>
+__device__ __forceinline__ void f8_wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// K % 128 == 0 variant: operands go global -> LDS by global_load_lds_dwordx4 (no VGPR round trip) into an
+// NS-deep ring, stages kt+1 .. kt+NS-2 in flight under stage kt's MFMAs (counted vmcnt, one raw barrier per
+// K-step).  A 128-byte K-step of e4m3 is byte-for-byte the 64-element bf16 K-step of gemm.hip, so the same
+// layout applies: 128-B LDS rows, the 16-B chunk c of row r stored at slot c ^ ((r >> 1) & 7) (applied on the
+// per-lane global source address, since the LDS-DMA destination is lane-linear), and the fragment's two
+// chunks 2*(lane >> 4) and 2*(lane >> 4) + 1 read back through the same XOR.  Rows past M / N are clamped.
+template <typename TO, int BM, int NS>
+__global__ __launch_bounds__(F8_NT) void gemm_e4m3_dma_kernel(const uint8_t* __restrict__ A, long long lda,
+                                                               const float* __restrict__ a_scale,
+                                                               const uint8_t* __restrict__ W, long long ldw,
+                                                               float w_scale, TO* __restrict__ C, long long ldc,
+                                                               int M, int N, int K, const float* __restrict__ bias,
+                                                               const TO* __restrict__ R, long long ldr, int act) {
+  constexpr int MI = BM / 32;
+  constexpr int A_INSTR = BM / 32, B_INSTR = F8_BN / 32;  // 1-KB DMA instructions per wave per stage
+  constexpr int PER = A_INSTR + B_INSTR;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + F8_BN) * 128;
+  __shared__ __attribute__((aligned(1024))) uint8_t smem[NS * STAGE];
+  const int tn = (N + F8_BN - 1) / F8_BN, tm = (M + BM - 1) / BM;
+  const int b = xcd_remap(blockIdx.x, tn * tm);
+  const int m0 = (b / tn) * BM, n0 = (b % tn) * F8_BN;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * 64;
+
+  // loader: instruction i of wave w fills LDS rows (i*4 + w)*8 .. +7; lane -> row (lane >> 3), slot (lane & 7)
+  const int lrow = lane >> 3, slot = lane & 7;
+  const uint8_t* a_src[A_INSTR];
+  const uint8_t* b_src[B_INSTR];
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
-      if (m >= M) continue;
-      const float s = a_scale[m] * w_scale;
-      if (act == FD_ACT_GEGLU) {
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          const int nh = n0 + wn + g * 32 + (lane & 15);
-          if (nh >= N) continue;
-          float hv = acc[i][2 * g][r] * s, gv = acc[i][2 * g + 1][r] * s;
-          if (bias) hv += bias[nh], gv += bias[nh + 16];
-          const int o = ((n0 + wn) / 32 + g) * 16 + (lane & 15);
-          float v = hv * gelu_f(gv);
-          if (R) v += (float)R[(long long)m * ldr + o];
-          C[(long long)m * ldc + o] = (TO)v;
-        }
-        continue;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + wn + j * 16 + (lane & 15);
-        if (n >= N) continue;
-        float v = acc[i][j][r] * s;
-        if (bias) v += bias[n];
-        if (act != FD_ACT_NONE) v = act_f(v, act);
-        if (R) v += (float)R[(long long)m * ldr + n];
-        C[(long long)m * ldc + n] = (TO)v;
-      }
-    }
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int r = (i * 4 + wid) * 8 + lrow;
+    a_src[i] = A + (long long)min(m0 + r, M - 1) * lda + ((slot ^ ((r >> 1) & 7)) << 4);
   }
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int r = (i * 4 + wid) * 8 + lrow;
+    b_src[i] = W + (long long)min(n0 + r, N - 1) * ldw + ((slot ^ ((r >> 1) & 7)) << 4);
+  }
+  auto stage = [&](int kt, int buf) {
+    const int k0 = kt * F8_BK;
+    uint8_t* sa = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + k0), LDS_PTR(sa + (i * 4 + wid) * 1024), 16, 0, 0);
+    uint8_t* sb = sa + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + k0), LDS_PTR(sb + (i * 4 + wid) * 1024), 16, 0, 0);
+  };
+
+  f32x4 acc[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / F8_BK;
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0)
+    if (s0 < nk) stage(s0, s0);
+  const int fr = lane & 15, c0 = 2 * (lane >> 4);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(NS - 2, nk - 1 - kt);
+    if (NS >= 4 && ahead >= 2) f8_wait_vmcnt<(NS >= 4 ? 2 * PER : 0)>();
+    else if (NS >= 3 && ahead >= 1) f8_wait_vmcnt<(NS >= 3 ? PER : 0)>();
+    else f8_wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt + NS - 1 < nk) stage(kt + NS - 1, (kt + NS - 1) % NS);
+    const uint8_t* sa = smem + (kt % NS) * STAGE;
+    const uint8_t* sb = sa + A_BYTES;
+    i32x8 fa[MI], fb[4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int r = wm + i * 16 + fr, sw = (r >> 1) & 7;
+      const u32x4 lo = *(const u32x4*)(sa + r * 128 + ((c0 ^ sw) << 4));
+      const u32x4 hi = *(const u32x4*)(sa + r * 128 + (((c0 + 1) ^ sw) << 4));
+      fa[i] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = wn + j * 16 + fr, sw = (r >> 1) & 7;
+      const u32x4 lo = *(const u32x4*)(sb + r * 128 + ((c0 ^ sw) << 4));
+      const u32x4 hi = *(const u32x4*)(sb + r * 128 + (((c0 + 1) ^ sw) << 4));
+      fb[j] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma_e4m3(fa[i], fb[j], acc[i][j]);
+  }
+  f8_epilogue<TO, MI>(acc, m0, n0, wm, wn, lane, a_scale, w_scale, C, ldc, M, N, bias, R, ldr, act);
 }
 
 // One workgroup per row: amax over the row, q = RNE_e4m3(x * 448 / amax), scale = amax / 448.
@@ -210,8 +319,14 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
   const int tn = (N + F8_BN - 1) / F8_BN, t128 = ((M + 127) / 128) * tn;
   const bool small = t128 < 256;
   const int tiles = small ? ((M + 63) / 64) * tn : t128;
+  // K % 128 == 0: LDS-DMA ring kernel -- 64-row tiles with 3 stages (72 KB: two workgroups per CU), 128-row
+  // tiles with 2 stages (64 KB; a 3-stage 96-KB ring leaves one workgroup per CU: 8192x640x640 23 -> 38 us).
+  // Ragged K, or FD_F8_KERNEL=reg (A/B timing): the register-staged kernel.
+  static const char* kenv = getenv("FD_F8_KERNEL");
+  const bool dma = (K % F8_BK) == 0 && !(kenv && kenv[0] == 'r');
   FD_DISPATCH_O(out_dtype, {
-    auto kern = small ? gemm_e4m3_kernel<TO, 64> : gemm_e4m3_kernel<TO, 128>;
+    auto kern = small ? (dma ? gemm_e4m3_dma_kernel<TO, 64, 3> : gemm_e4m3_kernel<TO, 64>)
+                      : (dma ? gemm_e4m3_dma_kernel<TO, 128, 2> : gemm_e4m3_kernel<TO, 128>);
     hipLaunchKernelGGL(kern, dim3(tiles), dim3(F8_NT), 0, (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
                        (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr, act);
   });

@@ -235,10 +235,14 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
 
 // ------------------------------------------------------------------------------------------------
 // LayerNorm: one wave per row, 4 rows per 256-thread block; row kept in registers (C <= 2048).
-template <typename T>
+// Q8: instead of y, write the row quantized to e4m3 for fd_gemm_e4m3 (the use_fp8 model): the LayerNorm output is
+// rounded to T first and then quantized exactly as fd_quant_rows_e4m3 does, so LN + quant fused == LN; quant.
+template <typename T, bool Q8>
 __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x, long long ldx, T* __restrict__ y,
                                                          long long ldy, const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, int M, int C, float eps) {
+                                                         const float* __restrict__ beta, int M, int C, float eps,
+                                                         uint8_t* __restrict__ q8, long long ldq,
+                                                         float* __restrict__ qscale) {
   typedef typename VecT<T>::v8 V8;
   constexpr int MAXV = 4;  // up to 4 vectors of 8 per lane => C <= 2048
   const int lane = threadIdx.x & 63;
@@ -287,6 +291,37 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
     }
   }
   const float rstd = rsqrtf(wave_sum(q) / C + eps);
+  if (Q8) {
+    V8 outs[MAXV];
+    float amax = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int v = lane + k * 64;
+      if (v < VPR) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          outs[k][i] = (T)((vals[k][i] - mean) * rstd * g4[k][i >> 2][i & 3] + b4[k][i >> 2][i & 3]);
+          amax = fmaxf(amax, fabsf((float)outs[k][i]));
+        }
+      }
+    }
+    amax = wave_max(amax);
+    const float inv = amax > 0.f ? __fdiv_rn(448.0f, amax) : 0.f;
+    if (lane == 0) qscale[row] = __fdiv_rn(amax, 448.0f);
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int v = lane + k * 64;
+      if (v < VPR) {
+        const V8 o = outs[k];
+        int lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)o[0] * inv, (float)o[1] * inv, 0, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)o[2] * inv, (float)o[3] * inv, lo, true);
+        int hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)o[4] * inv, (float)o[5] * inv, 0, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)o[6] * inv, (float)o[7] * inv, hi, true);
+        *(u32x2*)(q8 + row * ldq + v * 8) = u32x2{(unsigned)lo, (unsigned)hi};
+      }
+    }
+    return;
+  }
   T* yr = y + row * ldy;
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
@@ -307,8 +342,22 @@ extern "C" int fd_layer_norm(const void* x, long long ldx, void* y, long long ld
   if ((((unsigned long long)gamma) | ((unsigned long long)beta)) & 15) return FD_ERR_ARG;  // 16-B vector loads
   if (M <= 0 || C <= 0 || C % 8 || C > 2048 || (ldx & 7) || (ldy & 7)) return FD_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(layer_norm_kernel<T>, dim3((M + 3) / 4), dim3(256), 0, s, (const T*)x, ldx,
-                                          (T*)y, ldy, gamma, beta, M, C, eps));
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((layer_norm_kernel<T, false>), dim3((M + 3) / 4), dim3(256), 0, s,
+                                          (const T*)x, ldx, (T*)y, ldy, gamma, beta, M, C, eps, nullptr, 0, nullptr));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+extern "C" int fd_layer_norm_e4m3(const void* x, long long ldx, void* q, long long ldq, float* scale,
+                                  const float* gamma, const float* beta, int M, int C, float eps, int dtype,
+                                  void* stream) {
+  if (!x || !q || !scale || !gamma || !beta) return FD_ERR_ARG;
+  if ((((unsigned long long)gamma) | ((unsigned long long)beta)) & 15) return FD_ERR_ARG;
+  if (M <= 0 || C <= 0 || C % 8 || C > 2048 || (ldx & 7) || (ldq & 7) || ldq < C) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((layer_norm_kernel<T, true>), dim3((M + 3) / 4), dim3(256), 0, s,
+                                          (const T*)x, ldx, (T*)nullptr, 0, gamma, beta, M, C, eps, (uint8_t*)q, ldq,
+                                          scale));
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

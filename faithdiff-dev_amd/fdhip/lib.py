@@ -48,6 +48,7 @@ _SIGS = {
     "fd_group_norm": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_int, c_int, c_vp, c_vp]),
     "fd_gemm_e4m3": (c_int, [c_vp, c_ll, c_vp, c_vp, c_ll, c_f, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_ll,
                              c_int, c_int, c_vp]),
+    "fd_layer_norm_e4m3": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp]),
     "fd_quant_rows_e4m3": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp]),
     "fd_layer_norm": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp]),
     "fd_flash_attn": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_int, c_int,

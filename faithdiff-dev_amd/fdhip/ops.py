@@ -188,6 +188,20 @@ def quant_rows_e4m3(x, q=None, scale=None, M=None, K=None, ldx=None):
     return q, scale
 
 
+def layer_norm_e4m3(x, gamma, beta, eps=1e-5, q=None, scale=None):
+    """LayerNorm(x) quantized per row to e4m3 in one launch: (q uint8 [M, C], scale fp32 [M]) bitwise equal to
+    quant_rows_e4m3(layer_norm(x))."""
+    M, C = x.shape
+    if q is None:
+        q = torch.empty((M, C), dtype=torch.uint8, device=x.device)
+    if scale is None:
+        scale = torch.empty((M,), dtype=torch.float32, device=x.device)
+    L.check(L.load().fd_layer_norm_e4m3(L.ptr(x), x.stride(0), L.ptr(q), q.stride(0), L.ptr(scale), L.ptr(gamma),
+                                        L.ptr(beta), M, C, eps, L.dtype_code(x.dtype), L.stream()),
+            "fd_layer_norm_e4m3")
+    return q, scale
+
+
 def gemm_e4m3(a8, a_scale, w8, out=None, bias=None, residual=None, w_scale=1.0, act="none", out_dtype=torch.bfloat16):
     """out[M, N (N/2 for geglu)] = act(a_scale[m] * w_scale * (a8[M, K] @ w8[N, K]^T) + bias) + residual on the
     fp8 MFMA (geglu: w8 / bias packed by pack_geglu)."""

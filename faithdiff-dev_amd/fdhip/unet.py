@@ -227,22 +227,31 @@ class HipUNet:
         h = lin(h, t["pin"][0], bias=t["pin"][1])
         qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
         att = torch.empty((M, C), dtype=self.dtype, device=self.device)
-        n = torch.empty((M, C), dtype=self.dtype, device=self.device)
+        if self.fp8_mfma:  # LayerNorm writes e4m3 rows + scales straight into the fp8 GEMM's A operand
+            q8 = torch.empty((M, C), dtype=torch.uint8, device=self.device)
+            s8 = torch.empty((M,), dtype=torch.float32, device=self.device)
+
+            def ln_lin(norm, w, bias=None, out=None, act="none"):
+                ops.layer_norm_e4m3(h, *norm, 1e-5, q=q8, scale=s8)
+                return ops.gemm_e4m3(q8, s8, w, out=out, bias=bias, act=act, out_dtype=self.dtype)
+        else:
+            n = torch.empty((M, C), dtype=self.dtype, device=self.device)
+
+            def ln_lin(norm, w, bias=None, out=None, act="none"):
+                ops.layer_norm(h, *norm, 1e-5, out=n)
+                return lin(n, w, bias=bias, out=out, act=act)
         for b in t["blocks"]:
-            ops.layer_norm(h, *b["n1"], 1e-5, out=n)
-            lin(n, b["qkv"], out=qkv)
+            ln_lin(b["n1"], b["qkv"], out=qkv)
             ops.flash_attn(qkv, qkv[:, C:], qkv[:, 2 * C:], att, B, heads, HW, HW, 3 * C, 3 * C, 3 * C, C,
                            HW * 3 * C, HW * 3 * C, HW * 3 * C, HW * C, kv_mod=0, scale=0.125)
             lin(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
-            ops.layer_norm(h, *b["n2"], 1e-5, out=n)
-            q = lin(n, b["q2"], out=qkv[:, :C])  # row stride 3C (the view's)
+            ln_lin(b["n2"], b["q2"], out=qkv[:, :C])  # row stride 3C (the view's)
             kv = self._kv[:, b["kv_off"]:]  # [ncfg*77, ...] view; K at +0, V at +C, row stride kv_total
             Lk, ldkv = self.Lk, self.kv_total
             ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, ldkv, ldkv, C,
                            HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self.ncfg, scale=0.125)
             lin(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
-            ops.layer_norm(h, *b["n3"], 1e-5, out=n)
-            ff = lin(n, b["ff1"][0], bias=b["ff1"][1], act="geglu")
+            ff = ln_lin(b["n3"], b["ff1"][0], bias=b["ff1"][1], act="geglu")
             lin(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
         return lin(h, t["pout"][0], bias=t["pout"][1], residual=x)
 

@@ -115,6 +115,13 @@ long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups);
 int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
                   int groups, float eps, int silu, int dtype, void* ws, void* stream);
 
+/* LayerNorm fused with the per-row e4m3 quantization of fd_quant_rows_e4m3 (use_fp8 model): the row is
+ * normalised, rounded to dtype, then q[m][:] = e4m3_RNE(y * 448 / amax_m), scale[m] = amax_m / 448 -- bitwise
+ * equal to fd_layer_norm followed by fd_quant_rows_e4m3, without the 16-bit round trip.  ldq % 8 == 0.
+ * Replaces: norm1/2/3 of BasicTransformerBlock (diffusers) ahead of the quantized UNet's Linears. */
+int fd_layer_norm_e4m3(const void* x, long long ldx, void* q, long long ldq, float* scale, const float* gamma,
+                       const float* beta, int M, int C, float eps, int dtype, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * fp8 (OCP e4m3) GEMM on the block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales):
  *   C[m][n] = out( act(a_scale[m] * w_scale * sum_k A8[m][k] * W8[n][k] + bias[n]) + residual[m][n] )

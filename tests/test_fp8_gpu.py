@@ -109,6 +109,19 @@ def test_linear_e4m3_vs_dequantized_and_unquantized(M, N, K):
     assert rel_l2(got, want_ref) < 4e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,C", [(4096, 640), (1024, 1280), (7, 320), (130, 2048)])
+def test_layer_norm_e4m3_equals_layer_norm_then_quant(dtype, M, C):
+    """fd_layer_norm_e4m3 == fd_layer_norm; fd_quant_rows_e4m3, bit for bit (bytes and scales)."""
+    from fdhip import ops
+    x = (torch.randn(M, C, device=DEV) * 3 + 1).to(dtype)
+    g = torch.randn(C, device=DEV)
+    b = torch.randn(C, device=DEV)
+    q, s = ops.layer_norm_e4m3(x, g, b, 1e-5)
+    q_ref, s_ref = ops.quant_rows_e4m3(ops.layer_norm(x, g, b, 1e-5))
+    assert torch.equal(s, s_ref) and torch.equal(q, q_ref)
+
+
 def test_gemm_e4m3_rejects_bad_shapes():
     from fdhip import ops
     a8 = torch.zeros(64, 24, dtype=torch.uint8, device=DEV)  # K % 16 != 0
