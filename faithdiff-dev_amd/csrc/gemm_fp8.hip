@@ -162,6 +162,103 @@ __global__ __launch_bounds__(F8_NT) void gemm_e4m3_kernel(const uint8_t* __restr
   f8_epilogue<TO, MI>(acc, m0, n0, wm, wn, lane, a_scale, w_scale, C, ldc, M, N, bias, R, ldr, act);
 }
 
+template <typename TO> struct F8Vec;
+template <> struct F8Vec<bf16> {
+  static __device__ __forceinline__ void ld(const bf16* p, float (&v)[8]) {
+    const bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)x[i];
+  }
+  static __device__ __forceinline__ void st(bf16* p, const float (&v)[8]) {
+    bf16x8 x;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = (bf16)v[i];
+    *(bf16x8*)p = x;
+  }
+};
+template <> struct F8Vec<f16> {
+  static __device__ __forceinline__ void ld(const f16* p, float (&v)[8]) {
+    const f16x8 x = *(const f16x8*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)x[i];
+  }
+  static __device__ __forceinline__ void st(f16* p, const float (&v)[8]) {
+    f16x8 x;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = (f16)v[i];
+    *(f16x8*)p = x;
+  }
+};
+template <> struct F8Vec<float> {
+  static __device__ __forceinline__ void ld(const float* p, float (&v)[8]) {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+    v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+  }
+  static __device__ __forceinline__ void st(float* p, const float (&v)[8]) {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+    *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+};
+
+// Vector epilogue through LDS (needs BM * 128 * 4 bytes of `ep`, the drained operand ring): phase 1 writes
+// act(scale * acc + bias) -- GEGLU already combined -- as fp32 into a [BM][W] tile (W = 128, or 64 output
+// columns for GEGLU); phase 2 gives each thread 8 contiguous columns: one 16-B residual load and one 16-B
+// store per chunk instead of eight 2-byte ones.  Requires nout % 8 == 0, ldc % 8 == 0, ldr % 8 == 0.
+template <typename TO, int BM, int MI>
+__device__ __forceinline__ void f8_epilogue_vec(const f32x4 (&acc)[MI][4], float* ep, int m0, int n0, int wm,
+                                                int wn, int lane, const float* __restrict__ a_scale,
+                                                float w_scale, TO* __restrict__ C, long long ldc, int M, int N,
+                                                const float* __restrict__ bias, const TO* __restrict__ R,
+                                                long long ldr, int act) {
+  const bool geglu = act == FD_ACT_GEGLU;
+  const int W = geglu ? F8_BN / 2 : F8_BN;
+  __syncthreads();  // every wave is done reading the operand ring
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int lr = wm + i * 16 + (lane >> 4) * 4 + r;
+      const float s = a_scale[min(m0 + lr, M - 1)] * w_scale;
+      if (geglu) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const int nh = min(n0 + wn + g * 32, N - 32) + (lane & 15);  // whole groups past N: clamped, unused
+          float hv = acc[i][2 * g][r] * s, gv = acc[i][2 * g + 1][r] * s;
+          if (bias) hv += bias[nh], gv += bias[nh + 16];
+          ep[lr * W + (wn / 32 + g) * 16 + (lane & 15)] = hv * gelu_f(gv);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int lc = wn + j * 16 + (lane & 15);
+          float v = acc[i][j][r] * s;
+          if (bias) v += bias[min(n0 + lc, N - 1)];
+          if (act != FD_ACT_NONE) v = act_f(v, act);
+          ep[lr * W + lc] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int nout = geglu ? N / 2 : N, c0 = geglu ? n0 / 2 : n0;
+  const int cpr = W / 8;  // 8-column chunks per row
+  for (int c = threadIdx.x; c < BM * cpr; c += F8_NT) {
+    const int lr = c / cpr, lc = (c - lr * cpr) * 8;
+    const int m = m0 + lr, n = c0 + lc;
+    if (m >= M || n >= nout) continue;
+    float v[8];
+    const f32x4 a = *(const f32x4*)(ep + lr * W + lc), b = *(const f32x4*)(ep + lr * W + lc + 4);
+    v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+    if (R) {
+      float rv[8];
+      F8Vec<TO>::ld(R + (long long)m * ldr + n, rv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += rv[e];
+    }
+    F8Vec<TO>::st(C + (long long)m * ldc + n, v);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void f8_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -179,8 +276,10 @@ __global__ __launch_bounds__(F8_NT) void gemm_e4m3_dma_kernel(const uint8_t* __r
                                                                const uint8_t* __restrict__ W, long long ldw,
                                                                float w_scale, TO* __restrict__ C, long long ldc,
                                                                int M, int N, int K, const float* __restrict__ bias,
-                                                               const TO* __restrict__ R, long long ldr, int act) {
+                                                               const TO* __restrict__ R, long long ldr, int act,
+                                                               int vec) {
   constexpr int MI = BM / 32;
+  static_assert(NS * (BM + F8_BN) * 128 >= BM * F8_BN * 4, "vector epilogue tile must fit in the ring");
   constexpr int A_INSTR = BM / 32, B_INSTR = F8_BN / 32;  // 1-KB DMA instructions per wave per stage
   constexpr int PER = A_INSTR + B_INSTR;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + F8_BN) * 128;
@@ -257,7 +356,11 @@ __global__ __launch_bounds__(F8_NT) void gemm_e4m3_dma_kernel(const uint8_t* __r
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma_e4m3(fa[i], fb[j], acc[i][j]);
   }
-  f8_epilogue<TO, MI>(acc, m0, n0, wm, wn, lane, a_scale, w_scale, C, ldc, M, N, bias, R, ldr, act);
+  if (vec)
+    f8_epilogue_vec<TO, BM, MI>(acc, (float*)smem, m0, n0, wm, wn, lane, a_scale, w_scale, C, ldc, M, N, bias, R,
+                                ldr, act);
+  else
+    f8_epilogue<TO, MI>(acc, m0, n0, wm, wn, lane, a_scale, w_scale, C, ldc, M, N, bias, R, ldr, act);
 }
 
 // One workgroup per row: amax over the row, q = RNE_e4m3(x * 448 / amax), scale = amax / 448.
@@ -324,11 +427,21 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
   // Ragged K, or FD_F8_KERNEL=reg (A/B timing): the register-staged kernel.
   static const char* kenv = getenv("FD_F8_KERNEL");
   const bool dma = (K % F8_BK) == 0 && !(kenv && kenv[0] == 'r');
+  // 16-B vector epilogue when every output row / residual row starts 16-B aligned (FD_F8_KERNEL=scalar: off)
+  const int vec = (nout % 8) == 0 && (ldc % 8) == 0 && (((unsigned long long)C) & 15) == 0 &&
+                  (!residual || ((ldr % 8) == 0 && (((unsigned long long)residual) & 15) == 0)) &&
+                  !(kenv && kenv[0] == 's');
   FD_DISPATCH_O(out_dtype, {
-    auto kern = small ? (dma ? gemm_e4m3_dma_kernel<TO, 64, 3> : gemm_e4m3_kernel<TO, 64>)
-                      : (dma ? gemm_e4m3_dma_kernel<TO, 128, 2> : gemm_e4m3_kernel<TO, 128>);
-    hipLaunchKernelGGL(kern, dim3(tiles), dim3(F8_NT), 0, (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
-                       (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr, act);
+    if (dma) {
+      auto kern = small ? gemm_e4m3_dma_kernel<TO, 64, 3> : gemm_e4m3_dma_kernel<TO, 128, 2>;
+      hipLaunchKernelGGL(kern, dim3(tiles), dim3(F8_NT), 0, (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
+                         (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr, act,
+                         vec);
+    } else {
+      auto kern = small ? gemm_e4m3_kernel<TO, 64> : gemm_e4m3_kernel<TO, 128>;
+      hipLaunchKernelGGL(kern, dim3(tiles), dim3(F8_NT), 0, (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
+                         (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr, act);
+    }
   });
   FD_LAUNCH_CHECK();
   return FD_OK;

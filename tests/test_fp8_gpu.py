@@ -34,7 +34,8 @@ def widen(q):
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 128), (200, 72, 320), (77, 1280, 2048), (16, 16, 16),
-                                   (2048, 1280, 1280), (333, 640, 5120), (4100, 1030, 272), (8192, 640, 640)])
+                                   (2048, 1280, 1280), (333, 640, 5120), (4100, 1030, 272), (8192, 640, 640),
+                                   (96, 100, 256)])
 def test_gemm_e4m3_exact_integers(M, N, K):
     """Asymmetric small-integer operands: every product and partial sum is exact in fp32, so any error in
     the 16x16x128 lane map, the K / M / N tails or the epilogue shows as a mismatch."""
@@ -132,7 +133,7 @@ def test_gemm_e4m3_rejects_bad_shapes():
                       torch.zeros(32, 48, dtype=torch.uint8, device=DEV))
 
 
-@pytest.mark.parametrize("M,F,K", [(2048, 5120, 1280), (300, 96, 320)])
+@pytest.mark.parametrize("M,F,K", [(2048, 5120, 1280), (300, 96, 320), (300, 48, 256)])
 def test_gemm_e4m3_geglu(M, F, K):
     """GEGLU epilogue on the fp8 MFMA (diffusers GEGLU: (x W_h + b_h) * gelu(x W_g + b_g), exact GELU), against
     the fp64 product of the same dequantized operands: rel-L2 <= 5e-5 (fp32 out; erff and the gate product
