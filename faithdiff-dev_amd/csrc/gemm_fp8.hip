@@ -395,14 +395,59 @@ __global__ __launch_bounds__(256) void quant_rows_e4m3_kernel(const T* __restric
     *(i32x2*)(qr + k) = i32x2{lo, hi};
   }
 }
+// K <= 64 * 8 * MAXV: one wave per row, 4 rows per workgroup, the row held in registers between the amax
+// and the conversion (one HBM read instead of two, and no idle lanes on short rows).  Same arithmetic as
+// quant_rows_e4m3_kernel, so both give identical bytes.
+template <typename T, int MAXV>
+__global__ __launch_bounds__(256) void quant_rows_e4m3_wave_kernel(const T* __restrict__ x, long long ldx,
+                                                                   uint8_t* __restrict__ q, long long ldq,
+                                                                   float* __restrict__ scale, int M, int K) {
+  typedef typename VecT<T>::v8 V8;
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int VPR = K / 8;
+  const T* xr = x + row * ldx;
+  V8 v[MAXV];
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j)
+    if (lane + j * 64 < VPR) v[j] = *(const V8*)(xr + (lane + j * 64) * 8);
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j)
+    if (lane + j * 64 < VPR)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf((float)v[j][i]));
+  amax = wave_max(amax);
+  const float inv = amax > 0.f ? __fdiv_rn(448.0f, amax) : 0.f;
+  if (lane == 0) scale[row] = __fdiv_rn(amax, 448.0f);
+  uint8_t* qr = q + row * ldq;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int c = lane + j * 64;
+    if (c < VPR) {
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[j][0] * inv, (float)v[j][1] * inv, 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[j][2] * inv, (float)v[j][3] * inv, lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[j][4] * inv, (float)v[j][5] * inv, 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32((float)v[j][6] * inv, (float)v[j][7] * inv, hi, true);
+      *(i32x2*)(qr + c * 8) = i32x2{lo, hi};
+    }
+  }
+}
 }  // namespace
 
 extern "C" int fd_quant_rows_e4m3(const void* x, long long ldx, void* q, long long ldq, float* scale, int M, int K,
                                   int dtype, void* stream) {
   if (!x || !q || !scale) return FD_ERR_ARG;
   if (M <= 0 || K <= 0 || (K % 16) || (ldx % 8) || (ldq % 16) || ldx < K || ldq < K) return FD_ERR_SHAPE;
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(quant_rows_e4m3_kernel<T>, dim3(M), dim3(256), 0, (hipStream_t)stream,
-                                          (const T*)x, ldx, (uint8_t*)q, ldq, scale, K));
+  hipStream_t s = (hipStream_t)stream;
+  if (K <= 2048) {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((quant_rows_e4m3_wave_kernel<T, 4>), dim3((M + 3) / 4), dim3(256), 0, s,
+                                            (const T*)x, ldx, (uint8_t*)q, ldq, scale, M, K));
+  } else {  // long rows (the 5120-wide GEGLU output): a workgroup per row measured faster (6.3 vs 7.0 us at M = 2048)
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL(quant_rows_e4m3_kernel<T>, dim3(M), dim3(256), 0, s, (const T*)x, ldx,
+                                            (uint8_t*)q, ldq, scale, K));
+  }
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

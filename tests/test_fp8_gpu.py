@@ -66,7 +66,7 @@ def test_gemm_e4m3_scales_bias_residual():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("M,K", [(1, 16), (77, 2048), (2048, 1280), (513, 5120)])
+@pytest.mark.parametrize("M,K", [(1, 16), (77, 2048), (2048, 1280), (513, 5120), (33, 6144), (6, 2064)])
 def test_quant_rows_e4m3_bitexact(dtype, M, K):
     from fdhip import ops
     x = (torch.randn(M, K, device=DEV) * torch.logspace(-3, 2, M, device=DEV)[:, None]).to(dtype)
