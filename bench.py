@@ -36,6 +36,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0
+PEAK_FP8_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 
 
@@ -324,6 +325,13 @@ def main():
         "vae_norm": vae_norm,
         "kernel_ms_per_forward": {k: round(v[3], 3) for k, v in kstats.items()},
     }
+    if "gemm_e4m3" in kstats:  # use_fp8: the e4m3 Linears against the fp8 peak (the bf16 roofline above = convs)
+        n_f, fl_f, _, ms_f = kstats["gemm_e4m3"]
+        f8_tf = fl_f / (ms_f / 1e3) / 1e12
+        result["roofline_fp8"] = {"bound": "mfma", "achieved": round(f8_tf, 1), "peak": PEAK_FP8_TFLOPS,
+                                  "unit": "TFLOP/s", "frac": round(f8_tf / PEAK_FP8_TFLOPS, 4),
+                                  "kernel": "gemm_e4m3_dma_kernel (transformer Linears, e4m3 x e4m3)",
+                                  "launches": n_f, "algorithmic_flops": fl_f, "kernel_ms_per_forward": round(ms_f, 3)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(args.size)
