@@ -50,9 +50,9 @@ def test_gemm_e4m3_exact_integers(M, N, K):
     assert torch.equal(got.double(), want)
 
 
-def test_gemm_e4m3_scales_bias_residual():
+@pytest.mark.parametrize("M,N,K", [(300, 200, 640), (300, 320, 640), (2048, 1280, 256)])
+def test_gemm_e4m3_scales_bias_residual(M, N, K):
     from fdhip import ops
-    M, N, K = 300, 200, 640
     g = torch.Generator().manual_seed(5)
     a = torch.randint(-6, 7, (M, K), generator=g).float()
     w = torch.randint(-4, 5, (N, K), generator=g).float()
