@@ -1,140 +1,296 @@
 #!/usr/bin/env python3
 """FaithDiff denoising hot path on MI355X -- headline benchmark (BASELINE.json metric).
 
-metric: denoise steps/s at 1024x1024 (C2: one 128x128 latent tile, CFG batch 2, 20-step Euler), plus the
-fp16 VAE decode time at 1024^2.  A "step" = one pass of the hot path over one tile batch: TLC split +
-scale_model_input -> UNet (SDXL + FaithDiff extras, bf16) -> CFG combine + Euler step -> gaussian blend,
-exactly the per-step work of pipeline_FaithDiff_tlc.py:1324-1409.  Weights are seeded random-init of the
-real architecture (2.58 B params), inputs synthetic; everything is resident in HBM before timing.
+metric: denoise steps/s at 1024x1024 (C2 = BASELINE configs[1]: one 128x128 latent tile, CFG batch 2, 20-step
+Euler), plus the fp16 VAE decode time at 1024^2.  A "step" = one pass of the hot path over one tile batch: TLC
+split + scale_model_input -> UNet (SDXL + FaithDiff extras, bf16; one hipGraph replay through HipUNet.run, the
+same call the pipeline's denoise loop makes) -> CFG combine + Euler step -> gaussian blend, i.e. the per-step
+work of pipeline_FaithDiff_tlc.py:1324-1409.  Weights are seeded random-init of the real architecture (2.58 B
+params, built by the product factory FaithDiff_pipeline('random-init', ...)), inputs synthetic; everything is
+resident in HBM before timing.
 
-Multi-GPU (torchrun, one rank per GPU): every rank restores its own 1024^2 image (C5-style independent
-images, no data-path collective), so `scaling` is "weak" and value = total steps/s of all ranks (timed
-with a barrier + synchronize on both sides, max over ranks).  The tile-sharded path for one large image
-(C3/C4, one all-gather per step) is FaithDiff/pipelines/tile_parallel.py, exercised by the tests.
+Launch: ``python bench.py --gpus N`` starts N rank processes itself (torch.distributed.run, before any GPU call)
+unless it already runs under torchrun (WORLD_SIZE set, which must equal N).
 
-roofline: the dominant kernel is the MFMA GEMM (gemm_kernel: every projection, FF and implicit-GEMM 3x3
-conv of the UNet, ~76% of a step).  achieved = its algorithmic FLOPs (2*M*N*K per launch, summed over the
-launches of one UNet forward) / the summed launch durations, each launch bracketed by HIP events on its
-launch stream in an instrumented (eager) forward after the timed region; peak = 2500 TFLOP/s dense bf16
-MFMA (MI355X_MICROARCH.md).  traffic = HBM bytes of the same launches from the committed rocprofv3 PMC
-pass (profiles/r01_gemm_traffic.json: 2*FETCH_SIZE + WRITE_SIZE, gfx950 correction), else null.
-"step_roofline" is the same ratio for the whole graph-replayed step (14.217 TFLOP analytic);
-"attention" and "vae_norm" report flash-attention MFMA TFLOP/s and VAE GroupNorm HBM GB/s the same way.
-cpu_baseline: the fp32 CPU oracle (the repo's restatement of the reference path) timed on this host for
-a bounded sample (1 denoise step of the same C2 tile).
+Workloads (``--workload``; all ranks time exactly --steps steps between barrier + synchronize, max over ranks):
+  c2 (default)  every rank restores its own 1024^2 image (replicas, no data-path collective): value = total
+                steps/s, scaling "weak".  The same line also carries
+                  * "pipeline": the product ``pipe(...)`` call end to end at C2 (encode_prompt, denoise encoder,
+                    VAE encode, 20 steps, VAE decode, postprocess) -- s/image and its per-step time;
+                  * "c3": BASELINE configs[2] -- one 4096^2 image (49 TLC tiles, tiled VAE) restored by ALL
+                    ranks together through the product pipeline with ``enable_tile_parallel`` (tiles sharded,
+                    one all_gather_into_tensor per step over RCCL, sharded tiled decode): s/image, tile-steps/s;
+  c3            the C3 image is the timed unit: value = tile-steps/s of the whole job (strong scaling);
+  c5            BASELINE configs[4]: 8 images of 1024^2 x 50 steps split over the ranks: value = images/s.
+
+roofline: the dominant kernel family is the MFMA GEMM (gemm8_kernel + gemm_kernel: every projection, FF and
+implicit-GEMM conv of the UNet, ~80 % of a step).  While the UNet forward is captured, every launch is also
+recorded (ops.set_recorder); the GEMM launches of one forward are then captured on their own into a second
+hipGraph and that graph is timed with HIP events on its stream: achieved = sum 2*M*N*K of those launches / the
+measured time per forward.  The same is done for flash attention ("attention") and for the VAE decoder's
+GroupNorms ("vae_norm", HBM bytes).  profiles/<round>_roofline_check.json recomputes each figure from the
+rocprofv3 kernel trace of the same command.  peak: 2500 TFLOP/s dense bf16 MFMA (MI355X_MICROARCH.md).
+traffic: HBM bytes of the same launches from the committed rocprofv3 PMC pass (profiles/*_gemm_traffic.json).
+cpu_baseline: the fp32 CPU oracle (the repo's restatement of the reference path; the reference itself cannot run
+here: diffusers is absent) timed on this host for a bounded sample (1 denoise step of the same C2 tile).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "faithdiff-dev_amd"))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_FP8_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_gemm_traffic.json")
 
 
-def event_pair_overhead_ms(n=64):
-    """Median elapsed time of an event pair with nothing between them, on a busy-then-idle stream: the
-    per-launch bias the probe subtracts (rocprofv3 --kernel-trace of the same run cross-checks it)."""
-    x = torch.empty(1 << 20, device="cuda")
-    ts = []
-    for _ in range(n):
-        x.mul_(1.0)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        e1.record()
-        ts.append((e0, e1))
-    torch.cuda.synchronize()
-    v = sorted(a.elapsed_time(b) for a, b in ts)
-    return v[len(v) // 2]
-
-
-def probe(fn, reps=3):
-    """Run fn() `reps` times with the per-launch event probe on; per kind: (launches, FLOPs, bytes, ms),
-    averaged per call of fn, each launch's event time less the empty event-pair time."""
-    from fdhip import ops
-    bias = event_pair_overhead_ms()
-    rec = []
-    ops.set_probe(rec)
-    try:
-        for _ in range(reps):
-            fn()
-    finally:
-        ops.set_probe(None)
-    torch.cuda.synchronize()
-    agg = {}
-    for kind, fl, nb, e0, e1, *_ in rec:
-        a = agg.setdefault(kind, [0, 0.0, 0.0, 0.0])
-        a[0] += 1
-        a[1] += fl
-        a[2] += nb
-        a[3] += max(e0.elapsed_time(e1) - bias, 1e-4)
-    return {k: (v[0] // reps, v[1] / reps, v[2] / reps, v[3] / reps) for k, v in agg.items()}
-
-
-def load_traffic():
-    path = os.path.join(ROOT, "profiles", "r01_gemm_traffic.json")
-    try:
-        with open(path) as f:
-            return json.load(f)
-    except (OSError, ValueError):
-        return None
-
-
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--size", type=int, default=1024, help="image side (latent = size/8)")
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2")
+    ap.add_argument("--size", type=int, default=1024, help="C2 image side (latent = size/8)")
     ap.add_argument("--fp8", action="store_true", help="use_fp8 model (quantize_8bit weights; transformer Linears "
-                                                       "on the e4m3 MFMA): the C4 arithmetic on the C2 tile")
+                                                       "on the e4m3 MFMA): the C4 arithmetic")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vae", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the C2 pipe(...) s/image leg")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 leg of the c2 workload")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--c3-size", type=int, default=4096)
+    ap.add_argument("--c3-steps", type=int, default=20)
+    ap.add_argument("--c5-images", type=int, default=8)
+    ap.add_argument("--c5-steps", type=int, default=50)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof windows)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def setup_dist(n):
+# ------------------------------------------------------------------------------------------------ launch
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, n, port):
+    """The torchrun command that runs this script as n ranks (the driver's own form of the N-GPU run)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_launch(args, argv):
+    """--gpus N without WORLD_SIZE: start N rank processes (before anything touches the GPU) and return their
+    exit code; under torchrun, WORLD_SIZE must equal --gpus.  Returns None when this process is a rank."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus > 1:
+            env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+            return subprocess.call(launcher_cmd(argv, args.gpus, _free_port()), env=env)
+        return None
+    if int(world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to report a mislabelled run",
+              file=sys.stderr)
+        return 2
+    return None
+
+
+def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
     return world, rank, local
 
 
-def build(size, seed, fp8=False):
-    from fdhip import arch
-    from fdhip.unet import HipUNet
-    dev = torch.device("cuda", torch.cuda.current_device())
-    sd = arch.random_init(arch.unet_param_shapes(True), seed=seed, device=dev)
-    if fp8:
-        sd = arch.quantize_e4m3(sd)
-    unet = HipUNet(sd, dev, torch.bfloat16, fp8_mfma=fp8)
-    del sd
-    return unet
+def barrier(world):
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
 
 
+def max_over_ranks(x, world, dev):
+    t = torch.tensor([float(x)], device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ------------------------------------------------------------------------------------------------ model
+def build_pipe(dev, fp8):
+    from CKPT_PTH import FAITHDIFF_PATH, SDXL_PATH, VAE_FP16_PATH  # 'random-init' sentinels offline
+    from FaithDiff.create_FaithDiff_model import FaithDiff_pipeline
+    pipe = FaithDiff_pipeline(SDXL_PATH, VAE_FP16_PATH, FAITHDIFF_PATH, use_fp8=fp8, fp8_mfma=fp8 or None, seed=0,
+                              init_device=dev)
+    pipe = pipe.to(dev)
+    pipe.unet.release_host_weights()
+    return pipe
+
+
+def synthetic_image(H, W, seed):
+    """A smooth seeded RGB test card (content does not change the work; parity uses tests/golden inputs)."""
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    img = np.zeros((H, W, 3), np.float32)
+    for c in range(3):
+        fx, fy = rng.uniform(1, 8, 2)
+        img[..., c] = np.sin(xx / W * fx * 6.28) * np.cos(yy / H * fy * 6.28)
+    img += rng.normal(0, 0.1, (H, W, 3)).astype(np.float32)
+    img = (img - img.min()) / (img.max() - img.min())
+    return Image.fromarray((img * 255).astype(np.uint8))
+
+
+class EventTimer:
+    """The pipeline's ``timer`` hook: an event per (label, step) on the current stream."""
+
+    def __init__(self):
+        self.ev = []
+
+    def __call__(self, label, i):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.ev.append((label, i, e))
+
+    def step_ms(self):
+        st = [e for (lab, _, e) in self.ev if lab in ("loop_start", "step")]
+        d = [a.elapsed_time(b) for a, b in zip(st[:-1], st[1:])]
+        return d
+
+    def span_ms(self, a, b):
+        ea = next(e for (lab, _, e) in self.ev if lab == a)
+        eb = next(e for (lab, _, e) in reversed(self.ev) if lab == b)
+        return ea.elapsed_time(eb)
+
+
+# ------------------------------------------------------------------------------------------------ C2 hot loop
+class C2Loop:
+    """The per-step work of pipeline_FaithDiff_tlc.py:1324-1409 for one 128^2 tile (C2), on the pipeline's own
+    HipUNet.  Each step: fd_tlc_scale_input -> HipUNet.run (hipGraph replay) -> fd_tlc_cfg_euler_step ->
+    fd_tlc_blend."""
+
+    def __init__(self, pipe, size, rank):
+        from FaithDiff.pipelines.tlc import TileGrid
+        from FaithDiff.schedulers import EulerDiscreteScheduler
+        from fdhip import ops
+        self.ops = ops
+        self.unet = unet = pipe.unet.hip()
+        dev = unet.device
+        self.h = self.w = h = size // 8
+        self.k = k = min(128, h)
+        self.cfg, self.B = 2, 2
+        g = torch.Generator(device=dev).manual_seed(1234 + rank)
+        self.canvas = torch.randn((4, h, h), generator=g, device=dev) * 11.0
+        self.nxt = torch.empty_like(self.canvas)
+        self.cond = torch.randn((self.B * k * k, 512), generator=g, device=dev).to(unet.dtype)
+        ctx = torch.randn((2, 77, 2048), generator=g, device=dev)
+        self.text = torch.randn((self.B, 1280), generator=g, device=dev)
+        self.tids = torch.tensor([[size, size, 0, 0, size, size]] * self.B, dtype=torch.float32, device=dev)
+        self.grid = TileGrid(h, h, (128, 128), 0.5)
+        self.rows = torch.tensor(self.grid.rows, dtype=torch.int32, device=dev)
+        self.cols = torch.tensor(self.grid.cols, dtype=torch.int32, device=dev)
+        self.weights = torch.tensor(self.grid.weights(), dtype=torch.float64, device=dev)
+        sch = EulerDiscreteScheduler()
+        sch.set_timesteps(20)
+        self.sig, self.ts = [float(s) for s in sch.sigmas], [float(t) for t in sch.timesteps]
+        unet.set_context(ctx)
+        self.xin = torch.empty((self.B * k * k, 4), dtype=unet.dtype, device=dev)
+        self.t_buf = torch.full((self.B,), self.ts[0], device=dev)
+        self.out_tiles = torch.empty((self.grid.ntiles, 4, k, k), device=dev)
+        ops.reserve_gn_workspace(1 << 24, dev)
+
+    def args(self):
+        return (self.xin, self.t_buf, self.tids, self.text, self.cond, self.B, self.k, self.k)
+
+    def step(self, i):
+        ops, k, h = self.ops, self.k, self.h
+        s_, sn = self.sig[i % 20], self.sig[i % 20 + 1]
+        ops.tlc_scale_input(self.canvas, self.rows, self.cols, h, h, k, k, 0, self.grid.ntiles, self.cfg, s_,
+                            self.xin)
+        self.t_buf.fill_(self.ts[i % 20])
+        eps = self.unet.run(*self.args())
+        ops.tlc_cfg_euler_step(eps, self.canvas, self.rows, self.cols, h, h, k, k, 0, self.grid.ntiles, self.cfg,
+                               5.0, 0.0, s_, sn, self.out_tiles)
+        ops.tlc_blend(self.out_tiles, self.weights, self.rows, self.cols, 4, h, h, k, k, self.nxt)
+        self.canvas, self.nxt = self.nxt, self.canvas
+
+
+# ------------------------------------------------------------------------------------------------ kernel families
+def family_times(fn, kinds, reps=20):
+    """Capture fn() into a hipGraph with the launch recorder on, then capture the launches of each kind on their
+    own into a second graph and time its replays with HIP events.  Returns {kind: (launches, flops, bytes,
+    ms per call of fn)} plus the full graph's ms per call under key '_all'."""
+    from fdhip import ops
+    rec = []
+    torch.cuda.synchronize()
+    g_all = torch.cuda.CUDAGraph()
+    ops.set_recorder(rec)
+    try:
+        with torch.cuda.graph(g_all):
+            fn()
+    finally:
+        ops.set_recorder(None)
+    out = {}
+
+    def timed(g):
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    g_all.replay()
+    out["_all"] = (len(rec), sum(r[1] for r in rec), sum(r[2] for r in rec), timed(g_all))
+    for kind in kinds:
+        sel = [r for r in rec if r[0] == kind]
+        if not sel:
+            continue
+        gk = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gk):
+            for r in sel:
+                r[3]()
+        out[kind] = (len(sel), sum(r[1] for r in sel), sum(r[2] for r in sel), timed(gk))
+        del gk
+    del g_all
+    return out
+
+
+def load_traffic(workload):
+    try:
+        with open(TRAFFIC_FILE) as f:
+            tr = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return tr if tr.get("workload") == workload else None
+
+
+# ------------------------------------------------------------------------------------------------ legs
 def cpu_baseline(size):
     """One denoise step of the same C2 tile with the fp32 CPU oracle (test infrastructure, not shipped)."""
     sys.path.insert(0, ROOT)
     from oracle import schedulers as S
     from oracle.unet import UNet2DConditionModel
     threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(threads, 64))
+    threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", threads))))
     torch.set_num_threads(threads)
     with torch.no_grad():
         ref = UNet2DConditionModel()
@@ -157,192 +313,242 @@ def cpu_baseline(size):
         dt = time.perf_counter() - t0
     return {"value": 1.0 / dt, "unit": "steps/s", "cores": threads, "kind": "port",
             "sample": f"1 denoise step (UNet fwd B=2 @ {h}x{h} latent + CFG/Euler) of C2, fp32 oracle, "
-                      f"{threads} host threads, {dt:.1f} s"}
+                      f"{threads} host threads (OMP_NUM_THREADS / affinity), {dt:.1f} s"}
 
 
-def main():
-    args = parse()
-    world, rank, local = setup_dist(args.gpus)
+def run_pipeline_image(pipe, img, H, W, steps, target, seed=42):
+    """One product ``pipe(...)`` call as test_wo_llava.py:86 makes it; returns (s, EventTimer)."""
+    tm = EventTimer()
+    gen = torch.Generator(device=pipe.device).manual_seed(seed)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tm("call_start", 0)
+    pipe(lr_img=img, prompt="A high quality photo restored from a degraded capture.", negative_prompt="",
+         num_inference_steps=steps, guidance_scale=5.0, generator=gen, start_point="lr", height=H, width=W,
+         overlap=0.5, target_size=target, timer=tm)
+    tm("call_end", 0)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, tm
+
+
+def pipeline_leg(pipe, size, steps=20):
+    img = synthetic_image(size, size, 5)
+    run_pipeline_image(pipe, img, size, size, 2, (1024, 1024))  # warm: captures the UNet / VAE graphs
+    s, tm = run_pipeline_image(pipe, img, size, size, steps, (1024, 1024))
+    st = tm.step_ms()
+    return {"workload": f"C2 pipe(...) {size}x{size}, {steps} Euler steps, start_point 'lr', CFG 5, test_wo_llava.py "
+                        "call (encode_prompt + denoise encoder + VAE encode + denoise loop + VAE decode + postprocess)",
+            "s_per_image": round(s, 4), "loop_ms": round(sum(st), 2),
+            "step_ms_median": round(float(np.median(st)), 3), "step_ms_min": round(min(st), 3),
+            "decode_ms": round(tm.span_ms("decode_start", "decode"), 2),
+            "pre_loop_ms": round(tm.span_ms("call_start", "loop_start"), 2)}
+
+
+def c3_run(pipe, world, rank, dev, size, steps, warm=True):
+    """BASELINE configs[2]: one size^2 image (49 TLC tiles at 4096^2) restored by all ranks together."""
+    from FaithDiff.pipelines.tlc import TileGrid
+    if world > 1 and pipe.process_group is None:
+        pipe.enable_tile_parallel()
+    pipe.enable_vae_tiling()
+    img = synthetic_image(size, size, 6)
+    ntiles = TileGrid(size // 8, size // 8, (128, 128), 0.5).ntiles
+    try:
+        if warm:
+            run_pipeline_image(pipe, img, size, size, 1, (1024, 1024))
+        barrier(world)
+        s, tm = run_pipeline_image(pipe, img, size, size, steps, (1024, 1024))
+        barrier(world)
+    finally:
+        pipe.disable_vae_tiling()
+    s = max_over_ranks(s, world, dev)
+    st = tm.step_ms()
+    loop_s = max_over_ranks(sum(st) / 1e3, world, dev)
+    return {"workload": f"C3: {size}x{size} tiled restoration, {ntiles} TLC tiles x {steps} Euler steps, tiled VAE "
+                        f"encode/decode, tiles sharded over {world} rank(s), one all_gather_into_tensor per step",
+            "ntiles": ntiles, "steps": steps, "n_ranks": world, "s_per_image": round(s, 3),
+            "loop_s": round(loop_s, 3), "tile_steps_per_s": round(ntiles * steps / loop_s, 3),
+            "step_ms_median": round(float(np.median(st)), 2),
+            "pre_loop_ms": round(tm.span_ms("call_start", "loop_start"), 1),
+            "decode_ms": round(tm.span_ms("decode_start", "decode"), 1),
+            "all_gather_bytes_per_step": (ntiles + (-ntiles) % world) * 4 * 128 * 128 * 4 if world > 1 else 0}
+
+
+def roofline_leg(loop, fp8):
+    from fdhip import arch
+    fam = family_times(lambda: loop.unet.forward(*loop.args()), ["gemm", "flash_attn", "gemm_e4m3"])
+    n_g, fl_g, _, ms_g = fam["gemm"]
+    gemm_tf = fl_g / (ms_g / 1e3) / 1e12
+    res = {}
+    tr = None if fp8 else load_traffic(f"C2 {loop.h * 8}")
+    res["roofline"] = {
+        "bound": "mfma", "achieved": round(gemm_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(gemm_tf / PEAK_BF16_TFLOPS, 4),
+        "traffic": None if tr is None else tr["hbm_bytes_per_forward"],
+        "kernel": "gemm8_kernel + gemm_kernel (all MFMA GEMM + implicit-GEMM conv launches of one UNet forward)",
+        "launches": n_g, "algorithmic_flops": fl_g, "kernel_ms_per_forward": round(ms_g, 3),
+        "avg_launch_us": round(ms_g / n_g * 1e3, 2),
+        "method": "the forward's GEMM launches captured on their own into one hipGraph, replayed 20x between HIP "
+                  "events on the capture stream",
+        "traffic_note": "HBM bytes per forward of these launches (rocprofv3 PMC pass, " + os.path.basename(TRAFFIC_FILE)
+                        + ")" if tr else "no PMC pass committed for this workload"}
+    if "flash_attn" in fam:
+        n_a, fl_a, _, ms_a = fam["flash_attn"]
+        a_tf = fl_a / (ms_a / 1e3) / 1e12
+        res["attention"] = {"bound": "mfma", "achieved": round(a_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                            "frac": round(a_tf / PEAK_BF16_TFLOPS, 4), "launches": n_a, "ms_per_forward": round(ms_a, 3),
+                            "kernel": "flash_attn_d64_kernel (140 self/cross attentions per forward)"}
+    if "gemm_e4m3" in fam:
+        n_f, fl_f, _, ms_f = fam["gemm_e4m3"]
+        f8_tf = fl_f / (ms_f / 1e3) / 1e12
+        res["roofline_fp8"] = {"bound": "mfma", "achieved": round(f8_tf, 1), "peak": PEAK_FP8_TFLOPS,
+                               "unit": "TFLOP/s", "frac": round(f8_tf / PEAK_FP8_TFLOPS, 4),
+                               "kernel": "gemm_e4m3_dma_kernel (transformer Linears, e4m3 x e4m3)",
+                               "launches": n_f, "algorithmic_flops": fl_f, "kernel_ms_per_forward": round(ms_f, 3)}
+    flops = arch.unet_flops(loop.k, loop.k, loop.B)
+    res["forward_graph_ms"] = round(fam["_all"][3], 3)
+    res["kernel_ms_per_forward"] = {k: round(v[3], 3) for k, v in fam.items() if not k.startswith("_")}
+    return res, flops
+
+
+def vae_leg(pipe, loop):
     from fdhip import arch, ops
+    dec = pipe.vae.decoder_hip()
+    h, w = loop.h, loop.w
+    z = torch.empty((h * w, 4), dtype=torch.float16, device=loop.unet.device)
+    ops.nchw_to_nhwc(loop.canvas, z, 1, 4, h * w, 1.0 / 0.13025)
+    for _ in range(3):
+        dec.decode_graphed(z, 1, h, w)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dec.decode_graphed(z, 1, h, w)
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+    vae_ms = sorted(times)[2]
+    fam = family_times(lambda: dec.decode(z, 1, h, w), ["gemm", "group_norm"], reps=5)
+    res = {"vae_decode_ms": round(vae_ms, 2),
+           "vae_decode_tflops": round(arch.vae_decode_flops(h, w) / (vae_ms / 1e3) / 1e12, 1)}
+    if "group_norm" in fam:
+        n_n, _, nb_n, ms_n = fam["group_norm"]
+        gbs = nb_n / (ms_n / 1e3) / 1e9
+        res["vae_norm"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                           "frac": round(gbs / PEAK_HBM_GBS, 4), "launches": n_n, "ms": round(ms_n, 3),
+                           "algorithmic_bytes": nb_n, "kernel": "GroupNorm(+SiLU) of the 1024^2 VAE decode"}
+    if "gemm" in fam:
+        n_c, fl_c, _, ms_c = fam["gemm"]
+        res["vae_conv"] = {"bound": "mfma", "achieved": round(fl_c / (ms_c / 1e3) / 1e12, 1), "peak": PEAK_BF16_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(fl_c / (ms_c / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                           "launches": n_c, "ms": round(ms_c, 3), "kernel": "fp16 implicit-GEMM convs of the decode"}
+    res["vae_kernel_ms"] = {k: round(v[3], 3) for k, v in fam.items() if not k.startswith("_")}
+    return res
+
+
+# ------------------------------------------------------------------------------------------------ main
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    rc = maybe_launch(args, argv)
+    if rc is not None:
+        return rc
+    world, rank, local = setup_dist()
     from fdhip import lib as L
     L.require_device()
-    dev = torch.device("cuda", torch.cuda.current_device())
-    h = w = args.size // 8
-    k = min(128, h)
-    cfg, B = 2, 2
-    unet = build(args.size, seed=0, fp8=args.fp8)
+    dev = torch.device("cuda", local)
+    pipe = build_pipe(dev, args.fp8)
+    result = {"n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+              "vs_baseline": None, "dtype": "fp8-e4m3+bf16" if args.fp8 else "bf16",
+              "data": "synthetic (seeded random-init SDXL+FaithDiff weights, synthetic latents/conditions/images)"}
 
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    canvas = torch.randn((4, h, w), generator=g, device=dev) * 11.0
-    canvas_next = torch.empty_like(canvas)
-    cond = (torch.randn((B * k * k, 512), generator=g, device=dev)).to(torch.bfloat16)
-    ctx = torch.randn((2, 77, 2048), generator=g, device=dev)
-    text = torch.randn((B, 1280), generator=g, device=dev)
-    tids = torch.tensor([[args.size, args.size, 0, 0, args.size, args.size]] * B, dtype=torch.float32, device=dev)
-    rows = torch.tensor([0], dtype=torch.int32, device=dev)
-    cols = torch.tensor([0], dtype=torch.int32, device=dev)
-    from FaithDiff.pipelines.tlc import TileGrid
-    from FaithDiff.schedulers import EulerDiscreteScheduler
-    grid = TileGrid(h, w, (128, 128), 0.5)
-    rows = torch.tensor(grid.rows, dtype=torch.int32, device=dev)
-    cols = torch.tensor(grid.cols, dtype=torch.int32, device=dev)
-    weights = torch.tensor(grid.weights(), dtype=torch.float64, device=dev)
-    sch = EulerDiscreteScheduler()
-    sch.set_timesteps(20)
-    sig = sch.sigmas
-    unet.set_context(ctx)
-    xin = torch.empty((B * k * k, 4), dtype=torch.bfloat16, device=dev)
-    t_buf = torch.full((B,), float(sch.timesteps[0]), device=dev)
-    out_tiles = torch.empty((grid.ntiles, 4, k, k), device=dev)
-    ops.reserve_gn_workspace(1 << 24, dev)
-
-    def unet_fwd():
-        return unet.forward(xin, t_buf, tids, text, cond, B, k, k)
-
-    graph = None
-    eps_static = None
-    if not args.no_graph:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                unet_fwd()
-        torch.cuda.current_stream().wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            eps_static = unet_fwd()
-
-    state = {"cv": canvas, "nx": canvas_next}
-
-    def step(i):
-        s_, sn = float(sig[i % 20]), float(sig[i % 20 + 1])
-        ops.tlc_scale_input(state["cv"], rows, cols, h, w, k, k, 0, grid.ntiles, cfg, s_, xin)
-        t_buf.fill_(float(sch.timesteps[i % 20]))
-        if graph is not None:
-            graph.replay()
-            eps = eps_static
-        else:
-            eps = unet_fwd()
-        ops.tlc_cfg_euler_step(eps, state["cv"], rows, cols, h, w, k, k, 0, grid.ntiles, cfg, 5.0, 0.0, s_, sn,
-                               out_tiles)
-        ops.tlc_blend(out_tiles, weights, rows, cols, 4, h, w, k, k, state["nx"])
-        state["cv"], state["nx"] = state["nx"], state["cv"]
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for i in range(args.steps):
-        step(i)
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1)
-    t_local = torch.tensor([wall], device=dev)
-    if world > 1:
-        dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
-    t_max = float(t_local.item())
-    for i in range(args.profile_steps):
-        step(i)
-    torch.cuda.synchronize()
-    # instrumented eager forwards (outside the timed region): per-kernel-family durations
-    kstats = probe(unet_fwd)
-
-    # ---- VAE decode at the same size (ms), separately timed
-    vae_ms, vstats = None, {}
-    if not args.no_vae:
-        from fdhip.vae import HipDecoder
-        vsd = arch.random_init(arch.vae_param_shapes(), seed=3, device=dev)
-        dec = HipDecoder(vsd, dev, torch.float16)
-        del vsd
-        z = torch.empty((h * w, 4), dtype=torch.float16, device=dev)
-        ops.nchw_to_nhwc(state["cv"], z, 1, 4, h * w, 1.0 / 0.13025)
-        for _ in range(2):
-            dec.decode(z, 1, h, w)
+    if args.workload == "c3":
+        c3_run(pipe, world, rank, dev, args.c3_size, 1, warm=False)  # warm-up: graphs captured
+        reps = []
+        barrier(world)
+        for _ in range(max(1, args.steps // 20)):
+            reps.append(c3_run(pipe, world, rank, dev, args.c3_size, args.c3_steps, warm=False))
+        r = reps[-1]
+        result.update({"metric": "C3 tile-steps/sec @4096px 20-step (49 TLC tiles, tile-sharded over RCCL)",
+                       "value": r["tile_steps_per_s"], "unit": "tile-steps/s", "scaling": "strong",
+                       "ms_per_step": round(r["loop_s"] / r["steps"] * 1e3, 2),
+                       "config": {"workload": r["workload"], "s_per_image": r["s_per_image"],
+                                  "parallelism": f"tile-sharded x{world}"}, "c3": r})
+    elif args.workload == "c5":
+        ims = list(range(rank, args.c5_images, world))
+        img = synthetic_image(args.size, args.size, 7)
+        run_pipeline_image(pipe, img, args.size, args.size, 2, (1024, 1024))
+        barrier(world)
+        t0 = time.perf_counter()
+        for i in ims:
+            run_pipeline_image(pipe, img, args.size, args.size, args.c5_steps, (1024, 1024), seed=100 + i)
+        barrier(world)
+        t = max_over_ranks(time.perf_counter() - t0, world, dev)
+        result.update({"metric": "C5 images/sec, 1024px 50-step pipe(...) calls, batch of 8 split over ranks",
+                       "value": round(args.c5_images / t, 4), "unit": "images/s", "scaling": "strong",
+                       "ms_per_step": round(t / (len(ims) * args.c5_steps) * 1e3, 2),
+                       "config": {"workload": f"C5: {args.c5_images} images of {args.size}^2 x {args.c5_steps} "
+                                              "Euler steps, image-parallel replicas", "global_batch": args.c5_images,
+                                  "parallelism": f"replicas x{world}"}})
+    else:
+        loop = C2Loop(pipe, args.size, rank)
+        for i in range(args.warmup):
+            loop.step(i)
+        barrier(world)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record()
+        for i in range(args.steps):
+            loop.step(i)
+        ev1.record()
+        barrier(world)
+        wall = time.perf_counter() - t0
+        t_max = max_over_ranks(wall, world, dev)
+        for i in range(args.profile_steps):
+            loop.step(i)
         torch.cuda.synchronize()
-        times = []
-        for _ in range(3):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            dec.decode(z, 1, h, w)
-            e1.record()
-            torch.cuda.synchronize()
-            times.append(e0.elapsed_time(e1))
-        vae_ms = sorted(times)[1]
-        vstats = probe(lambda: dec.decode(z, 1, h, w), reps=2)
-
-    steps_total = args.steps * world
-    value = steps_total / t_max
-    ms_step = t_max / args.steps * 1e3
-    flops = arch.unet_flops(k, k, B)
-    step_s = ev_ms / 1e3 / args.steps
-    achieved = flops / step_s / 1e12
-    n_g, fl_g, _, ms_g = kstats["gemm"]
-    gemm_tf = fl_g / (ms_g / 1e3) / 1e12
-    tr = load_traffic()
-    traffic = None
-    if tr and tr.get("workload") == f"C2 {args.size}" and not args.fp8:
-        traffic = tr["hbm_bytes_per_forward"]
-    n_a, fl_a, _, ms_a = kstats["flash_attn"]
-    attn_tf = fl_a / (ms_a / 1e3) / 1e12
-    vae_norm = None
-    if "group_norm" in vstats:
-        n_n, _, nb_n, ms_n = vstats["group_norm"]
-        vae_norm = {"bound": "hbm", "achieved": round(nb_n / (ms_n / 1e3) / 1e9, 1), "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": round(nb_n / (ms_n / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
-                    "launches": n_n, "ms": round(ms_n, 3), "algorithmic_bytes": nb_n}
-    result = {
-        "metric": "denoise steps/sec @1024px 20-step + VAE decode ms",
-        "value": round(value, 4), "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp8-e4m3+bf16" if args.fp8 else "bf16", "data": "synthetic (seeded random-init SDXL+FaithDiff weights, random latents/conditions)",
-        "config": {"workload": f"C2: {args.size}x{args.size} single TLC tile, CFG batch 2, Euler step + blend, "
-                               f"UNet {'use_fp8: transformer Linears e4m3 MFMA, convs bf16' if args.fp8 else 'bf16'} "
-                               f"(hipGraph={graph is not None}), VAE fp16",
-                   "model": "SDXL UNet + FaithDiff extras (2.58B params)", "global_batch": 2 * world,
-                   "latent": [h, w], "parallelism": f"replicas x{world}"},
-        "vae_decode_ms": None if vae_ms is None else round(vae_ms, 2),
-        "vae_decode_tflops": None if vae_ms is None else round(arch.vae_decode_flops(h, w) / (vae_ms / 1e3) / 1e12, 1),
-        "roofline": {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(gemm_tf / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                     "kernel": "gemm8_kernel + gemm_kernel (all MFMA GEMM + implicit-GEMM conv launches of one UNet forward)",
-                     "launches": n_g, "algorithmic_flops": fl_g, "kernel_ms_per_forward": round(ms_g, 3),
-                     "avg_launch_us": round(ms_g / n_g * 1e3, 2),
-                     "traffic_note": "HBM bytes per forward of these launches (PMC pass)" if traffic else
-                                     "no PMC pass committed for this workload"},
-        "step_roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
-                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                          "algorithmic_flops_per_step": flops, "event_ms_per_step": round(step_s * 1e3, 3)},
-        "attention": {"bound": "mfma", "achieved": round(attn_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                      "frac": round(attn_tf / PEAK_BF16_TFLOPS, 4), "launches": n_a, "ms": round(ms_a, 3)},
-        "vae_norm": vae_norm,
-        "kernel_ms_per_forward": {k: round(v[3], 3) for k, v in kstats.items()},
-    }
-    if "gemm_e4m3" in kstats:  # use_fp8: the e4m3 Linears against the fp8 peak (the bf16 roofline above = convs)
-        n_f, fl_f, _, ms_f = kstats["gemm_e4m3"]
-        f8_tf = fl_f / (ms_f / 1e3) / 1e12
-        result["roofline_fp8"] = {"bound": "mfma", "achieved": round(f8_tf, 1), "peak": PEAK_FP8_TFLOPS,
-                                  "unit": "TFLOP/s", "frac": round(f8_tf / PEAK_FP8_TFLOPS, 4),
-                                  "kernel": "gemm_e4m3_dma_kernel (transformer Linears, e4m3 x e4m3)",
-                                  "launches": n_f, "algorithmic_flops": fl_f, "kernel_ms_per_forward": round(ms_f, 3)}
+        ev_ms = ev0.elapsed_time(ev1)
+        from fdhip import arch
+        flops = arch.unet_flops(loop.k, loop.k, loop.B)
+        step_s = ev_ms / 1e3 / args.steps
+        result.update({
+            "metric": "denoise steps/sec @1024px 20-step + VAE decode ms",
+            "value": round(args.steps * world / t_max, 4), "unit": "steps/s",
+            "ms_per_step": round(t_max / args.steps * 1e3, 3), "scaling": "weak",
+            "config": {"workload": f"C2: {args.size}x{args.size} single TLC tile, CFG batch 2, Euler step + blend, "
+                                   f"UNet {'use_fp8: transformer Linears e4m3 MFMA, convs bf16' if args.fp8 else 'bf16'}"
+                                   " (HipUNet.run: hipGraph replay), VAE fp16",
+                       "model": "SDXL UNet + FaithDiff extras (2.58B params)", "global_batch": 2 * world,
+                       "latent": [loop.h, loop.w], "parallelism": f"replicas x{world}"},
+            "step_roofline": {"bound": "mfma", "achieved": round(flops / step_s / 1e12, 1), "peak": PEAK_BF16_TFLOPS,
+                              "unit": "TFLOP/s", "frac": round(flops / step_s / 1e12 / PEAK_BF16_TFLOPS, 4),
+                              "algorithmic_flops_per_step": flops, "event_ms_per_step": round(step_s * 1e3, 3)}})
+        if not args.no_roofline:
+            rl, _ = roofline_leg(loop, args.fp8)
+            result.update(rl)
+        if not args.no_vae:
+            result.update(vae_leg(pipe, loop))
+        del loop
+        if not args.no_pipeline:
+            result["pipeline"] = pipeline_leg(pipe, args.size)
+        if not args.no_c3:
+            result["c3"] = c3_run(pipe, world, rank, dev, args.c3_size, args.c3_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(args.size)
         except Exception as e:  # the baseline must not sink the GPU measurement
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:
-        print(json.dumps(result))
+        order = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                 "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"]
+        line = {k: result[k] for k in order if k in result}
+        line.update({k: v for k, v in result.items() if k not in line})
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

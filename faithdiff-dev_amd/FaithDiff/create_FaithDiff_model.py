@@ -7,7 +7,9 @@ Paths that equal CKPT_PTH.RANDOM_INIT ('random-init') draw seeded random weights
 diffusers directories / a local ``FaithDiff.bin`` are loaded with safe loaders (no hub download, no
 pickle execution).  Extra keyword arguments (defaults keep the reference call working unchanged):
 ``seed`` (random-init seed), ``unet_dtype`` (bf16 per the north star; fp16 also supported),
-``init_device`` ('cpu' for host-generated weights shared with the CPU oracle, 'cuda' for fast init).
+``init_device`` ('cpu' for host-generated weights shared with the CPU oracle, 'cuda' for fast init),
+``fp8_mfma`` (with ``use_fp8``: opt in to the e4m3 MFMA for the transformer Linears; default None = the
+FD_FP8_MFMA env var, default off = the reference's 16-bit arithmetic on e4m3 weights).
 """
 import torch
 
@@ -19,7 +21,7 @@ from .schedulers import DDPMScheduler
 
 
 def FaithDiff_pipeline(sdxl_path, VAE_FP16_path, FaithDiff_path, use_fp8=False, seed=0,
-                       unet_dtype=torch.bfloat16, init_device="cpu"):
+                       unet_dtype=torch.bfloat16, init_device="cpu", fp8_mfma=None):
     dtype = torch.float16
     vae = AutoencoderKL.from_pretrained(VAE_FP16_path, seed=seed, init_device=init_device).to(dtype=dtype)
     unet = UNet2DConditionModel.from_pretrained(sdxl_path, subfolder="unet", variant="fp16", seed=seed,
@@ -29,7 +31,7 @@ def FaithDiff_pipeline(sdxl_path, VAE_FP16_path, FaithDiff_path, use_fp8=False, 
         fd_path = f"{fd_path}/FaithDiff.bin"
     unet.load_additional_layers(weight_path=fd_path, dtype=dtype, init_device=init_device)
     if use_fp8:
-        quantize_8bit(unet)
+        quantize_8bit(unet, fp8_mfma=fp8_mfma)
     unet.to(dtype=unet_dtype)
     pipe = FaithDiffStableDiffusionXLPipeline.from_pretrained(
         sdxl_path, vae=vae, add_sample=True, denoise_encoder=unet.denoise_encoder, DDPM_scheduler=DDPMScheduler(),

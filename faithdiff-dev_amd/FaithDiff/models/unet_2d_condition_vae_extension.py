@@ -68,6 +68,7 @@ class UNet2DConditionModel:
         self._device = torch.device("cpu")
         self._hip = None
         self._fp8 = False
+        self._fp8_mfma = None
         self.denoise_encoder = None
         self.information_transformer_layes = None
         self.condition_embedding = None
@@ -123,11 +124,16 @@ class UNet2DConditionModel:
         self.spatial_ch_projs = "spatial_ch_projs.weight" in self._sd or None
         self._hip = None
 
-    def quantize_8bit(self):
+    def quantize_8bit(self, fp8_mfma=None):
         """utils/system.py:13-32: every UNet parameter (core + extras, incl. norms and biases) becomes unscaled
-        float8_e4m3fn; compute stays 16-bit (bf16 here, fp16 under the reference's autocast).  The denoise
-        encoder stays fp16 (:24-26).  See fdhip.arch.quantize_e4m3."""
+        float8_e4m3fn.  By default compute stays 16-bit on the exact e4m3 values (bf16 here, fp16 under the
+        reference's autocast, pipeline:1349) -- the reference's arithmetic.  ``fp8_mfma=True`` (or
+        FD_FP8_MFMA=1) opts in to the CDNA4 e4m3 MFMA for the transformer Linears, which ALSO quantizes their
+        activations per row to e4m3: a numerics change the reference does not make.  The
+        denoise encoder stays fp16 (:24-26).  See fdhip.arch.quantize_e4m3."""
         self._fp8 = True
+        if fp8_mfma is not None:
+            self._fp8_mfma = bool(fp8_mfma)
         self._hip = None
 
     # ------------------------------------------------------------------ device
@@ -162,9 +168,10 @@ class UNet2DConditionModel:
             cdt = torch.bfloat16 if self._dtype in (torch.float32, torch.bfloat16, torch.float8_e4m3fn) \
                 else self._dtype
             sd = arch.quantize_e4m3(self._sd) if self._fp8 else self._sd
-            # the quantized model's transformer Linears run on the e4m3 MFMA (FD_FP8_MFMA=0: 16-bit MFMA on the
-            # widened e4m3 values, i.e. exactly the reference's autocast arithmetic)
-            fp8_mfma = self._fp8 and os.environ.get("FD_FP8_MFMA", "1") != "0"
+            # default: 16-bit MFMA on the widened e4m3 values (exactly the reference's autocast arithmetic);
+            # opt-in (quantize_8bit(fp8_mfma=True) or FD_FP8_MFMA=1): transformer Linears on the e4m3 MFMA
+            opt = self._fp8_mfma if self._fp8_mfma is not None else os.environ.get("FD_FP8_MFMA", "0") == "1"
+            fp8_mfma = self._fp8 and opt
             self._hip = HipUNet(sd, self._device, cdt, fp8_mfma=fp8_mfma)
         return self._hip
 
@@ -251,7 +258,7 @@ class Encoder:
         if self.use_tiling and (W > self.tile_latent_min_size or H > self.tile_latent_min_size):
             from fdhip.tiling import tiled_encoder_forward
             return tiled_encoder_forward(self, x, H, W, self.process_group)
-        return self.hip().encode(x, 1, H, W)
+        return self.hip().encode_graphed(x, 1, H, W)
 
     def __call__(self, sample):
         """NCHW [1,3,H,W] -> NCHW [1,512,H/8,W/8] (reference signature, ext:192-196)."""
@@ -345,20 +352,20 @@ class AutoencoderKL:
         if self.use_tiling and (H > self.tile_sample_min_size or W > self.tile_sample_min_size):
             from fdhip.tiling import tiled_vae_encode
             return tiled_vae_encode(self, x, H, W, self.process_group)
-        return self.encoder_hip().encode(x, 1, H, W)
+        return self.encoder_hip().encode_graphed(x, 1, H, W)
 
     def decode_nhwc(self, z, h, w):
         tl = self.tile_latent_min_size
         if self.use_tiling and (h > tl or w > tl):
             from fdhip.tiling import tiled_vae_decode
             return tiled_vae_decode(self, z, h, w, self.process_group)
-        return self.decoder_hip().decode(z, 1, h, w)
+        return self.decoder_hip().decode_graphed(z, 1, h, w)
 
     def encode(self, x, return_dict=True):
         _, _, H, W = x.shape
         xn = torch.empty((H * W, 3), dtype=self.dtype, device=self._device)
         ops.nchw_to_nhwc(x.to(self._device).contiguous(), xn, 1, 3, H * W)
-        m = self.encode_moments_nhwc(xn, H, W)
+        m = self.encode_moments_nhwc(xn, H, W).clone()  # the latent_dist outlives the graph's output buffer
         d = _LatentDist(self, m, H // 8, W // 8)
         return SimpleNamespace(latent_dist=d) if return_dict else (d,)
 

@@ -17,6 +17,8 @@ import math
 import torch
 import torch.distributed as dist
 
+from fdhip.comm import all_gather_into, broadcast  # noqa: F401  (re-exported for the pipeline)
+
 
 class TileShard:
     def __init__(self, ntiles, group=None):
@@ -32,7 +34,7 @@ class TileShard:
         """local: [per, ...] (first `count` rows valid); buf: [world*per, ...].  Returns the first N rows."""
         if self.world == 1:
             return local[:self.ntiles]
-        dist.all_gather_into_tensor(buf, local, group=self.group)
+        all_gather_into(buf, local, self.group)
         return buf[:self.ntiles]
 
 
@@ -56,7 +58,7 @@ def broadcast_state_dict(sd, group=None, src=0, device=None, bucket_bytes=256 <<
                 nbytes += sd[k].numel() * sd[k].element_size()
             if bucket and (k is None or nbytes >= bucket_bytes):
                 flat = torch.cat([sd[b].reshape(-1) for b in bucket]).to(device or sd[bucket[0]].device)
-                dist.broadcast(flat, src=src_global, group=group)
+                broadcast(flat, src_global, group)
                 off = 0
                 for b in bucket:
                     n = sd[b].numel()

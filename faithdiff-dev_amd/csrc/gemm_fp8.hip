@@ -440,6 +440,8 @@ extern "C" int fd_quant_rows_e4m3(const void* x, long long ldx, void* q, long lo
                                   int dtype, void* stream) {
   if (!x || !q || !scale) return FD_ERR_ARG;
   if (M <= 0 || K <= 0 || (K % 16) || (ldx % 8) || (ldq % 16) || ldx < K || ldq < K) return FD_ERR_SHAPE;
+  // 16-B vector loads of x rows and 8-B stores of q rows: an offset view (x[:, 8:]) must be rejected, not faulted
+  if ((((unsigned long long)x) | ((unsigned long long)q)) & 15) return FD_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (K <= 2048) {
     FD_DISPATCH_T(dtype, hipLaunchKernelGGL((quant_rows_e4m3_wave_kernel<T, 4>), dim3((M + 3) / 4), dim3(256), 0, s,
@@ -461,6 +463,8 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
   if (M <= 0 || N <= 0 || K <= 0 || (K % 16) || (lda % 16) || (ldw % 16) || lda < K || ldw < K || ldc < nout)
     return FD_ERR_SHAPE;
   if (act == FD_ACT_GEGLU && (N % 32)) return FD_ERR_SHAPE;
+  // both kernels stage A / W rows with 16-B loads (register or LDS-DMA): base pointers must be 16-B aligned
+  if ((((unsigned long long)A) | ((unsigned long long)W)) & 15) return FD_ERR_ARG;
   if (residual && ldr < nout) return FD_ERR_SHAPE;
   if (residual && out_dtype == FD_F32) return FD_ERR_DTYPE;
   // 64-row tiles when 128-row tiles leave CUs idle (fewer than 256 workgroups, e.g. the M = 2048 projections)

@@ -1,0 +1,65 @@
+"""hipGraph capture of whole forwards (UNet, VAE decoder / encoders) for the product path.
+
+A UNet forward is ~800 kernel launches issued from Python through ctypes; replaying it as one hipGraph
+removes the host from the denoise loop (pipeline_FaithDiff_tlc.py:1330-1376 launches the same work eagerly
+per tile).  ``GraphCache.run(key, fn, inputs)``:
+
+  * the first call with a given key runs ``fn`` eagerly (it also sizes the split-K / GroupNorm workspaces,
+    which must not grow inside a capture);
+  * the second call captures ``fn`` on static copies of the inputs into a private memory pool;
+  * every later call copies the inputs into those static buffers (a few MB at most) and replays.
+
+The returned tensor is the graph's static output: valid until the next replay of the same key, so callers
+that keep it (tiled decode) copy it out.  Non-tensor arguments must be part of ``key``.  FD_GRAPHS=0
+disables capture (every call eager), for A/B timing and debugging.
+"""
+import collections
+import os
+
+import torch
+
+
+class GraphCache:
+    def __init__(self, max_graphs=8, min_uses=2):
+        self.max_graphs = max_graphs
+        self.min_uses = min_uses
+        self.enabled = os.environ.get("FD_GRAPHS", "1") != "0"
+        self._uses = collections.Counter()
+        self._graphs = collections.OrderedDict()  # key -> (graph, static inputs, static output)
+
+    def clear(self):
+        self._graphs.clear()
+        self._uses.clear()
+
+    def __len__(self):
+        return len(self._graphs)
+
+    def run(self, key, fn, inputs):
+        """fn(*inputs) -> tensor.  ``inputs``: tensors (None allowed) whose shapes / dtypes are fixed by key."""
+        if not self.enabled or torch.cuda.is_current_stream_capturing():
+            return fn(*inputs)
+        ent = self._graphs.get(key)
+        if ent is None:
+            self._uses[key] += 1
+            if self._uses[key] < self.min_uses:
+                return fn(*inputs)
+            ent = self._capture(key, fn, inputs)
+        else:
+            self._graphs.move_to_end(key)
+        g, static, out = ent
+        for s, x in zip(static, inputs):
+            if s is not None and s.data_ptr() != x.data_ptr():
+                s.copy_(x)
+        g.replay()
+        return out
+
+    def _capture(self, key, fn, inputs):
+        static = [None if x is None else x.clone() for x in inputs]
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = fn(*static)
+        self._graphs[key] = (g, static, out)
+        while len(self._graphs) > self.max_graphs:
+            self._graphs.popitem(last=False)
+        return self._graphs[key]

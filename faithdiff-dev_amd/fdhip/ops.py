@@ -93,18 +93,32 @@ def pack_geglu(w, b):
 
 # --------------------------------------------------------------------------------------- GEMM / conv
 _probe = None
+_recorder = None
 
 
 def set_probe(records):
-    """Measurement hook (bench.py's roofline leg, never on in timed steps): while ``records`` is a list,
-    every GEMM / conv (fd_gemm), flash-attention, GroupNorm and LayerNorm launch appends
+    """Measurement hook (per-launch event probe, never on in timed steps): while ``records`` is a list, every
+    GEMM / conv (fd_gemm), flash-attention, GroupNorm and LayerNorm launch appends
     (kind, algorithmic FLOPs, algorithmic HBM bytes, start event, end event) recorded on the launch stream.
     None turns it off."""
     global _probe
     _probe = records
 
 
+def set_recorder(records):
+    """Measurement hook for bench.py's kernel-family graphs: while ``records`` is a list, every timed-kind
+    launch also appends (kind, algorithmic FLOPs, algorithmic HBM bytes, relaunch, label), where relaunch()
+    issues the identical launch again (same parameters and buffers).  Used while a whole forward is being
+    captured into a hipGraph, so the buffers are that graph's and stay allocated while it lives; bench.py then
+    captures the relaunches of ONE kind (e.g. every GEMM of the forward) into a second graph and times it with
+    HIP events.  None turns it off."""
+    global _recorder
+    _recorder = records
+
+
 def _timed(kind, flops, nbytes, launch, label=None):
+    if _recorder is not None:
+        _recorder.append((kind, float(flops), float(nbytes), launch, label))
     if _probe is None:
         launch()
         return
@@ -118,7 +132,7 @@ def _timed(kind, flops, nbytes, launch, label=None):
 def _launch_gemm(p, what):
     flops = 2.0 * p.M * p.N * p.K * max(p.batch, 1)
     label = None
-    if _probe is not None:
+    if _probe is not None or _recorder is not None:
         act = {v: k for k, v in L.ACT.items()}[p.act]
         label = (f"{'conv' if p.conv else 'gemm'} M={p.M} N={p.N} K={p.K} b={p.batch} {act}"
                  f"{' up' if p.upsample else ''}{' cat' if p.A2 else ''}{' res' if p.residual else ''}")
@@ -212,6 +226,8 @@ def gemm_e4m3(a8, a_scale, w8, out=None, bias=None, residual=None, w_scale=1.0, 
     nout = N // 2 if act == "geglu" else N
     if out is None:
         out = torch.empty((M, nout), dtype=out_dtype, device=a8.device)
+    if residual is not None and residual.dtype != out.dtype:
+        raise ValueError(f"gemm_e4m3: residual dtype {residual.dtype} != output dtype {out.dtype}")
     args = (L.ptr(a8), a8.stride(0), L.ptr(a_scale), L.ptr(w8), w8.stride(0), w_scale, L.ptr(out), out.stride(0),
             M, N, K, L.ptr(bias), L.ptr(residual), 0 if residual is None else residual.stride(0), L.ACT[act],
             L.dtype_code(out.dtype), L.stream())

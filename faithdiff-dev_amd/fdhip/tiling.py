@@ -17,6 +17,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
+from .comm import all_gather_into
 
 
 def map_tiles(specs, fn, C, device, dtype, group=None):
@@ -38,7 +39,7 @@ def map_tiles(specs, fn, C, device, dtype, group=None):
         s = specs[begin + k]
         local[k, :s[-1]].copy_(fn(*s[:-1]))
     buf = torch.empty((world * per, maxr, C), dtype=dtype, device=device)
-    dist.all_gather_into_tensor(buf, local, group=group)
+    all_gather_into(buf, local, group)
     return [buf[t, :specs[t][-1]] for t in range(n)]
 
 
@@ -79,8 +80,9 @@ def tiled_vae_decode(vae, z, h, w, group=None):
     dec = vae.decoder_hip()
     grid = [[(i, j, min(tl, h - i), min(tl, w - j)) for j in range(0, w, overlap)] for i in range(0, h, overlap)]
     specs = [(i, j, th, tw, 64 * th * tw) for row in grid for (i, j, th, tw) in row]
-    outs = map_tiles(specs, lambda i, j, th, tw: dec.decode(_crop(z, h, w, 4, i, j, th, tw), 1, th, tw), 3,
-                     z.device, z.dtype, group)
+    # decode_graphed returns the graph's static buffer: copy each tile out before the next replay
+    outs = map_tiles(specs, lambda i, j, th, tw: dec.decode_graphed(_crop(z, h, w, 4, i, j, th, tw), 1, th, tw).clone(),
+                     3, z.device, z.dtype, group)
     it = iter(outs)
     rows = [[(next(it), 8 * th, 8 * tw) for (_, _, th, tw) in row] for row in grid]
     return _assemble(rows, 3, blend, limit, 8 * h, 8 * w, z.device, z.dtype)
@@ -104,12 +106,14 @@ def _tiled_encode(encode_fn, x, H, W, C_out, ts, tl, f, group=None):
 def tiled_vae_encode(vae, x, H, W, group=None):
     """x: NHWC [H*W, 3] -> moments NHWC [(H/8)*(W/8), 8] (quant_conv output)."""
     enc = vae.encoder_hip()
-    return _tiled_encode(lambda t, th, tw: enc.encode(t, 1, th, tw), x, H, W, 8, vae.tile_sample_min_size,
+    return _tiled_encode(lambda t, th, tw: enc.encode_graphed(t, 1, th, tw).clone(), x, H, W, 8,
+                         vae.tile_sample_min_size,
                          vae.tile_latent_min_size, vae.tile_overlap_factor, group)
 
 
 def tiled_encoder_forward(encoder, x, H, W, group=None):
     """FaithDiff Encoder.tiled_encode (ext:164-190): x NHWC [H*W, 3] -> [(H/8)*(W/8), 512]."""
     enc = encoder.hip()
-    return _tiled_encode(lambda t, th, tw: enc.encode(t, 1, th, tw), x, H, W, 512, encoder.tile_sample_min_size,
+    return _tiled_encode(lambda t, th, tw: enc.encode_graphed(t, 1, th, tw).clone(), x, H, W, 512,
+                         encoder.tile_sample_min_size,
                          encoder.tile_latent_min_size, encoder.tile_overlap_factor, group)

@@ -28,6 +28,7 @@ import torch
 from . import arch
 from . import lib as L
 from . import ops
+from .graphs import GraphCache
 
 
 def _dev(t, device, dtype):
@@ -187,6 +188,7 @@ class HipUNet:
         self.kv_total = off
         self.ctx = None
         self.ncfg = None
+        self.graphs = GraphCache()
 
     # ------------------------------------------------------------------------------------------ context
     def _all_t2d(self):
@@ -329,6 +331,14 @@ class HipUNet:
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
         return self._side
+
+    def run(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True):
+        """forward() through the graph cache (fdhip/graphs.py): eager on the first call of a shape, captured on
+        the second, one hipGraph replay after that.  The result is the graph's static output buffer (valid
+        until the next run() of the same shape).  This is what the pipeline's denoise loop and bench.py call."""
+        key = ("unet", B, H, Wd, bool(add_sample), cond is None, x.dtype)
+        return self.graphs.run(key, lambda *a: self.forward(*a, B, H, Wd, add_sample=add_sample),
+                               [x, t, time_ids, text_embeds, cond])
 
     def forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True):
         """x: NHWC [B*H*W, 4] (dtype); t: fp32 [B]; time_ids fp32 [B, 6]; text_embeds fp32 [B, 1280];

@@ -14,6 +14,7 @@ import torch
 from . import arch
 from . import lib as L
 from . import ops
+from .graphs import GraphCache
 
 
 def _dev(t, device, dtype):
@@ -116,6 +117,11 @@ class HipEncoder:
         self.tile_latent_min_size = int(self.tile_sample_min_size / 8)
         self.tile_overlap_factor = 0.25
         self.use_tiling = False
+        self.graphs = GraphCache()
+
+    def encode_graphed(self, x, n, H, W):
+        """encode() through the graph cache (fdhip/graphs.py); returns the graph's static output."""
+        return self.graphs.run(("enc", n, H, W, x.dtype), lambda x_: self.encode(x_, n, H, W), [x])
 
     def encode(self, x, n, H, W):
         """x: NHWC [n*H*W, 3] (dtype) in [-1, 1].  Returns NHWC [n*(H/8)*(W/8), 8 or 512]."""
@@ -156,6 +162,11 @@ class HipDecoder:
             prev = c
         self.norm_out = (t.f32("decoder.conv_norm_out.weight"), t.f32("decoder.conv_norm_out.bias"))
         self.conv_out = t.conv("decoder.conv_out")
+        self.graphs = GraphCache()
+
+    def decode_graphed(self, z, n, h, w):
+        """decode() through the graph cache (fdhip/graphs.py); returns the graph's static output."""
+        return self.graphs.run(("dec", n, h, w, z.dtype), lambda z_: self.decode(z_, n, h, w), [z])
 
     def decode(self, z, n, h, w):
         """z: NHWC [n*h*w, 4] (already divided by scaling_factor).  Returns NHWC [n*8h*8w, 3] (dtype)."""

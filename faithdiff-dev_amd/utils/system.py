@@ -1,7 +1,9 @@
 """Mirror of utils/system.py: torch_gc and quantize_8bit (fp8 e4m3 weight storage).
 
-quantize_8bit(unet) marks the HIP UNet to store its GEMM/conv weights as OCP float8_e4m3fn (native on
-gfx950), unscaled like the reference (utils/system.py:20); the denoise encoder stays fp16 (:24-26).
+quantize_8bit(unet) rounds every UNet weight to unscaled OCP float8_e4m3fn like the reference
+(utils/system.py:20) and keeps 16-bit compute on those values (the reference's autocast arithmetic);
+fp8_mfma=True opts in to the gfx950 e4m3 MFMA for the transformer Linears.  The denoise encoder stays fp16
+(:24-26).
 """
 import gc
 
@@ -14,8 +16,8 @@ def torch_gc():
         torch.cuda.empty_cache()
 
 
-def quantize_8bit(unet):
+def quantize_8bit(unet, fp8_mfma=None):
     if unet is None:
         return
-    unet.quantize_8bit()
+    unet.quantize_8bit(fp8_mfma=fp8_mfma)
     torch_gc()

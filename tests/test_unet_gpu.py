@@ -1,8 +1,9 @@
 """Full UNet forward (HIP bf16) vs the fp32 CPU oracle on identical seeded random-init weights.
 
 Tolerance: bf16 storage of every activation through ~1000 fused ops gives a relative L2 error of a
-few 1e-3 per layer that does not compound much (residual stream); the bar is rel-L2 <= 3e-2 and
-cosine >= 0.999 on eps at C2's tile shape (B=2, 128x128 latent), and the same at a ragged tile.
+few 1e-3 per layer that does not compound much (residual stream).  Measured rel-L2 8.3e-3 .. 8.7e-3 and
+cosine 0.99996 (round 1); the bar is about 2x that: rel-L2 <= 1.5e-2 and cosine >= 0.9999 on eps, at C2's tile
+shape (B=2, 128x128 latent), a small tile and a ragged two-tile batch.
 """
 import pytest
 import torch
@@ -74,7 +75,7 @@ def test_unet_forward_matches_oracle(h, w, ntiles, t):
     exp = run_ref(ref, B, x, cond, ctx, text, tids, t)
     rel, cos = metrics(out, exp)
     print(f"unet {h}x{w} tiles={ntiles}: rel_l2={rel:.3e} cos={cos:.6f} |eps|={exp.norm().item():.3e}")
-    assert rel < 3e-2 and cos > 0.999
+    assert rel < 1.5e-2 and cos > 0.9999
 
 
 def test_unet_cfg_rows_and_tile_batching_consistent():
@@ -91,7 +92,8 @@ def test_unet_cfg_rows_and_tile_batching_consistent():
 def test_unet_fp8_weights_match_oracle():
     """quantize_8bit / use_fp8 (utils/system.py:13-32): every UNet parameter rounded to unscaled
     float8_e4m3fn, compute at 16 bit.  The HIP UNet (bf16 compute on the e4m3 values) against the fp32 oracle
-    on the same e4m3-rounded weights: same bar as the bf16 model (rel-L2 <= 3e-2, cos >= 0.999).  The e4m3
+    on the same e4m3-rounded weights: same bar as the bf16 model (rel-L2 <= 1.5e-2, cos >= 0.9999; measured
+    7.5e-3).  This is the default use_fp8 arithmetic (quantize_8bit without fp8_mfma).  The e4m3
     rounding itself (fp8 model vs bf16 model) is reported, not bounded: it is the reference's own choice."""
     from fdhip import arch
     from fdhip.unet import HipUNet
@@ -111,4 +113,4 @@ def test_unet_fp8_weights_match_oracle():
     out16 = run_hip(hip16, B, x, cond, ctx, text, tids, 951.0, h, w)
     q_rel, _ = metrics(out, out16)
     print(f"unet fp8-weights {h}x{w}: rel_l2 vs oracle={rel:.3e} cos={cos:.6f}; e4m3 vs bf16 weights rel={q_rel:.3e}")
-    assert rel < 3e-2 and cos > 0.999
+    assert rel < 1.5e-2 and cos > 0.9999
