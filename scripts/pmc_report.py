@@ -1,14 +1,14 @@
 #!/usr/bin/env python3
 """Summarise the rocprofv3 passes of scripts/r02_prof.sh over one scripts/pmc_work.py workload.
 
-Input: gpurun_out/pmc_<what>/{trace,FETCH_SIZE,WRITE_SIZE,sq1,sq2,...}/**.csv + meta.json.  The measured window
+Input: <dir>/{trace,FETCH_SIZE,WRITE_SIZE,sq1,sq2,...}/**.csv + meta.json (dir default gpurun_out/pmc_<what>).  The measured window
 is the dispatches between the last two fd_postprocess_u8 markers; the calibration copy sits between the two
 before.  Per kernel family: launches, summed durations from the trace-only pass (profiled PMC passes run slower,
 so durations never come from them), HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB; gfx950 FETCH_SIZE counts half
 of a 16-B/lane streaming read, MI355X_MICROARCH.md HBM section; the calibration copy's measured bytes/count is
 recorded beside it), achieved GB/s and TFLOP/s, and every SQ counter summed over the family's dispatches, with
 MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMD x 256 CU x GRBM_GUI_ACTIVE / 8 XCD).
-Usage: pmc_report.py <what> <out.json>"""
+Usage: pmc_report.py <what> <out.json> [dir]"""
 import csv
 import glob
 import json
@@ -57,8 +57,8 @@ def load_counters(d):
     return [(per[k][0], dict(per[k][1])) for k in sorted(per)]
 
 
-def main(what, out_path):
-    base = os.path.join(ROOT, "gpurun_out", f"pmc_{what}")
+def main(what, out_path, base=None):
+    base = base or os.path.join(ROOT, "gpurun_out", f"pmc_{what}")
     meta = json.load(open(os.path.join(base, "meta.json")))
     tr = load_trace(os.path.join(base, "trace"))
     (c0, c1), (w0, w1) = window([n for n, _ in tr])
@@ -115,4 +115,4 @@ def main(what, out_path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])

@@ -4,7 +4,7 @@
 launches of one C2 forward.  Each is preceded by a calibration copy of known size (1 GiB -> 1 GiB, larger than
 the Infinity Cache); fd_postprocess_u8 launches (never part of the workloads) mark the windows: [m1, m2) = the
 copy, [m2, m3) = the measured workload.  The workload runs once eagerly first (warm caches and workspaces, same
-kernels as the graph replays).  Writes gpurun_out/pmc_<what>/meta.json (launch / FLOP / algorithmic-byte counts
+kernels as the graph replays).  Writes /tmp/fdprof/pmc_<what>/meta.json (launch / FLOP / algorithmic-byte counts
 per kernel family).  Run under rocprofv3 with ONE counter group per pass and no trace domains besides
 --kernel-trace (scripts/r02_prof.sh)."""
 import argparse
@@ -99,7 +99,7 @@ def main():
     fn()  # the measured pass
     ops.postprocess_u8(mk_in, mk_out)
     torch.cuda.synchronize()
-    out = os.path.join(ROOT, "gpurun_out", f"pmc_{a.what}")
+    out = os.environ.get("FD_PMC_DIR") or os.path.join("/tmp/fdprof", f"pmc_{a.what}")
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, "meta.json"), "w") as f:
         json.dump({"workload": name, "families": {k: {"launches": v[0], "flops": v[1], "algorithmic_bytes": v[2]}

@@ -27,7 +27,7 @@ for step in "$@"; do
     bench_quick) run bench_quick 600 python bench.py --no-cpu-baseline --no-c3 ;;
     bench_c3) run bench_c3 600 python bench.py --workload c3 --no-cpu-baseline ;;
     bench_fp8) run bench_fp8 600 python bench.py --fp8 --no-cpu-baseline --no-c3 --no-pipeline ;;
-    prof) run prof 600 bash -c 'cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d $0/gpurun_out/prof -o run -- python3 $0/bench.py --no-cpu-baseline --no-c3 --no-pipeline --steps 20 > $0/gpurun_out/prof_bench.log 2>&1 && python3 $0/scripts/prof_window.py $(find $0/gpurun_out/prof -name "*kernel_trace.csv" | head -1) 3 > $0/gpurun_out/prof_window.txt && python3 $0/scripts/roofline_check.py $(find $0/gpurun_out/prof -name "*kernel_trace.csv" | head -1) $0/gpurun_out/prof_bench.log > $0/gpurun_out/prof_roofline_check.json' "$(pwd)" ;;
+    prof) run prof 600 bash scripts/r02_trace.sh ;;
     pmc_unet) run pmc_unet 700 bash scripts/r02_prof.sh unet r02_unet_pmc ;;
     pmc_vae) run pmc_vae 700 bash scripts/r02_prof.sh vae r02_vae_pmc ;;
     pmc_attn) run pmc_attn 700 bash scripts/r02_prof.sh attn r02_attn_pmc ;;
