@@ -70,6 +70,7 @@ def main(what, out_path, base=None):
     res = {"workload": meta["workload"], "window_us": sum(us for _, us in tr[w0:w1]),
            "calibration_copy_us": sum(us for _, us in tr[c0:c1])}
     calib = {}
+    seen = set()
     for p in sorted(os.listdir(base)):
         d = os.path.join(base, p)
         if p == "trace" or not os.path.isdir(d):
@@ -78,12 +79,27 @@ def main(what, out_path, base=None):
         if cs is None:
             continue
         (a0, a1), (b0, b1) = window([n for n, _ in cs])
+        # a counter collected in several passes (GRBM_GUI_ACTIVE rides along with each SQ group) is taken
+        # from the first pass only; the same pass's own kernel trace gives the durations its clock refers to
+        pass_names = set(k for _, vals in cs for k in vals)
+        fresh = pass_names - seen
+        seen |= pass_names
+        ptr = load_trace(d)
+        (_, _), (pw0, pw1) = window([n for n, _ in ptr])
+        pdur = defaultdict(float)
+        for n, us in ptr[pw0:pw1]:
+            pdur[family(n)] += us
         for n, vals in cs[b0:b1]:
             for k, v in vals.items():
-                fams[family(n)]["counters"][k] += v
+                if k in fresh:
+                    fams[family(n)]["counters"][k] += v
+        if "GRBM_GUI_ACTIVE" in fresh:
+            for fn_, us in pdur.items():
+                fams[fn_]["grbm_pass_us"] = us
         for n, vals in cs[a0:a1]:
             for k, v in vals.items():
-                calib[k] = calib.get(k, 0.0) + v
+                if k in fresh:
+                    calib[k] = calib.get(k, 0.0) + v
     out = {}
     for name, f in sorted(fams.items(), key=lambda x: -x[1]["us"]):
         c = f["counters"]
@@ -100,10 +116,19 @@ def main(what, out_path, base=None):
             e.update(hbm_read_bytes=rd, hbm_write_bytes=wr, hbm_gbs=round((rd + wr) / (f["us"] / 1e6) / 1e9, 1))
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c and c["GRBM_GUI_ACTIVE"]:
             e["mfma_busy"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * 256 * c["GRBM_GUI_ACTIVE"] / 8), 4)
-            e["effective_clock_ghz_profiled"] = round(c["GRBM_GUI_ACTIVE"] / 8 / (f["us"] * 1e3), 3)
+            if f.get("grbm_pass_us"):
+                e["effective_clock_ghz_profiled"] = round(c["GRBM_GUI_ACTIVE"] / 8 / (f["grbm_pass_us"] * 1e3), 3)
         e["counters"] = {k: v for k, v in sorted(c.items())}
         out[name] = e
     res["families"] = out
+    # per-launch table of the timed kinds, in launch order (labels recorded by pmc_work.py)
+    labs = [x for x in meta.get("labels", []) if x[0] in ("gemm", "gemm_e4m3", "flash_attn", "group_norm")]
+    timed = [(n, us) for n, us in tr[w0:w1] if family(n) in ("gemm", "gemm_e4m3", "flash_attn", "group_norm")
+             and "gn_partial" not in n and "gn_finalize" not in n]
+    if labs and len(labs) == len(timed):
+        res["launches"] = [{"kind": k, "label": lab, "us": round(us, 2),
+                            "tflops": round(fl / (us / 1e6) / 1e12, 1) if fl else None}
+                           for (k, lab, fl), (n, us) in zip(labs, timed)]
     if "FETCH_SIZE" in calib:
         res["calibration"] = {"bytes_read": meta["calib_bytes_read"], "bytes_written": meta["calib_bytes_written"],
                               "fetch_kib_x2": 2 * calib["FETCH_SIZE"] * 1024 if "FETCH_SIZE" in calib else None,

@@ -82,6 +82,7 @@ def main():
     ops.set_recorder(None)
     torch.cuda.synchronize()
     fam = {}
+    labels = [(kind, lab, fl) for kind, fl, nb, _, lab in rec]
     for kind, fl, nb, *_ in rec:
         c = fam.setdefault(kind, [0, 0.0, 0.0])
         c[0] += 1
@@ -104,7 +105,8 @@ def main():
     with open(os.path.join(out, "meta.json"), "w") as f:
         json.dump({"workload": name, "families": {k: {"launches": v[0], "flops": v[1], "algorithmic_bytes": v[2]}
                                                   for k, v in fam.items()},
-                   "calib_bytes_read": rows * cols * 2, "calib_bytes_written": rows * cols * 2}, f, indent=1)
+                   "calib_bytes_read": rows * cols * 2, "calib_bytes_written": rows * cols * 2,
+                   "labels": labels}, f, indent=1)
     print("ok", name, {k: v[0] for k, v in fam.items()})
 
 
