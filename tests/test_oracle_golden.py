@@ -71,3 +71,44 @@ def test_condition_embedding(golden):
     with torch.no_grad():
         out = cne(det_tensor((1, 512, 8, 8), 31)).numpy()
     np.testing.assert_allclose(out, golden["cne_out"], rtol=1e-5, atol=1e-5)
+
+
+class _OracleUNet:
+    """oracle/pipeline.py's UNet call signature over the shared stand-in (tests/golden/_det.py)."""
+
+    def __call__(self, x, t, ctx, added, input_embedding=None, add_sample=True):
+        from _det import standin_eps
+        return standin_eps(x, t, ctx, added["text_embeds"], added["time_ids"], input_embedding)
+
+
+class _OracleVAE:
+    scaling_factor = 0.13025
+
+    def encode_sample(self, x, eps):
+        from _det import standin_moments
+        mean, logvar = standin_moments(x).chunk(2, dim=1)
+        return mean + torch.exp(0.5 * logvar.clamp(-30.0, 20.0)) * eps
+
+    def decode(self, z):
+        from _det import standin_decode
+        return standin_decode(z)
+
+
+def test_pipeline_orchestration_matches_reference_call():
+    """oracle/pipeline.py:run_pipeline against the reference's own FaithDiffStableDiffusionXLPipeline.__call__
+    (pipeline_FaithDiff_tlc.py:1187-1459, run by tests/golden/make_call_golden.py) with the same stand-in models:
+    CFG order, per-tile add_time_ids, per-tile scheduler state, rescale_noise_cfg, 'lr' / 'noise' start, TLC blend
+    and decode scaling, at a multi-tile, a ragged and a clamped-tile size."""
+    import os
+
+    from _det import call_cases, call_inputs, standin_features
+    from oracle.pipeline import run_pipeline
+    gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "call_golden.npz"))
+    for k, (name, H, W, target, steps, g, rescale, start) in enumerate(call_cases()):
+        img, pe, npe, ppe, nppe, noise, post = call_inputs(H, W, 500 + 10 * k)
+        res = run_pipeline(_OracleUNet(), _OracleVAE(), standin_features, img, pe, npe, ppe, nppe, noise, post,
+                           num_inference_steps=steps, guidance_scale=g, overlap=0.5, target_size=target,
+                           original_size=(H, W), start_point=start, guidance_rescale=rescale)
+        np.testing.assert_allclose(res["latents"].numpy(), gold[f"{name}_latents"], rtol=2e-5, atol=2e-5,
+                                   err_msg=name)
+        np.testing.assert_allclose(res["image"].numpy(), gold[f"{name}_image"], rtol=2e-5, atol=2e-5, err_msg=name)
