@@ -112,3 +112,23 @@ def test_pipeline_orchestration_matches_reference_call():
         np.testing.assert_allclose(res["latents"].numpy(), gold[f"{name}_latents"], rtol=2e-5, atol=2e-5,
                                    err_msg=name)
         np.testing.assert_allclose(res["image"].numpy(), gold[f"{name}_image"], rtol=2e-5, atol=2e-5, err_msg=name)
+
+
+def test_denoise_encoder_tiling_matches_reference(golden):
+    """oracle DenoiseEncoder.blend_v / blend_h / tiled_encode / forward against the reference's Encoder methods
+    (ext:150-196), both run on the same stand-in trunk: tile grid, in-place blend order, crop."""
+    import types
+
+    from _det import standin_features
+    from oracle.vae import DenoiseEncoder
+    for name, (H, W, ts, ov) in {"a": (160, 136, 64, 0.25), "b": (200, 96, 96, 0.25)}.items():
+        ns = types.SimpleNamespace(tile_sample_min_size=ts, tile_latent_min_size=ts // 8, tile_overlap_factor=ov,
+                                   use_tiling=True, encode=standin_features, blend_v=DenoiseEncoder.blend_v,
+                                   blend_h=DenoiseEncoder.blend_h)
+        ns.tiled_encode = types.MethodType(DenoiseEncoder.tiled_encode, ns)
+        x = det_tensor((1, 3, H, W), 4000 + H + W, 0.7)
+        np.testing.assert_array_equal(DenoiseEncoder.forward(ns, x).numpy(), golden[f"enc_tiled_{name}"])
+    av, bv = det_tensor((1, 8, 12, 11), 4100), det_tensor((1, 8, 9, 11), 4101)
+    np.testing.assert_array_equal(DenoiseEncoder.blend_v(av, bv.clone(), 5).numpy(), golden["enc_blend_v"])
+    ah, bh = det_tensor((1, 8, 9, 10), 4102), det_tensor((1, 8, 9, 11), 4103)
+    np.testing.assert_array_equal(DenoiseEncoder.blend_h(ah, bh.clone(), 4).numpy(), golden["enc_blend_h"])
