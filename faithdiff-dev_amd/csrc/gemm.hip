@@ -170,6 +170,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   }
   // upsample: the conv runs on a nearest-resized (Hout x Wout) image; exact x2 or diffusers' upsample_size
   const int Hl = p.upsample ? p.Hout : p.Hin, Wl = p.upsample ? p.Wout : p.Win;
+  const bool up2 = p.upsample && Hl == 2 * p.Hin && Wl == 2 * p.Win;
   const int C1 = p.C1 > 0 ? p.C1 : p.Cin;
   const T* __restrict__ A2 = (const T*)p.A2;
 
@@ -186,7 +187,18 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
       for (int i = 0; i < A_INSTR; ++i) {
         const int iy = a_iy0[i] + ky, ix = a_ix0[i] + kx;
         const bool ok = a_ok[i] && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
-        const int py = p.upsample ? (iy * p.Hin) / Hl : iy, px = p.upsample ? (ix * p.Win) / Wl : ix;
+        // exact x2 (every Upsample2D except diffusers' odd-size upsample_size path): a shift, not a VALU
+        // integer division per lane and load (the two divisions cost ~60 VALU instructions per A load)
+        int py = iy, px = ix;
+        if (p.upsample) {
+          if (up2) {
+            py = iy >> 1;
+            px = ix >> 1;
+          } else {
+            py = (iy * p.Hin) / Hl;
+            px = (ix * p.Win) / Wl;
+          }
+        }
         const long long pix = a_pix[i] + (long long)py * p.Win + px;
         const T* src = second ? (A2 + pix * (p.Cin - C1) + (c0 - C1) + a_chunk[i] * 8)
                               : (A + pix * p.lda + c0 + a_chunk[i] * 8);

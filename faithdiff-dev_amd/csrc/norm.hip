@@ -10,12 +10,15 @@
 #define GN_MAXC 2560
 
 static inline int gn_rows_per_chunk(int nimg, int HW) {
-  // 256 chunks per image at most, chosen from HW alone: the per-(image, group) reduction order -- and so
+  // chunk count chosen from HW alone: the per-(image, group) reduction order -- and so
   // every bit of the result -- does not depend on how many images share the launch (tile batching, CFG
   // rows, tile-parallel sharding all give identical outputs).  512+ blocks at the UNet's B >= 2.
+  // Large images (the VAE at 512^2 / 1024^2: HW up to 1M rows) get up to 1024 chunks of >= 64 rows: 256 chunks
+  // of 4096 rows left one 4-wave block per CU, latency-bound at ~4 TB/s.
   (void)nimg;
+  const int target = HW / 64 > 1024 ? 1024 : (HW / 64 < 256 ? 256 : HW / 64);
   int r = 1;
-  while ((HW + r - 1) / r > 256) r *= 2;
+  while ((HW + r - 1) / r > target) r *= 2;
   return r;
 }
 
