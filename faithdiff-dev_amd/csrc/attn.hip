@@ -357,6 +357,198 @@ extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const 
 }
 
 // ------------------------------------------------------------------------------------------------
+// flash_attn_d512: single-head d = 512 attention of the VAE mid block (diffusers Attention with one head of 512
+// channels and upcast softmax; pipeline_FaithDiff_tlc.py:1436-1442 decodes through it, T = 16384 at 1024^2) --
+// the [T, T] score and probability matrices (1.5 GB at T = 16384) are never formed.  One workgroup = 4 waves x
+// 16 queries; K / V tiles of 32 keys x 512 (32 KB each) double-buffered in LDS by global_load_lds (128 KB: one
+// workgroup per CU, one wave per SIMD, 512 VGPRs).  Per tile and wave: S^T = K Q^T (32 MFMAs, Q fragments held
+// in 64 VGPRs), online softmax in fp32 (one query per lane column, as flash_attn_d64), O^T += V^T P^T (32 MFMAs,
+// O^T in 128 VGPRs, V^T fragments by ds_read_b64_tr_b16), denominators on the MFMA pipe (ones . P^T).
+// LDS rows are 1024 B, so both tiles are XOR-swizzled at the source (K: 16-B chunk ^ (row & 15) for the 16-row
+// ds_read_b128 fragments; V: chunk ^ 2 (row & 7) for the 8-row transposed reads) -- conflict-free reads.
+template <typename T>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) flash_attn_d512_kernel(
+    const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V, long long ld, long long bs,
+    T* __restrict__ O, long long ldo, long long obs, int L, float scale_log2) {
+  typedef typename VecT<T>::v8 V8;
+  constexpr int KT = 32;            // keys per tile
+  constexpr int TB = KT * 1024;     // bytes of one K (or V) tile in LDS
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[4 * TB];  // [buf][K | V]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nq = (L + 63) / 64;
+  const int qblk = blockIdx.x % nq, b = blockIdx.x / nq;
+  const T* Qb = Q + (long long)b * bs;
+  const T* Kb = K + (long long)b * bs;
+  const T* Vb = V + (long long)b * bs;
+  const int q0 = qblk * 64 + wave * 16;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  V8 qf[16];  // B operand: Q[q0 + fr][32 ds + 8 fg .. +7]
+  {
+    const int q = min(q0 + fr, L - 1);
+#pragma unroll
+    for (int ds = 0; ds < 16; ++ds) qf[ds] = *(const V8*)(Qb + (long long)q * ld + ds * 32 + fg * 8);
+  }
+  // DMA: wave w stages K / V rows r = w + 4 i (i < 8); lane l fills LDS chunk l of the row with source chunk
+  // l ^ swz(r) (the swizzle is an involution on 0..63)
+  unsigned koff[8], voff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = wave + 4 * i;
+    koff[i] = (unsigned)((r * ld + ((lane ^ (r & 15)) * 8)) * sizeof(T));
+    voff[i] = (unsigned)((r * ld + ((lane ^ (2 * (r & 7))) * 8)) * sizeof(T));
+  }
+  const int nt = (L + KT - 1) / KT;
+  auto stage = [&](int t, int bi) {
+    unsigned char* sk = smem + bi * 2 * TB;
+    unsigned char* sv = sk + TB;
+    if (t * KT + KT <= L) {
+      const char* kt = (const char*)(Kb + (long long)t * KT * ld);
+      const char* vt = (const char*)(Vb + (long long)t * KT * ld);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_global_load_lds((const void*)(kt + koff[i]), LDS_PTR(sk + (wave + 4 * i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(vt + voff[i]), LDS_PTR(sv + (wave + 4 * i) * 1024), 16, 0, 0);
+      }
+    } else {  // ragged last tile: rows past L re-read key L-1 (scored -inf)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = wave + 4 * i;
+        const long long key = min(t * KT + r, L - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(Kb + key * ld + (lane ^ (r & 15)) * 8),
+                                         LDS_PTR(sk + r * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(Vb + key * ld + (lane ^ (2 * (r & 7))) * 8),
+                                         LDS_PTR(sv + r * 1024), 16, 0, 0);
+      }
+    }
+  };
+  // lane-constant LDS read offsets.  K fragment (kb, ds): row kb*16 + fr, chunk (4 ds + fg) ^ fr =
+  //   16 (ds >> 2) + 4 ((ds & 3) ^ (fr >> 2)) + (fg ^ (fr & 3))  ->  base kro[ds & 3] + 256 (ds >> 2) + 16384 kb.
+  // V^T (db = 8 dg + j, lo / hi): row r0 = 4 fg + (fr >> 2) (+16), element column 16 db + 4 (fr & 3):
+  //   chunk 2 (db ^ (r0 & 7)) + ((fr & 3) >> 1), +8 B for odd (fr & 3)  ->  base vro[j] + 256 dg (+16384 hi).
+  int kro[4], vro[8];
+#pragma unroll
+  for (int d4 = 0; d4 < 4; ++d4) kro[d4] = fr * 1024 + 16 * (4 * (d4 ^ (fr >> 2)) + (fg ^ (fr & 3)));
+  {
+    const int r0 = 4 * fg + (fr >> 2), pp = fr & 3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vro[j] = r0 * 1024 + 32 * (j ^ (r0 & 7)) + 16 * (pp >> 1) + 8 * (pp & 1);
+  }
+
+  f32x4 o[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  f32x4 lsum = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float mrow = -INFINITY;
+  V8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (T)1.0f;
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = 0; t < nt; ++t) {
+    const int bi = t & 1;
+    if (t + 1 < nt) stage(t + 1, bi ^ 1);  // buffer bi^1 held tile t-1: every wave passed the barrier after it
+    const unsigned char* sk = smem + bi * 2 * TB;
+    f32x4 sc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ds = 0; ds < 16; ++ds) {
+        const V8 kf = *(const V8*)(sk + kro[ds & 3] + 256 * (ds >> 2) + 16384 * kb);
+        sc[kb] = mfma16x16x32(kf, qf[ds], sc[kb]);
+      }
+    if (t * KT + KT > L) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (t * KT + kb * 16 + fg * 4 + i >= L) sc[kb][i] = -INFINITY;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[kb][i]);
+    mx = xor_max_16_32(mx);
+    const float mnew = fmaxf(mrow, mx * scale_log2);
+    V8 pf;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pf[kb * 4 + i] = (T)__builtin_amdgcn_exp2f(fmaf(sc[kb][i], scale_log2, -mnew));
+    if (__any(mnew != mrow)) {  // exact skip when no query of this wave raised its running max
+      const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
+      lsum *= alpha;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) o[i] *= alpha;
+    }
+    mrow = mnew;
+    // O^T += V^T P^T in four groups of 8 d-blocks (transposed V reads by inline asm: the builtin makes hipcc
+    // drain vmcnt(0) -- the next tile's DMA -- in front of it)
+    const unsigned vb = (unsigned)(unsigned long)LDS_PTR(smem + bi * 2 * TB + TB);
+#pragma unroll
+    for (int dg = 0; dg < 4; ++dg) {
+      s16x4 vtr[8][2];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[j][0]) : "v"(vb + vro[j]), "i"(256 * dg));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[j][1]) : "v"(vb + vro[j]),
+                     "i"(256 * dg + 16384));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        typedef __attribute__((ext_vector_type(8))) short s16x8;
+        const s16x4 lo = vtr[j][0], hi = vtr[j][1];
+        const s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[dg * 8 + j] = mfma16x16x32(__builtin_bit_cast(V8, w), pf, o[dg * 8 + j]);
+      }
+    }
+    lsum = mfma16x16x32(ones, pf, lsum);
+    if (t + 1 < nt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 landed
+      __builtin_amdgcn_s_waitcnt(0xc07f);                // this wave's reads of tile t retired
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  // lane holds O^T[d = 16 db + 4 fg + j][q = q0 + fr]
+  const int q = q0 + fr;
+  if (q < L) {
+    const float inv = 1.0f / lsum[0];
+    T* orow = O + (long long)b * obs + (long long)q * ldo;
+    typedef __attribute__((ext_vector_type(4))) T T4;
+#pragma unroll
+    for (int db = 0; db < 32; ++db) {
+      T4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = (T)(o[db][j] * inv);
+      *(T4*)(orow + db * 16 + fg * 4) = w;
+    }
+  }
+}
+
+extern "C" int fd_flash_attn_d512(const void* q, const void* k, const void* v, long long ld, long long bs, void* o,
+                                  long long ldo, long long obs, int batch, int L, float scale, int dtype,
+                                  void* stream) {
+  if (!q || !k || !v || !o) return FD_ERR_ARG;
+  if (batch <= 0 || L <= 0 || (long long)batch * ((L + 63) / 64) > 0x7fffffff) return FD_ERR_SHAPE;
+  if ((ld & 7) || (ldo & 3) || ld < 512 || ldo < 512 || (bs & 7) || (obs & 3)) return FD_ERR_SHAPE;
+  if (32LL * ld * 2 > 0xffffffffLL) return FD_ERR_SHAPE;  // 32-bit DMA row offsets
+  if ((((unsigned long long)q) | ((unsigned long long)k) | ((unsigned long long)v)) & 15) return FD_ERR_ARG;
+  if (((unsigned long long)o) & 7) return FD_ERR_ARG;
+  dim3 grid((unsigned)(batch * ((L + 63) / 64))), block(256);
+  const float sl2 = scale * 1.4426950408889634f;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d512_kernel<T>), grid, block, 0, (hipStream_t)stream,
+                                          (const T*)q, (const T*)k, (const T*)v, ld, bs, (T*)o, ldo, obs, L, sl2));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
 // MultiheadAttention over the sequence axis L (the CFG pair) for every pixel n, grouped: rows
 // [g*L, (g+1)*L) of the batch form one attention problem.  qkv [Btot][N][3E] -> o [Btot][N][E].
 // One thread per (group, pixel, head) computes all L query rows; the heads of a pixel are adjacent

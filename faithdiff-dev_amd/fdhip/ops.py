@@ -340,6 +340,16 @@ def flash_attn(q, k, v, out, batch, heads, Lq, Lk, ldq, ldk, ldv, ldo, qbs, kbs,
     return out
 
 
+def flash_attn_d512(qkv, out, nimg, T, scale=512 ** -0.5):
+    """Single-head d=512 attention on the qkv projection [nimg*T, 1536] (q | k | v) -> out [nimg*T, 512]."""
+    ld = qkv.stride(0)
+    _timed("flash_attn_d512", 4.0 * nimg * T * T * 512, 0, label=f"flash512 n={nimg} T={T}", launch=lambda: L.check(
+        L.load().fd_flash_attn_d512(L.ptr(qkv), L.ptr(qkv[:, 512:]), L.ptr(qkv[:, 1024:]), ld, T * ld, L.ptr(out),
+                                    out.stride(0), T * out.stride(0), nimg, T, scale, L.dtype_code(qkv.dtype),
+                                    L.stream()), "fd_flash_attn_d512"))
+    return out
+
+
 def embed_tokens(ids, tok, pos, out, batch, L_):
     """ids int32 [batch*L_] (device); tok [vocab, D], pos [>=L_, D] -> out [batch*L_, D]."""
     D = tok.shape[1]

@@ -5,9 +5,8 @@ resnets without temb (GN eps 1e-6), VAE Downsample2D = zero pad (0,1,0,1) + conv
 implicit-GEMM gather as pad=0 with a bottom/right zero fringe), Upsample2D = nearest x2 folded into the
 next conv's gather, mid-block single-head d=512 attention with residual.
 
-The d=512 attention runs as GEMM (S = QK^T/sqrt(512), fp32) -> fp32 row softmax -> GEMM (P V) on the MFMA
-GEMM kernel: a [T, T] fp32 score matrix is 1 GiB at T = 16384, which 288 GB of HBM3E holds without
-tiling; the two GEMMs carry the 0.55 TFLOP of the 1024^2 decode's attention.
+The d=512 mid-block attention runs as one flash kernel (fd_flash_attn_d512: online softmax in fp32, QK^T and PV on
+the MFMA, K / V tiles staged through LDS), so no [T, T] score / probability buffer (1.5 GB at T = 16384) exists.
 """
 import torch
 
@@ -67,22 +66,27 @@ def run_resnet(r, x, n, H, W, dtype, device):
 
 
 def run_attn(a, x, n, H, W):
-    """Single-head d=C attention with residual (diffusers Attention, AttnProcessor2_0)."""
+    """Single-head d=C attention with residual (diffusers Attention, AttnProcessor2_0): GroupNorm -> fused QKV
+    projection -> fd_flash_attn_d512 (no [T, T] buffers) -> out projection + residual."""
     C = a["out"][0].shape[0]
     T = H * W
     h = ops.group_norm(x, *a["gn"], n, T, C, 32, 1e-6, silu=False)
     qkv = ops.gemm(h, a["qkv"][0], bias=a["qkv"][1])  # [n*T, 3C]
     out = torch.empty((n * T, C), dtype=x.dtype, device=x.device)
-    Tp = (T + 63) // 64 * 64  # the P.V GEMM contracts over T: pad K to the kernel's 64 granule with zeros
-    S = torch.empty((T, T), dtype=torch.float32, device=x.device)
-    P = torch.zeros((T, Tp), dtype=x.dtype, device=x.device)
-    Vt = torch.zeros((C, Tp), dtype=x.dtype, device=x.device)
-    for i in range(n):  # per image (the VAE runs batch 1)
-        q = qkv[i * T:(i + 1) * T]
-        ops.gemm(q, q[:, C:], out=S, M=T, N=T, K=C, lda=3 * C, ldw=3 * C, alpha=C ** -0.5, out_dtype=torch.float32)
-        ops.softmax_rows(S, P, T, T, 1.0, ldp=Tp)
-        ops.transpose(q[:, 2 * C:], 3 * C, Vt, Tp, T, C)
-        ops.gemm(P, Vt, out=out[i * T:(i + 1) * T], K=Tp)
+    if C == 512:
+        ops.flash_attn_d512(qkv, out, n, T, C ** -0.5)
+    else:  # materialised fallback for other head widths (not used by the SDXL VAE)
+        Tp = (T + 63) // 64 * 64  # the P.V GEMM contracts over T: pad K to the kernel's 64 granule with zeros
+        S = torch.empty((T, T), dtype=torch.float32, device=x.device)
+        P = torch.zeros((T, Tp), dtype=x.dtype, device=x.device)
+        Vt = torch.zeros((C, Tp), dtype=x.dtype, device=x.device)
+        for i in range(n):
+            q = qkv[i * T:(i + 1) * T]
+            ops.gemm(q, q[:, C:], out=S, M=T, N=T, K=C, lda=3 * C, ldw=3 * C, alpha=C ** -0.5,
+                     out_dtype=torch.float32)
+            ops.softmax_rows(S, P, T, T, 1.0, ldp=Tp)
+            ops.transpose(q[:, 2 * C:], 3 * C, Vt, Tp, T, C)
+            ops.gemm(P, Vt, out=out[i * T:(i + 1) * T], K=Tp)
     return ops.gemm(out, a["out"][0], bias=a["out"][1], residual=x)
 
 

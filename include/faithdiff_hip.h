@@ -169,8 +169,16 @@ int fd_flash_attn(const void* q, long long ldq, long long q_bstride, const void*
  * (FaithDiff's 640 / 8); exact for distinct rows. */
 int fd_mha_seq_axis(const void* qkv, void* o, int L, int groups, int N, int E, int heads, int dtype, void* stream);
 
+/* Single-head flash attention with head_dim 512 (the VAE mid-block Attention: diffusers Attention with one head
+ * of 512 channels, upcast softmax -- AutoencoderKL decode, pipeline_FaithDiff_tlc.py:1436-1442, and the VAE /
+ * FaithDiff denoise encoders, ext:39-196).  q/k/v: token rows of length >= 512 with row stride ld (elements; the
+ * qkv projection output [L][1536] gives q, k = q + 512, v = q + 1024), batch stride bs; o: [L][ldo] rows, batch
+ * stride obs.  L may be any size (masked tail).  No [L, L] buffer is formed.  16-B aligned q/k/v, ld % 8 == 0. */
+int fd_flash_attn_d512(const void* q, const void* k, const void* v, long long ld, long long bs, void* o,
+                       long long ldo, long long obs, int batch, int L, float scale, int dtype, void* stream);
+
 /* Row softmax of fp32 scores s[R][C] (scaled by `scale`) into p[R][ldp] (dtype).  With fd_gemm this forms
- * the single-head d=512 VAE mid-block attention (diffusers Attention, 1 head, upcast softmax). */
+ * a materialised single-head attention (kept for head dims other than 512; the VAE uses fd_flash_attn_d512). */
 int fd_softmax_rows(const float* s, void* p, int R, int C, long long ldp, float scale, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

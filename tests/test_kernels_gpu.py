@@ -324,3 +324,20 @@ def test_tlc_grids_nhwc():
         r, c = rows[tid // 2].item(), cols[tid % 2].item()
         assert torch.equal(out[2 * t], cv[r:r + k, c:c + k])
         assert torch.equal(out[2 * t + 1], cv[r:r + k, c:c + k])
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("n,T", [(1, 4096), (2, 1000), (1, 77), (1, 16384)])
+def test_flash_attn_d512(dtype, n, T):
+    """fd_flash_attn_d512 (the VAE mid-block attention, one head of 512 channels) against fp32 SDPA on the same
+    qkv projection rows [q | k | v] (ld 1536), incl. ragged tails (T = 1000, 77) and the 1024^2 size (16384)."""
+    from fdhip import ops
+    C = 512
+    scale = 1.0 if T > 4096 else 2.0  # score spread: keep the softmax peaked enough to be a real test
+    qkv = (rnd(n, T, 3 * C, dtype=torch.float32) * scale).to(dtype)
+    o = torch.empty(n * T, C, dtype=dtype, device=DEV)
+    ops.flash_attn_d512(qkv.view(n * T, 3 * C), o, n, T)
+    x = qkv.float()
+    q, k, v = x[..., :C], x[..., C:2 * C], x[..., 2 * C:]
+    ref = F.scaled_dot_product_attention(q[:, None], k[:, None], v[:, None])[:, 0].reshape(n * T, C)
+    assert rel_l2(o, ref) < 1.5 * TOL[dtype], rel_l2(o, ref)
