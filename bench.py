@@ -107,13 +107,21 @@ def maybe_launch(args, argv):
 
 
 def setup_dist():
+    """One rank per GPU over RCCL ('nccl').  FD_BENCH_REHEARSAL=1 (tests on a one-GPU box only) puts every rank
+    on cuda:0 with gloo, to exercise the N-rank code path where N GPUs are not available."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    rehearsal = os.environ.get("FD_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
@@ -125,6 +133,8 @@ def barrier(world):
 
 
 def max_over_ranks(x, world, dev):
+    if world > 1 and dist.get_backend() == "gloo":
+        dev = torch.device("cpu")
     t = torch.tensor([float(x)], device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

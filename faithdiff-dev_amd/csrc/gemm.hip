@@ -607,7 +607,8 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
   }
 }
 
-extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream);  // gemm8.hip
+extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream);    // gemm8.hip
+extern "C" int fd_gemm256_try(const fd_gemm_params* p, void* stream);  // gemm256.hip
 
 extern "C" int fd_gemm(const fd_gemm_params* p, void* stream) {
   if (!p || !p->A || !p->B || !p->C) return FD_ERR_ARG;
@@ -625,6 +626,9 @@ extern "C" int fd_gemm(const fd_gemm_params* p, void* stream) {
     return FD_ERR_SHAPE;
   if (p->ln_in && (p->K % 320 || p->K > 1280 || p->batch > 1 || p->conv || !p->ln_c)) return FD_ERR_SHAPE;
   if (!p->ln_out) {
+    const int r256 = fd_gemm256_try(p, stream);  // large-M, N % 256 == 0: 256 x 256 tiles
+    if (r256 < 0) return r256;
+    if (r256 == 1) return FD_OK;
     const int r8 = fd_gemm8_try(p, stream);
     if (r8 < 0) return r8;
     if (r8 == 1) return FD_OK;
