@@ -22,6 +22,12 @@
 
 __device__ __attribute__((aligned(256))) unsigned char g_zero_page256[256];
 
+// diagnostic builds only (-DFD_G256_DIAG=m; 0 in the product): 1 = no operand loads, 2 = no LDS reads / MFMA,
+// 4 = no epilogue stores (scripts/g256_diag.sh)
+#ifndef FD_G256_DIAG
+#define FD_G256_DIAG 0
+#endif
+
 namespace {
 
 template <int N>
@@ -29,15 +35,19 @@ __device__ __forceinline__ void vm_wait256() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename T, typename TO, bool CONV>
-__global__ void __launch_bounds__(512) gemm256_kernel(const fd_gemm_params p, const int group_m) {
+template <typename T, typename TO, bool CONV, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, NW == 4 ? 1 : 2)))
+gemm256_kernel(const fd_gemm_params p, const int group_m) {
+  // NW = 8: 4 x 2 waves of 64 x 128, two waves per SIMD; NW = 4: 2 x 2 waves of 128 x 128, one wave per SIMD
+  // (a third fewer fragment bytes read from LDS per slot; 512-VGPR waves)
   typedef typename VecT<T>::v8 V8;
-  constexpr int BM = 256, BN = 256, NW = 8, NTHR = 512, WAVES_N = 2;
-  constexpr int WM = 64, WN = 128, MT = WM / 16, NT = WN / 16;
+  constexpr int BM = 256, BN = 256, NTHR = 64 * NW, WAVES_N = 2, WAVES_M = NW / WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, MT = WM / 16, NT = WN / 16;
+  constexpr int AI = 16 / NW;            // 16-row DMA blocks of A (and of B) per wave per slot
   constexpr int NSL = 5;                 // ring slots
   constexpr int SLOT = (BM + BN) * 64;   // 32 KB: 512 rows of 32 k
   constexpr int A_BYTES = BM * 64;
-  constexpr int PER = 4;                 // LDS-DMA instructions per wave per slot (2 A + 2 B, 16 rows each)
+  constexpr int PER = 2 * AI;            // LDS-DMA instructions per wave per slot (A + B, 16 rows each)
   constexpr int LDE = BN + 4;
   constexpr int EROWS = 128;
   static_assert(EROWS * LDE * 4 <= NSL * SLOT, "epilogue staging");
@@ -71,73 +81,82 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const fd_gemm_params p, co
   // source chunk (lane & 3) ^ ((row >> 2) & 3) = (lane & 3) ^ (lane >> 4)
   const int lrow = lane >> 2, chunk = (lane & 3) ^ (lane >> 4);
 
-  const T* a_row[2];
-  int a_iy0[2], a_ix0[2];
-  long long a_pix[2];
-  bool a_ok[2];
+  // A rows of this lane's DMA pieces: plain GEMM -> row pointers; conv -> the output pixel (decoded per tap)
+  const T* a_row[AI];
+  int a_m[AI];  // conv: output row, -1 past M
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < AI; ++i) {
     const int m = m0 + (w + NW * i) * 16 + lrow;
-    a_ok[i] = m < M;
     const int mm = m < M ? m : M - 1;
-    if (CONV) {
-      const int hw = p.Hout * p.Wout;
-      const int img = mm / hw;
-      const int rem = mm - img * hw;
-      const int oy = rem / p.Wout, ox = rem - (rem / p.Wout) * p.Wout;
-      a_iy0[i] = oy * p.stride - p.pad;
-      a_ix0[i] = ox * p.stride - p.pad;
-      a_pix[i] = (long long)img * p.Hin * p.Win;
-      a_row[i] = nullptr;
-    } else {
-      a_row[i] = A + (long long)mm * p.lda + chunk * 8;
-      a_iy0[i] = a_ix0[i] = 0;
-      a_pix[i] = 0;
-    }
+    a_m[i] = m < M ? m : -1;
+    a_row[i] = CONV ? nullptr : A + (long long)mm * p.lda + chunk * 8;
   }
-  const T* b_row[2];
+  int b_off[AI];  // element offsets of this lane's B rows (32-bit: fd_gemm256_try checks N * ldb < 2^31)
 #pragma unroll
-  for (int i = 0; i < 2; ++i) b_row[i] = Bw + (long long)(n0 + (w + NW * i) * 16 + lrow) * p.ldb + chunk * 8;
+  for (int i = 0; i < AI; ++i) b_off[i] = (n0 + (w + NW * i) * 16 + lrow) * p.ldb + chunk * 8;
   const int Hl = p.upsample ? p.Hout : p.Hin, Wl = p.upsample ? p.Wout : p.Win;
   const bool up2 = p.upsample && Hl == 2 * p.Hin && Wl == 2 * p.Win;
   const int C1 = p.C1 > 0 ? p.C1 : p.Cin;
 
+  constexpr int mode = FD_G256_DIAG;
+  int g_key = -1;         // conv: (tap, source) of the gather offsets below; stage() runs in slot order
+  constexpr int ZP = -0x7fffffff - 1;  // g_off sentinel: the zero page (a real offset can be negative: A2 - C1)
+  int g_off[AI];          // per DMA row: source pixel's channel-0 element offset for this tap, ZP = zero page
+#pragma unroll
+  for (int i = 0; i < AI; ++i) g_off[i] = ZP;
   auto stage = [&](int s, int buf) {  // slot s = k [32 s, 32 s + 32)
+    if (mode & 1) return;
     const int k0 = s * 32;
     unsigned char* sa = smem + buf * SLOT;
     if (CONV) {
       const int tap = k0 / p.Cin;
       const int c0 = k0 - tap * p.Cin;
-      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
       const bool second = (A2 != nullptr) && (c0 >= C1);
+      const int key = tap * 2 + (int)second;
+      if (key != g_key) {  // the im2col source rows change only with the tap (every Cin / 32 slots): uniform
+        g_key = key;
+        const int ky = tap / 3, kx = tap - (tap / 3) * 3;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int iy = a_iy0[i] + ky, ix = a_ix0[i] + kx;
-        const bool ok = a_ok[i] && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
-        int py = iy, px = ix;
-        if (p.upsample) {
-          if (up2) {
-            py = iy >> 1;
-            px = ix >> 1;
-          } else {
-            py = (iy * p.Hin) / Hl;
-            px = (ix * p.Win) / Wl;
+        for (int i = 0; i < AI; ++i) {
+          const int mm = a_m[i] < 0 ? 0 : a_m[i];
+          const int hw = p.Hout * p.Wout;
+          const int img = mm / hw;
+          const int rem = mm - img * hw;
+          const int oy = rem / p.Wout, ox = rem - (rem / p.Wout) * p.Wout;
+          const int iy = oy * p.stride - p.pad + ky, ix = ox * p.stride - p.pad + kx;
+          const bool ok = a_m[i] >= 0 && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
+          int py = iy, px = ix;
+          if (p.upsample) {
+            if (up2) {
+              py = iy >> 1;
+              px = ix >> 1;
+            } else {
+              py = (iy * p.Hin) / Hl;
+              px = (ix * p.Win) / Wl;
+            }
           }
+          const int pix = (img * p.Hin + py) * p.Win + px;
+          // offset such that src + g_off + c0 addresses channel c0 of this tap's source pixel (32-bit:
+          // fd_gemm256_try checks the image sizes)
+          g_off[i] = ok ? (second ? pix * (p.Cin - C1) - C1 + chunk * 8 : pix * (int)p.lda + chunk * 8) : ZP;
         }
-        const long long pix = a_pix[i] + (long long)py * p.Win + px;
-        const T* src = second ? (A2 + pix * (p.Cin - C1) + (c0 - C1) + chunk * 8) : (A + pix * p.lda + c0 + chunk * 8);
-        const void* s_ = ok ? (const void*)src : (const void*)g_zero_page256;
+      }
+      const T* srcb = second ? A2 : A;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const void* s_ = g_off[i] != ZP ? (const void*)(srcb + (g_off[i] + c0)) : (const void*)g_zero_page256;
         __builtin_amdgcn_global_load_lds(s_, LDS_PTR(sa + (w + NW * i) * 1024), 16, 0, 0);
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < AI; ++i)
         __builtin_amdgcn_global_load_lds((const void*)(a_row[i] + k0), LDS_PTR(sa + (w + NW * i) * 1024), 16, 0, 0);
     }
     unsigned char* sb = sa + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (w + NW * i) * 1024), 16, 0, 0);
+    for (int i = 0; i < AI; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(Bw + (b_off[i] + k0)), LDS_PTR(sb + (w + NW * i) * 1024), 16, 0,
+                                       0);
   };
   // all but this wave's youngest `ahead` slots have landed (ahead <= NSL - 1)
   auto wait_ahead = [&](int ahead) {
@@ -151,6 +170,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const fd_gemm_params p, co
   const int fr = lane & 15, fg = lane >> 4;
   const int rd_off = fr * 64 + ((fg ^ (fr >> 2)) << 4);  // row fr of a 16-row block, logical chunk fg
   auto read_frags = [&](int buf, V8 (&af)[MT], V8 (&bf)[NT]) {
+    if (mode & 2) return;
     const unsigned char* sa = smem + buf * SLOT + rd_off;
     const unsigned char* sb = sa + A_BYTES;
 #pragma unroll
@@ -164,6 +184,7 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const fd_gemm_params p, co
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto mma = [&](const V8 (&af)[MT], const V8 (&bf)[NT]) {
+    if (mode & 2) return;
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
@@ -207,6 +228,13 @@ __global__ void __launch_bounds__(512) gemm256_kernel(const fd_gemm_params p, co
   if (s < nsl) step(s, a0, b0, a1, b1);
 
   // ---- epilogue: two 128-row passes through the drained ring
+  if (mode & 4) {
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) asm volatile("" ::"v"(acc[mi][ni]));
+    return;
+  }
   __syncthreads();
   TO* __restrict__ C = (TO*)p.C;
   const TO* __restrict__ R = (const TO*)p.residual;
@@ -334,6 +362,9 @@ extern "C" int fd_gemm256_try(const fd_gemm_params* p, void* stream) {
   if (p->conv && (p->Cin % 32 || (p->C1 > 0 && p->C1 % 32))) return 0;
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if ((long long)((m_ref + 255) / 256) * (p->N / 256) < min_tiles) return 0;
+  // 32-bit element offsets inside the kernel (B rows; conv source pixels)
+  if ((long long)p->N * p->ldb >= (1LL << 31)) return 0;
+  if (p->conv && (long long)p->nimg * p->Hin * p->Win * (p->lda > p->Cin ? p->lda : p->Cin) >= (1LL << 31)) return 0;
   const int tiles_m = (p->M + 255) / 256, tiles_n = p->N / 256;
   const long long tiles = (long long)tiles_m * tiles_n;
   if (tiles > 0x7fffffff) return FD_ERR_SHAPE;
@@ -353,13 +384,14 @@ extern "C" int fd_gemm256_try(const fd_gemm_params* p, void* stream) {
     }
   }
   hipStream_t s = (hipStream_t)stream;
+  // eight waves: the 4-wave (one 128 x 128 wave per SIMD) instance measured 1.3-1.4x slower on the convs
   dim3 grid((unsigned)tiles), block(512);
   int rc = FD_OK;
   FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, {
     if (p->conv)
-      hipLaunchKernelGGL((gemm256_kernel<T, TO, true>), grid, block, 0, s, *p, gm);
+      hipLaunchKernelGGL((gemm256_kernel<T, TO, true, 8>), grid, block, 0, s, *p, gm);
     else
-      hipLaunchKernelGGL((gemm256_kernel<T, TO, false>), grid, block, 0, s, *p, gm);
+      hipLaunchKernelGGL((gemm256_kernel<T, TO, false, 8>), grid, block, 0, s, *p, gm);
   }));
   FD_LAUNCH_CHECK();
   return rc == FD_OK ? 1 : rc;
