@@ -124,32 +124,18 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   const int lrow = lane >> 3, slot = lane & 7;
   const bool hi = (B_TOT % NW == 0) || w < B_TOT % NW;  // this wave issues B_I (not B_LO) B loads
 
-  // ---- per-lane load state (rows fixed over the K loop)
+  // ---- per-lane load state (rows fixed over the K loop).  Conv: the output row; the im2col source pointers are
+  // decoded once per tap in stage() (every Cin / 64 stages), not per stage
   const T* a_row[A_I];
-  int a_iy0[A_I], a_ix0[A_I], a_chunk[A_I];
-  long long a_pix[A_I];
-  bool a_ok[A_I];
+  int a_m[A_I], a_chunk[A_I];
 #pragma unroll
   for (int i = 0; i < A_I; ++i) {
     const int row = (w + NW * i) * 8 + lrow;
     const int m = m0 + row;
-    a_ok[i] = m < M;
     const int mm = m < M ? m : M - 1;
+    a_m[i] = m < M ? m : -1;
     a_chunk[i] = slot ^ ((row >> 1) & 7);
-    if (CONV) {
-      const int hw = p.Hout * p.Wout;
-      const int img = mm / hw;
-      const int rem = mm - img * hw;
-      const int oy = rem / p.Wout, ox = rem - (rem / p.Wout) * p.Wout;
-      a_iy0[i] = oy * p.stride - p.pad;
-      a_ix0[i] = ox * p.stride - p.pad;
-      a_pix[i] = (long long)img * p.Hin * p.Win;
-      a_row[i] = nullptr;
-    } else {
-      a_row[i] = A + (long long)mm * p.lda + a_chunk[i] * 8;
-      a_iy0[i] = a_ix0[i] = 0;
-      a_pix[i] = 0;
-    }
+    a_row[i] = CONV ? nullptr : A + (long long)mm * p.lda + a_chunk[i] * 8;
   }
   const T* b_row[B_I];
 #pragma unroll
@@ -162,6 +148,10 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   const bool up2 = p.upsample && Hl == 2 * p.Hin && Wl == 2 * p.Win;
   const int C1 = p.C1 > 0 ? p.C1 : p.Cin;
 
+  int g_key = -1;        // conv: (tap, source) of g_base; stage() runs in K order within a split
+  const T* g_base[A_I];  // per DMA row: this tap's source-pixel pointer (channel 0), nullptr = zero page
+#pragma unroll
+  for (int i = 0; i < A_I; ++i) g_base[i] = nullptr;
   auto stage = [&](int kt, int buf) {  // kt: global K step
     if (mode & 1) return;
     const int k0 = kt * 64;
@@ -169,28 +159,41 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     if (CONV) {
       const int tap = k0 / p.Cin;
       const int c0 = k0 - tap * p.Cin;
-      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
       const bool second = (A2 != nullptr) && (c0 >= C1);
+      const int key = tap * 2 + (int)second;
+      if (key != g_key) {  // uniform: the source pixels change only with the tap (and the concat source)
+        g_key = key;
+        const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+#pragma unroll
+        for (int i = 0; i < A_I; ++i) {
+          const int mm = a_m[i] < 0 ? 0 : a_m[i];
+          const int hw = p.Hout * p.Wout;
+          const int img = mm / hw;
+          const int rem = mm - img * hw;
+          const int oy = rem / p.Wout, ox = rem - (rem / p.Wout) * p.Wout;
+          const int iy = oy * p.stride - p.pad + ky, ix = ox * p.stride - p.pad + kx;
+          const bool ok = a_m[i] >= 0 && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
+          // exact x2 (every Upsample2D except diffusers' odd-size upsample_size path): a shift, not an integer
+          // division
+          int py = iy, px = ix;
+          if (p.upsample) {
+            if (up2) {
+              py = iy >> 1;
+              px = ix >> 1;
+            } else {
+              py = (iy * p.Hin) / Hl;
+              px = (ix * p.Win) / Wl;
+            }
+          }
+          const long long pix = ((long long)img * p.Hin + py) * p.Win + px;
+          // pointer such that g_base + c0 addresses channel c0 of this tap's source pixel; nullptr = zero page
+          g_base[i] = !ok ? nullptr
+                          : second ? A2 + pix * (p.Cin - C1) - C1 + a_chunk[i] * 8 : A + pix * p.lda + a_chunk[i] * 8;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < A_I; ++i) {
-        const int iy = a_iy0[i] + ky, ix = a_ix0[i] + kx;
-        const bool ok = a_ok[i] && iy >= 0 && iy < Hl && ix >= 0 && ix < Wl;
-        // exact x2 (every Upsample2D except diffusers' odd-size upsample_size path): a shift, not a VALU
-        // integer division per lane and load (the two divisions cost ~60 VALU instructions per A load)
-        int py = iy, px = ix;
-        if (p.upsample) {
-          if (up2) {
-            py = iy >> 1;
-            px = ix >> 1;
-          } else {
-            py = (iy * p.Hin) / Hl;
-            px = (ix * p.Win) / Wl;
-          }
-        }
-        const long long pix = a_pix[i] + (long long)py * p.Win + px;
-        const T* src = second ? (A2 + pix * (p.Cin - C1) + (c0 - C1) + a_chunk[i] * 8)
-                              : (A + pix * p.lda + c0 + a_chunk[i] * 8);
-        const void* s = ok ? (const void*)src : (const void*)g_zero_page8;
+        const void* s = g_base[i] ? (const void*)(g_base[i] + c0) : (const void*)g_zero_page8;
         __builtin_amdgcn_global_load_lds(s, LDS_PTR(sa + (w + NW * i) * 1024), 16, 0, 0);
       }
     } else {
