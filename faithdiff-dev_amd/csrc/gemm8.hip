@@ -263,6 +263,24 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   for (int s0 = 0; s0 < NS; ++s0)
     if (s0 < nkl) stage(kb + s0, s0);
   wait_ahead(min(nkl - 1, NS - 1));
+  if (LNF && tid < BN) ln_cs[tid] = lncv;
+  if (LNF && tid < BM) {  // (mean, rstd) per row, fp64 fold in a fixed order; written once stage 0 (issued after
+    // the partials) has landed, so the 17 partial registers are not live across the K loop; read after its barriers
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int i = 0; i < (LNF ? 4 : 1); ++i)
+      if (2 * i < lnP) {
+        s += lnv4[i][0];
+        q += lnv4[i][1];
+        s += lnv4[i][2];
+        q += lnv4[i][3];
+      }
+    const double ik = 1.0 / 1024.0 * (1024.0f / (float)K);  // 1/K without an fp64 divide
+    const double mu = s * ik;
+    double var = q * ik - mu * mu;
+    if (var < 0.0) var = 0.0;
+    ln_tab[tid] = make_float2((float)mu, rsqrtf((float)var + p.ln_eps));
+  }
   __builtin_amdgcn_s_barrier();
   V8 a0[MT], b0[NT], a1[MT], b1[NT];
   read_frags(0, 0, a0, b0);
@@ -451,23 +469,6 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
       gbh[q] = bias ? bias[np] : 0.f;
       gbg[q] = bias ? bias[np + 16] : 0.f;
     }
-  }
-  if (LNF && tid < BN) ln_cs[tid] = lncv;
-  if (LNF && tid < BM) {  // (mean, rstd) per row, fp64 fold in a fixed order; read after the first barrier below
-    double s = 0.0, q = 0.0;
-#pragma unroll
-    for (int i = 0; i < (LNF ? 4 : 1); ++i)
-      if (2 * i < lnP) {
-        s += lnv4[i][0];
-        q += lnv4[i][1];
-        s += lnv4[i][2];
-        q += lnv4[i][3];
-      }
-    const double ik = 1.0 / 1024.0 * (1024.0f / (float)K);  // 1/K without an fp64 divide
-    const double mu = s * ik;
-    double var = q * ik - mu * mu;
-    if (var < 0.0) var = 0.0;
-    ln_tab[tid] = make_float2((float)mu, rsqrtf((float)var + p.ln_eps));
   }
   const bool vec = (Nout % 8 == 0) && (p.ldc % 8 == 0) && ((((unsigned long long)C) & 15) == 0) &&
                    (!R || ((p.ldr % 8 == 0) && ((((unsigned long long)R) & 15) == 0))) &&

@@ -27,6 +27,7 @@ for step in "$@"; do
     bench_quick) run bench_quick 600 python bench.py --no-cpu-baseline --no-c3 ;;
     bench_c3) run bench_c3 600 python bench.py --workload c3 --no-cpu-baseline ;;
     bench_fp8) run bench_fp8 600 python bench.py --fp8 --no-cpu-baseline --no-c3 --no-pipeline ;;
+    rehearsal) FD_BENCH_REHEARSAL=1 run rehearsal 600 python bench.py --gpus 2 --no-cpu-baseline --no-pipeline --no-roofline --no-vae --c3-steps 2 --steps 5 ;;
     prof) run prof 600 bash scripts/r02_trace.sh ;;
     pmc_unet) run pmc_unet 700 bash scripts/r02_prof.sh unet r02_unet_pmc ;;
     pmc_vae) run pmc_vae 700 bash scripts/r02_prof.sh vae r02_vae_pmc ;;
