@@ -394,7 +394,7 @@ def roofline_leg(loop, fp8):
         "bound": "mfma", "achieved": round(gemm_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
         "frac": round(gemm_tf / PEAK_BF16_TFLOPS, 4),
         "traffic": None if tr is None else tr["hbm_bytes_per_forward"],
-        "kernel": "gemm8_kernel + gemm_kernel (all MFMA GEMM + implicit-GEMM conv launches of one UNet forward)",
+        "kernel": "gemm8_kernel + gemm256_kernel + gemm_kernel (all MFMA GEMM + implicit-GEMM conv launches of one UNet forward)",
         "launches": n_g, "algorithmic_flops": fl_g, "kernel_ms_per_forward": round(ms_g, 3),
         "avg_launch_us": round(ms_g / n_g * 1e3, 2),
         "method": "the forward's GEMM launches captured on their own into one hipGraph, replayed 20x between HIP "

@@ -22,8 +22,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def family(name):
     if "gemm_e4m3" in name:
         return "gemm_e4m3"
-    if "gemm_kernel" in name or "gemm8_kernel" in name:
+    if "gemm_kernel" in name or "gemm8_kernel" in name or "gemm256_kernel" in name:
         return "gemm"
+    if "quant_rows_e4m3" in name or "layer_norm_e4m3" in name:
+        return "fp8_quant"
     if "flash_attn" in name:
         return "flash_attn"
     if "gn_" in name:
@@ -117,7 +119,10 @@ def main(what, out_path, base=None):
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c and "GRBM_GUI_ACTIVE" in c and c["GRBM_GUI_ACTIVE"]:
             e["mfma_busy"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * 256 * c["GRBM_GUI_ACTIVE"] / 8), 4)
             if f.get("grbm_pass_us"):
+                # GRBM_GUI_ACTIVE / 8 / wall reads high on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md,
+                # DVFS give-back), so mfma_busy above is a lower bound; the bound below assumes the 2.4 GHz peak clock
                 e["effective_clock_ghz_profiled"] = round(c["GRBM_GUI_ACTIVE"] / 8 / (f["grbm_pass_us"] * 1e3), 3)
+                e["mfma_busy_at_2p4ghz"] = round(c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * 2.4e3 * f["grbm_pass_us"]), 4)
         e["counters"] = {k: v for k, v in sorted(c.items())}
         out[name] = e
     res["families"] = out

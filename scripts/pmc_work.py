@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Workloads for rocprofv3 passes (kernel trace, PMC counters): ``--what unet`` = one C2 UNet forward (B=2,
-128x128 latent, bf16); ``--what vae`` = one 1024^2 fp16 VAE decode; ``--what attn`` = the 140 flash-attention
+128x128 latent, bf16); ``--what unet_fp8`` = the same with quantize_8bit weights and the
+e4m3-MFMA Linears; ``--what vae`` = one 1024^2 fp16 VAE decode; ``--what attn`` = the 140 flash-attention
 launches of one C2 forward.  Each is preceded by a calibration copy of known size (1 GiB -> 1 GiB, larger than
 the Infinity Cache); fd_postprocess_u8 launches (never part of the workloads) mark the windows: [m1, m2) = the
 copy, [m2, m3) = the measured workload.  The workload runs once eagerly first (warm caches and workspaces, same
@@ -17,12 +18,14 @@ sys.path.insert(0, os.path.join(ROOT, "faithdiff-dev_amd"))
 import torch  # noqa: E402
 
 
-def unet_work(dev):
+def unet_work(dev, fp8=False):
     from fdhip import arch, ops
     from fdhip.unet import HipUNet
     k, B = 128, 2
     sd = arch.random_init(arch.unet_param_shapes(True), seed=0, device=dev)
-    unet = HipUNet(sd, dev, torch.bfloat16)
+    if fp8:  # quantize_8bit weights, transformer Linears on the e4m3 MFMA (bench.py --fp8)
+        sd = arch.quantize_e4m3(sd)
+    unet = HipUNet(sd, dev, torch.bfloat16, fp8_mfma=fp8)
     del sd
     g = torch.Generator(device=dev).manual_seed(0)
     unet.set_context(torch.randn((2, 77, 2048), generator=g, device=dev))
@@ -32,7 +35,8 @@ def unet_work(dev):
     tids = torch.tensor([[1024.0, 1024.0, 0, 0, 1024.0, 1024.0]] * B, device=dev)
     text = torch.randn((B, 1280), generator=g, device=dev)
     ops.reserve_gn_workspace(1 << 24, dev)
-    return "C2 1024 UNet forward", lambda: unet.forward(x, t, tids, text, cond, B, k, k)
+    name = "C2 1024 UNet forward" + (" (use_fp8, e4m3 MFMA Linears)" if fp8 else "")
+    return name, lambda: unet.forward(x, t, tids, text, cond, B, k, k)
 
 
 def vae_work(dev):
@@ -67,13 +71,14 @@ def attn_work(dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", choices=("unet", "vae", "attn"), required=True)
+    ap.add_argument("--what", choices=("unet", "unet_fp8", "vae", "attn"), required=True)
     a = ap.parse_args()
     from fdhip import lib as L
     from fdhip import ops
     L.require_device()
     dev = torch.device("cuda", 0)
-    name, fn = {"unet": unet_work, "vae": vae_work, "attn": attn_work}[a.what](dev)
+    work = {"unet": unet_work, "unet_fp8": lambda d: unet_work(d, fp8=True), "vae": vae_work, "attn": attn_work}
+    name, fn = work[a.what](dev)
     fn()
     torch.cuda.synchronize()
     rec = []

@@ -31,6 +31,8 @@ for step in "$@"; do
     prof) run prof 600 bash scripts/r02_trace.sh ;;
     pmc_unet) run pmc_unet 700 bash scripts/r02_prof.sh unet r02_unet_pmc ;;
     pmc_vae) run pmc_vae 700 bash scripts/r02_prof.sh vae r02_vae_pmc ;;
+    pmc_fp8) run pmc_fp8 700 bash scripts/r02_prof.sh unet_fp8 r02_unet_fp8_pmc ;;
+    vendor) run vendor 300 python scripts/vendor_compare.py ;;
     pmc_attn) run pmc_attn 700 bash scripts/r02_prof.sh attn r02_attn_pmc ;;
     *) echo "unknown step $step"; exit 3 ;;
   esac
