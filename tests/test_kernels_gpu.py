@@ -107,7 +107,10 @@ def conv_ref(x_nhwc, w, b, nimg, H, W, stride, pad, upsample=False, vae_pad=Fals
 @pytest.mark.parametrize("nimg,H,W,Cin,Cout,stride,pad,up", [
     (2, 128, 128, 320, 320, 1, 1, False), (2, 32, 32, 1280, 1280, 1, 1, False), (2, 64, 64, 640, 640, 2, 1, False),
     (1, 33, 47, 128, 256, 1, 1, False), (1, 64, 64, 128, 128, 2, 0, False), (2, 32, 32, 1280, 1280, 1, 1, True),
-    (1, 40, 24, 256, 3, 1, 1, False), (2, 16, 16, 320, 4, 1, 1, False)])
+    (1, 40, 24, 256, 3, 1, 1, False), (2, 16, 16, 320, 4, 1, 1, False),
+    # Cout <= 8: the narrow conv kernel (VAE conv_out 128 -> 3, encoder 512 -> 8)
+    (1, 256, 192, 128, 3, 1, 1, False), (2, 33, 17, 512, 8, 1, 1, False), (1, 64, 64, 128, 6, 2, 0, False),
+    (1, 31, 29, 64, 1, 2, 1, False)])
 def test_conv3x3(dtype, nimg, H, W, Cin, Cout, stride, pad, up):
     from fdhip import ops
     x = rnd(nimg * H * W, Cin, dtype=dtype)
