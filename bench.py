@@ -414,7 +414,7 @@ def roofline_leg(loop, fp8):
                                "unit": "TFLOP/s", "frac": round(f8_tf / PEAK_FP8_TFLOPS, 4),
                                "kernel": "gemm_e4m3_dma_kernel (transformer Linears, e4m3 x e4m3)",
                                "launches": n_f, "algorithmic_flops": fl_f, "kernel_ms_per_forward": round(ms_f, 3)}
-    flops = arch.unet_flops(loop.k, loop.k, loop.B)
+    flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False)
     res["forward_graph_ms"] = round(fam["_all"][3], 3)
     res["kernel_ms_per_forward"] = {k: round(v[3], 3) for k, v in fam.items() if not k.startswith("_")}
     return res, flops
@@ -519,7 +519,8 @@ def main(argv=None):
         torch.cuda.synchronize()
         ev_ms = ev0.elapsed_time(ev1)
         from fdhip import arch
-        flops = arch.unet_flops(loop.k, loop.k, loop.B)
+        # the prompt's attn2 K/V projection runs once per prompt (HipUNet.set_context), not in the step
+        flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False)
         step_s = ev_ms / 1e3 / args.steps
         result.update({
             "metric": "denoise steps/sec @1024px 20-step + VAE decode ms",

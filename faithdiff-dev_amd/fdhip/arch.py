@@ -244,10 +244,11 @@ def count(shapes):
     return n
 
 
-def unet_flops(h, w, B=2, with_extras=True, Lk=77):
+def unet_flops(h, w, B=2, with_extras=True, Lk=77, prompt_kv=True):
     """Algorithmic FLOPs (2 per MAC) of one UNet forward on B rows of an h x w latent: every conv / Linear
     GEMM plus attention QK^T and PV (4*Lq*Lk*d per head); norms/elementwise are bytes, not FLOPs
-    (SURVEY 8(d)).  C2 (B=2, 128x128) = 14.217 TFLOP."""
+    (SURVEY 8(d)).  C2 (B=2, 128x128) = 14.217 TFLOP.  prompt_kv=False leaves out the attn2 to_k / to_v
+    projections of the prompt (0.105 TFLOP at C2), which HipUNet computes once per prompt (set_context)."""
     C, Lr, Hd = UNET_CH, UNET_LAYERS, UNET_HEADS
     f = 0.0
 
@@ -267,7 +268,8 @@ def unet_flops(h, w, B=2, with_extras=True, Lk=77):
         x = 2 * lin(M, c, c)
         for _ in range(layers):
             x += lin(M, c, 3 * c) + lin(M, c, c) + 4.0 * B * T * T * c        # attn1
-            x += lin(M, c, c) + lin(B * Lk, 2048, 2 * c) + lin(M, c, c) + 4.0 * B * T * Lk * c  # attn2
+            x += lin(M, c, c) + (lin(B * Lk, 2048, 2 * c) if prompt_kv else 0.0) + lin(M, c, c) \
+                + 4.0 * B * T * Lk * c  # attn2
             x += lin(M, c, 8 * c) + lin(M, 4 * c, c)                          # GEGLU FF
         return x
 

@@ -188,6 +188,7 @@ class HipUNet:
         self.kv_total = off
         self.ctx = None
         self.ncfg = None
+        self._kv = None
         self.graphs = GraphCache()
 
     # ------------------------------------------------------------------------------------------ context
@@ -199,10 +200,21 @@ class HipUNet:
             yield from blk["attns"]
 
     def set_context(self, ctx):
-        """ctx: [ncfg, 77, 2048] prompt embeddings ([neg, pos] under CFG).  Stored on device; every forward
-        projects it through all 70 attn2 to_k/to_v at once (one K/V pair serves every tile of the batch)."""
-        self.ctx = ctx.to(device=self.device, dtype=self.dtype).contiguous().reshape(-1, ctx.shape[-1])
+        """ctx: [ncfg, 77, 2048] prompt embeddings ([neg, pos] under CFG).  Projects them through all 70 attn2
+        to_k/to_v at once into ``self._kv`` [ncfg*77, sum 2C] -- once per prompt, not per forward: the
+        reference recomputes attn2's K/V of the same prompt in every UNet call of the loop (pipeline:1350, 20
+        steps x every tile); the product is identical, the GEMM (105 GFLOP, ~0.23 ms) runs once.
+        The device buffers keep their addresses across calls with the same shape (a new prompt is copied in),
+        so the hipGraphs captured by run() stay valid; a new shape drops them."""
+        c = ctx.to(device=self.device, dtype=self.dtype).reshape(-1, ctx.shape[-1])
+        if self.ctx is not None and self.ctx.shape == c.shape and self.ncfg == ctx.shape[0]:
+            self.ctx.copy_(c)
+        else:
+            self.ctx = c.contiguous().clone()
+            self._kv = torch.empty((c.shape[0], self.kv_total), dtype=self.dtype, device=self.device)
+            self.graphs.clear()
         self.ncfg, self.Lk = ctx.shape[0], ctx.shape[1]
+        ops.gemm(self.ctx, self.kv_w, out=self._kv)  # [ncfg*77, sum 2C]: every attn2 K/V
 
     # ------------------------------------------------------------------------------------------ blocks
     def _resnet(self, r, x, B, H, Wd, temb, x2=None, C1=None):
@@ -349,23 +361,19 @@ class HipUNet:
             return self._forward(x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample)
 
     def _forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample):
-        # The time / add embeddings (six M = 2 launches) and the attn2 K/V projection of the prompt for all 70
-        # blocks depend on nothing the input path computes: they run on a second stream beside conv_in and
-        # the FaithDiff extras (a fork / join inside the captured graph).  Neither uses split-K, so the two
-        # streams never share the GEMM workspace.  Opt-in (FD_SIDE_STREAM=1): measured 0.39 ms/step SLOWER at
-        # C2 -- the K/V GEMM's 2600 workgroups compete with the extras' full-chip convs.
+        # The time / add embeddings (six M = 2 launches) depend on nothing the input path computes: they can run
+        # on a second stream beside conv_in and the FaithDiff extras (a fork / join inside the captured graph;
+        # no split-K, so the streams never share the GEMM workspace).  Opt-in (FD_SIDE_STREAM=1): measured
+        # 0.39 ms/step SLOWER at C2 when it also carried the prompt K/V GEMM (now in set_context).
         cur = torch.cuda.current_stream(self.device)
         side = self._side_stream()
         if side is not None:
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 temb = self.embeddings(t, time_ids, text_embeds, B)
-                self._kv = ops.gemm(self.ctx, self.kv_w)
             temb.record_stream(cur)
-            self._kv.record_stream(cur)
         else:
             temb = self.embeddings(t, time_ids, text_embeds, B)
-            self._kv = ops.gemm(self.ctx, self.kv_w)  # [ncfg*77, sum 2C]: every attn2 K/V of this forward
         x0 = ops.conv_direct(x, *self.conv_in, B, H, Wd, 4, 3, 1, 1, out_dtype=self.dtype)
         if cond is not None and self.has_extras:
             feat = self._extras(x0, cond, B, H, Wd)
