@@ -208,7 +208,7 @@ class C2Loop:
         self.canvas = torch.randn((4, h, h), generator=g, device=dev) * 11.0
         self.nxt = torch.empty_like(self.canvas)
         self.cond = torch.randn((self.B * k * k, 512), generator=g, device=dev).to(unet.dtype)
-        ctx = torch.randn((2, 77, 2048), generator=g, device=dev)
+        self.ctx = ctx = torch.randn((2, 77, 2048), generator=g, device=dev)
         self.text = torch.randn((self.B, 1280), generator=g, device=dev)
         self.tids = torch.tensor([[size, size, 0, 0, size, size]] * self.B, dtype=torch.float32, device=dev)
         self.grid = TileGrid(h, h, (128, 128), 0.5)
@@ -229,6 +229,8 @@ class C2Loop:
 
     def step(self, i):
         ops, k, h = self.ops, self.k, self.h
+        if i % 20 == 0:  # once per image, as __call__ does: the prompt's attn2 K/V projection (set_context)
+            self.unet.set_context(self.ctx)
         s_, sn = self.sig[i % 20], self.sig[i % 20 + 1]
         ops.tlc_scale_input(self.canvas, self.rows, self.cols, h, h, k, k, 0, self.grid.ntiles, self.cfg, s_,
                             self.xin)
@@ -519,8 +521,9 @@ def main(argv=None):
         torch.cuda.synchronize()
         ev_ms = ev0.elapsed_time(ev1)
         from fdhip import arch
-        # the prompt's attn2 K/V projection runs once per prompt (HipUNet.set_context), not in the step
-        flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False)
+        # the prompt's attn2 K/V projection runs once per 20-step image (HipUNet.set_context), as in __call__
+        kv_fl = arch.unet_flops(loop.k, loop.k, loop.B) - arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False)
+        flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False) + kv_fl * ((args.steps + 19) // 20) / args.steps
         step_s = ev_ms / 1e3 / args.steps
         result.update({
             "metric": "denoise steps/sec @1024px 20-step + VAE decode ms",
