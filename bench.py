@@ -220,22 +220,30 @@ class C2Loop:
         self.sig, self.ts = [float(s) for s in sch.sigmas], [float(t) for t in sch.timesteps]
         unet.set_context(ctx)
         self.xin = torch.empty((self.B * k * k, 4), dtype=unet.dtype, device=dev)
+        self.ie = torch.empty((self.B * k * k, 320), dtype=unet.dtype, device=dev)
+        self.per_image()
         self.t_buf = torch.full((self.B,), self.ts[0], device=dev)
         self.out_tiles = torch.empty((self.grid.ntiles, 4, k, k), device=dev)
         ops.reserve_gn_workspace(1 << 24, dev)
 
     def args(self):
-        return (self.xin, self.t_buf, self.tids, self.text, self.cond, self.B, self.k, self.k)
+        return (self.xin, self.t_buf, self.tids, self.text, self.ie, self.B, self.k, self.k)
+
+    def per_image(self):
+        """What __call__ does once per image: the prompt's attn2 K/V projection (set_context) and the condition
+        embedding of the tile's image latents (cond_embed)."""
+        self.unet.set_context(self.ctx)
+        self.ie = self.unet.cond_embed(self.cond, self.B, self.k, self.k, out=self.ie)
 
     def step(self, i):
         ops, k, h = self.ops, self.k, self.h
-        if i % 20 == 0:  # once per image, as __call__ does: the prompt's attn2 K/V projection (set_context)
-            self.unet.set_context(self.ctx)
+        if i % 20 == 0:  # once per 20-step image, as __call__ does
+            self.per_image()
         s_, sn = self.sig[i % 20], self.sig[i % 20 + 1]
         ops.tlc_scale_input(self.canvas, self.rows, self.cols, h, h, k, k, 0, self.grid.ntiles, self.cfg, s_,
                             self.xin)
         self.t_buf.fill_(self.ts[i % 20])
-        eps = self.unet.run(*self.args())
+        eps = self.unet.run(*self.args(), cond_embedded=True)
         ops.tlc_cfg_euler_step(eps, self.canvas, self.rows, self.cols, h, h, k, k, 0, self.grid.ntiles, self.cfg,
                                5.0, 0.0, s_, sn, self.out_tiles)
         ops.tlc_blend(self.out_tiles, self.weights, self.rows, self.cols, 4, h, h, k, k, self.nxt)
@@ -387,7 +395,7 @@ def c3_run(pipe, world, rank, dev, size, steps, warm=True):
 
 def roofline_leg(loop, fp8):
     from fdhip import arch
-    fam = family_times(lambda: loop.unet.forward(*loop.args()), ["gemm", "flash_attn", "gemm_e4m3"])
+    fam = family_times(lambda: loop.unet.forward(*loop.args(), cond_embedded=True), ["gemm", "flash_attn", "gemm_e4m3"])
     n_g, fl_g, _, ms_g = fam["gemm"]
     gemm_tf = fl_g / (ms_g / 1e3) / 1e12
     res = {}
@@ -416,7 +424,7 @@ def roofline_leg(loop, fp8):
                                "unit": "TFLOP/s", "frac": round(f8_tf / PEAK_FP8_TFLOPS, 4),
                                "kernel": "gemm_e4m3_dma_kernel (transformer Linears, e4m3 x e4m3)",
                                "launches": n_f, "algorithmic_flops": fl_f, "kernel_ms_per_forward": round(ms_f, 3)}
-    flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False)
+    flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False, cond_embed=False)
     res["forward_graph_ms"] = round(fam["_all"][3], 3)
     res["kernel_ms_per_forward"] = {k: round(v[3], 3) for k, v in fam.items() if not k.startswith("_")}
     return res, flops
@@ -521,9 +529,10 @@ def main(argv=None):
         torch.cuda.synchronize()
         ev_ms = ev0.elapsed_time(ev1)
         from fdhip import arch
-        # the prompt's attn2 K/V projection runs once per 20-step image (HipUNet.set_context), as in __call__
-        kv_fl = arch.unet_flops(loop.k, loop.k, loop.B) - arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False)
-        flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False) + kv_fl * ((args.steps + 19) // 20) / args.steps
+        # the prompt's attn2 K/V projection and the tile's condition embedding run once per 20-step image
+        # (HipUNet.set_context / cond_embed, C2Loop.per_image), as in __call__
+        base = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False, cond_embed=False)
+        flops = base + (arch.unet_flops(loop.k, loop.k, loop.B) - base) * ((args.steps + 19) // 20) / args.steps
         step_s = ev_ms / 1e3 / args.steps
         result.update({
             "metric": "denoise steps/sec @1024px 20-step + VAE decode ms",

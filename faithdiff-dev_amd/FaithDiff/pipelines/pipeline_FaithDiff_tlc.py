@@ -420,6 +420,17 @@ class FaithDiffStableDiffusionXLPipeline:
         # 7. per-row conditioning, computed once per image
         unet.set_context(ctx.to(dev))
         tb = max(1, min(self.tile_batch, shard.count or 1))
+        # the FaithDiff condition embedding (ext:528-534) of every tile's image latents: fixed across the denoise
+        # loop, so computed once per image here (the reference recomputes it inside every UNet call, :1350),
+        # per tile batch, bitwise what the forward would compute (HipUNet.cond_embed)
+        cond_emb = False
+        if cond_tiles is not None and unet.has_extras:
+            ie_tiles = torch.empty((cond_tiles.shape[0], kh * kw, 320), dtype=cond_dt, device=dev)
+            for c0 in range(0, shard.count, tb):
+                r0, r1 = c0 * cfg, min(c0 + tb, shard.count) * cfg
+                unet.cond_embed(cond_tiles[r0:r1].reshape(-1, 512), r1 - r0, kh, kw,
+                                out=ie_tiles[r0:r1].reshape(-1, 320))
+            cond_tiles, cond_emb = ie_tiles, True
         B = tb * cfg
         text_rows = text.to(dev).repeat(tb, 1).contiguous()  # [B, 1280]
         tids_all = torch.tensor([[original_size[0], original_size[1], i, j, target_size[0], target_size[1]]
@@ -437,11 +448,11 @@ class FaithDiffStableDiffusionXLPipeline:
                 n = min(tb, count - c0)
                 rows = n * cfg
                 ops.tlc_scale_input(state["canvas"], rows_t, cols_t, h, w, kh, kw, begin + c0, n, cfg, s, xin)
-                cond = cond_tiles[c0 * cfg:(c0 + n) * cfg].reshape(rows * kh * kw, 512)
+                cond = cond_tiles[c0 * cfg:(c0 + n) * cfg].reshape(rows * kh * kw, cond_tiles.shape[-1])
                 tid = tids_all[(begin + c0) * cfg:(begin + c0 + n) * cfg]
                 # one hipGraph replay per tile batch after the first two steps (HipUNet.run, fdhip/graphs.py)
                 eps = unet.run(xin[:rows * kh * kw], t_rows[i, :rows], tid, text_rows[:rows], cond, rows, kh, kw,
-                               add_sample=add_sample)
+                               add_sample=add_sample, cond_embedded=cond_emb)
                 ops.tlc_cfg_euler_step(eps, state["canvas"], rows_t, cols_t, h, w, kh, kw, begin + c0, n, cfg,
                                        guidance_scale, guidance_rescale, s, s_next, out[c0:c0 + n])
 

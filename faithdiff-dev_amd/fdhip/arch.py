@@ -244,11 +244,13 @@ def count(shapes):
     return n
 
 
-def unet_flops(h, w, B=2, with_extras=True, Lk=77, prompt_kv=True):
+def unet_flops(h, w, B=2, with_extras=True, Lk=77, prompt_kv=True, cond_embed=True):
     """Algorithmic FLOPs (2 per MAC) of one UNet forward on B rows of an h x w latent: every conv / Linear
     GEMM plus attention QK^T and PV (4*Lq*Lk*d per head); norms/elementwise are bytes, not FLOPs
     (SURVEY 8(d)).  C2 (B=2, 128x128) = 14.217 TFLOP.  prompt_kv=False leaves out the attn2 to_k / to_v
-    projections of the prompt (0.105 TFLOP at C2), which HipUNet computes once per prompt (set_context)."""
+    projections of the prompt (0.105 TFLOP at C2), which HipUNet computes once per prompt (set_context);
+    cond_embed=False the condition embedding of the image latents (0.251 TFLOP), computed once per tile
+    (HipUNet.cond_embed)."""
     C, Lr, Hd = UNET_CH, UNET_LAYERS, UNET_HEADS
     f = 0.0
 
@@ -280,7 +282,8 @@ def unet_flops(h, w, B=2, with_extras=True, Lk=77, prompt_kv=True):
     T = [a * b for a, b in sizes]
     f += conv(M[0], 4, C[0])
     if with_extras:
-        f += conv(M[0], 512, 512) + conv(M[0], 512, 320)
+        if cond_embed:
+            f += conv(M[0], 512, 512) + conv(M[0], 512, 320)
         f += 2 * (lin(M[0], 640, 1920) + lin(M[0], 640, 640) + 4.0 * M[0] * B * 640 + lin(M[0], 640, 1280)
                   + lin(M[0], 1280, 640))
         f += lin(M[0], 640, 320)

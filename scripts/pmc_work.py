@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Workloads for rocprofv3 passes (kernel trace, PMC counters): ``--what unet`` = one C2 UNet forward (B=2,
-128x128 latent, bf16); ``--what unet_fp8`` = the same with quantize_8bit weights and the
+128x128 latent, bf16; the prompt K/V and the condition embedding precomputed, as in the denoise loop); ``--what unet_fp8`` = the same with quantize_8bit weights and the
 e4m3-MFMA Linears; ``--what vae`` = one 1024^2 fp16 VAE decode; ``--what attn`` = the 140 flash-attention
 launches of one C2 forward.  Each is preceded by a calibration copy of known size (1 GiB -> 1 GiB, larger than
 the Infinity Cache); fd_postprocess_u8 launches (never part of the workloads) mark the windows: [m1, m2) = the
@@ -36,7 +36,8 @@ def unet_work(dev, fp8=False):
     text = torch.randn((B, 1280), generator=g, device=dev)
     ops.reserve_gn_workspace(1 << 24, dev)
     name = "C2 1024 UNet forward" + (" (use_fp8, e4m3 MFMA Linears)" if fp8 else "")
-    return name, lambda: unet.forward(x, t, tids, text, cond, B, k, k)
+    ie = unet.cond_embed(cond, B, k, k)  # once per tile in __call__ and in bench.py's step (not in the window)
+    return name, lambda: unet.forward(x, t, tids, text, ie, B, k, k, cond_embedded=True)
 
 
 def vae_work(dev):

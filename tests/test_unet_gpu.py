@@ -142,3 +142,24 @@ def test_graph_replay_follows_set_context():
     assert torch.equal(r2, e2)
     assert torch.equal(r1, e1)
     assert not torch.equal(r1, r2)
+
+
+def test_cond_embed_hoisted_is_bitwise():
+    """HipUNet.cond_embed (the condition embedding computed once per tile, outside the loop) + forward(...,
+    cond_embedded=True) gives the bits of forward(image latents) -- for a two-tile batch whose embedding is
+    computed in one launch set as in the pipeline."""
+    _, hip = unet_pair()
+    h, w = 40, 24
+    B, x, cond, ctx, text, tids = make_inputs(h, w, 2, seed=5)
+    dev = "cuda"
+    hip.set_context(ctx)
+    xn = x.permute(0, 2, 3, 1).reshape(B * h * w, 4).to(dev, torch.bfloat16).contiguous()
+    cn = cond.permute(0, 2, 3, 1).reshape(B * h * w, 512).to(dev, torch.bfloat16).contiguous()
+    tt = torch.full((B,), 701.0, device=dev)
+    full = hip.forward(xn, tt, tids.to(dev), text.to(dev), cn, B, h, w).clone()
+    ie = hip.cond_embed(cn, B, h, w)
+    hoisted = hip.forward(xn, tt, tids.to(dev), text.to(dev), ie, B, h, w, cond_embedded=True)
+    assert torch.equal(full, hoisted)
+    # per-tile embeddings (2 rows each) == the batched one
+    ie1 = torch.cat([hip.cond_embed(cn[i * 2 * h * w:(i + 1) * 2 * h * w].contiguous(), 2, h, w) for i in range(2)])
+    assert torch.equal(ie1, ie)
