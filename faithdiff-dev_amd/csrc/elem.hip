@@ -301,7 +301,7 @@ extern "C" int fd_time_features(const float* t, const float* time_ids, const flo
 template <typename TO>
 __global__ void tlc_scale_input_kernel(const float* __restrict__ canvas, const int* __restrict__ row_org,
                                        const int* __restrict__ col_org, int nc, int H, int W, int kh, int kw,
-                                       int tile_begin, int ntiles, int cfg, float inv_s, TO* __restrict__ out) {
+                                       int tile_begin, int ntiles, int cfg, float s, TO* __restrict__ out) {
   const long long per = (long long)kh * kw;
   const long long total = (long long)ntiles * per;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
@@ -312,7 +312,7 @@ __global__ void tlc_scale_input_kernel(const float* __restrict__ canvas, const i
     const int oy = row_org[tid / nc] + y, ox = col_org[tid % nc] + x;
     float v[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) v[c] = canvas[((long long)c * H + oy) * W + ox] * inv_s;
+    for (int c = 0; c < 4; ++c) v[c] = __fdiv_rn(canvas[((long long)c * H + oy) * W + ox], s);
     for (int d = 0; d < cfg; ++d) {
       TO* o = out + (((long long)(t * cfg + d)) * per + p) * 4;
 #pragma unroll
@@ -327,10 +327,12 @@ extern "C" int fd_tlc_scale_input(const float* canvas, const int* row_org, int n
   if (!canvas || !row_org || !col_org || !out) return FD_ERR_ARG;
   if (ntiles <= 0 || tile_begin < 0 || tile_begin + ntiles > nr * nc || kh > H || kw > W || cfg <= 0)
     return FD_ERR_SHAPE;
-  const float inv_s = 1.0f / sqrtf(sigma * sigma + 1.0f);
-  hipStream_t s = (hipStream_t)stream;
+  // scale_model_input divides by (sigma^2 + 1)^0.5 (diffusers EulerDiscreteScheduler; pipeline:1336): `sigma`
+  // here is that divisor, computed by the caller the way torch does in fp32; correctly rounded division per element
+  if (!(sigma > 0.f)) return FD_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
   FD_DISPATCH_O(dtype, hipLaunchKernelGGL(tlc_scale_input_kernel<TO>, grid1d((long long)ntiles * kh * kw), dim3(256), 0,
-                                          s, canvas, row_org, col_org, nc, H, W, kh, kw, tile_begin, ntiles, cfg, inv_s,
+                                          st, canvas, row_org, col_org, nc, H, W, kh, kw, tile_begin, ntiles, cfg, sigma,
                                           (TO*)out));
   FD_LAUNCH_CHECK();
   return FD_OK;

@@ -414,9 +414,17 @@ def time_features(t, time_ids, text_embeds, tfeat, afeat, batch):
 
 
 # --------------------------------------------------------------------------------------- denoise loop
+def euler_scale_divisor(sigma):
+    """(sigma^2 + 1)^0.5 in fp32 exactly as torch computes scale_model_input's divisor from the fp32 sigmas."""
+    sg = torch.tensor(float(sigma), dtype=torch.float32)
+    return float((sg ** 2 + 1) ** 0.5)
+
+
 def tlc_scale_input(canvas, row_org, col_org, H, W, kh, kw, tile_begin, ntiles, cfg, sigma, out):
+    """Tiles of the canvas / (sigma^2 + 1)^0.5 (correctly rounded fp32 division), CFG-duplicated, NHWC."""
     L.check(L.load().fd_tlc_scale_input(L.ptr(canvas), L.ptr(row_org), row_org.numel(), L.ptr(col_org),
-                                        col_org.numel(), H, W, kh, kw, tile_begin, ntiles, cfg, sigma, L.ptr(out),
+                                        col_org.numel(), H, W, kh, kw, tile_begin, ntiles, cfg,
+                                        euler_scale_divisor(sigma), L.ptr(out),
                                         L.dtype_code(out.dtype), L.stream()), "fd_tlc_scale_input")
     return out
 

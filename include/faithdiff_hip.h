@@ -214,7 +214,9 @@ int fd_time_features(const float* t, const float* time_ids, const float* text_em
  * are this call's (a rank's shard when tiles are spread over GPUs).
  * ------------------------------------------------------------------------------------------- */
 /* grids + CFG duplicate + EulerDiscreteScheduler.scale_model_input (:1326,1334-1336):
- * out NHWC dtype [ntiles*cfg][kh*kw][4] = canvas tile / sqrt(sigma^2 + 1). */
+ * out NHWC dtype [ntiles*cfg][kh*kw][4] = canvas tile / scale, correctly rounded fp32 division, where the
+ * argument `sigma` carries scale = (sigma^2 + 1)^0.5 as torch computes it in fp32 from the sigma (ops.py
+ * euler_scale_divisor); must be > 0. */
 int fd_tlc_scale_input(const float* canvas, const int* row_org, int nr, const int* col_org, int nc, int H, int W,
                        int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma, void* out, int dtype,
                        void* stream);

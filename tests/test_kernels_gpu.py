@@ -295,9 +295,11 @@ def test_tlc_scale_input_and_euler_step():
     xin = torch.empty(nt * 2, k * k, 4, dtype=torch.bfloat16, device=DEV)
     ops.tlc_scale_input(canvas, rows, cols, H, W, k, k, 0, nt, 2, sig, xin)
     tiles = torch.stack([canvas[:, r:r + k, c:c + k] for r in rows.tolist() for c in cols.tolist()])
-    ref_in = S.euler_scale(tiles, sig).permute(0, 2, 3, 1).reshape(nt, k * k, 4)
-    torch.testing.assert_close(xin.view(nt, 2, k * k, 4)[:, 0].float(), ref_in.to(torch.bfloat16).float())
-    torch.testing.assert_close(xin.view(nt, 2, k * k, 4)[:, 1].float(), ref_in.to(torch.bfloat16).float())
+    # reference on the host: tensor / tensor true division (a device tensor / python scalar multiplies by the
+    # reciprocal, which is not what scale_model_input computes)
+    ref_in = (tiles.cpu() / ((torch.tensor(sig) ** 2 + 1) ** 0.5)).permute(0, 2, 3, 1).reshape(nt, k * k, 4).to(DEV)
+    assert torch.equal(xin.view(nt, 2, k * k, 4)[:, 0], ref_in.to(torch.bfloat16))
+    assert torch.equal(xin.view(nt, 2, k * k, 4)[:, 1], ref_in.to(torch.bfloat16))
     eps = rnd(nt * 2, k * k, 4)
     out = torch.empty(nt, 4, k, k, device=DEV)
     ops.tlc_cfg_euler_step(eps, canvas, rows, cols, H, W, k, k, 0, nt, 2, g, 0.0, sig, sig_n, out)
