@@ -17,6 +17,7 @@ run on the HIP kernels (fdhip/clip.py) when built by from_pretrained, with a see
 only for pipelines constructed without them.
 """
 import inspect
+import os
 import zlib
 from types import SimpleNamespace
 from typing import Any, Callable, Dict, List, Optional, Tuple, Union
@@ -86,7 +87,9 @@ class FaithDiffStableDiffusionXLPipeline:
         self.default_sample_size = 128
         self.watermark = None
         self.device = torch.device("cpu")
-        self.tile_batch = 4          # TLC tiles per UNet forward (B = 2 * tile_batch rows)
+        # TLC tiles per UNet forward (B = 2 * tile_batch rows; C3 4096^2: 4 -> 13 tiles = 51.6 -> 53.2 tile-steps/s,
+        # scripts/tb_sweep.sh); FD_TILE_BATCH overrides (A/B timing)
+        self.tile_batch = int(os.environ.get("FD_TILE_BATCH", "13"))
         self.process_group = None    # torch.distributed group for tile parallelism (None: single GPU)
         self.last_timings = {}
 
