@@ -70,6 +70,47 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// GroupNorm statistics of a 256-row GEMM / conv output tile (fd_gemm_params.gn_part): in the vector epilogue
+// each thread owns one 8-column chunk (NTHR % VPR == 0), whose columns fall in at most two groups (cpg >= 4 and
+// the tile's first column a multiple of cpg); sums of the STORED values, then one fixed-order reduction per group.
+struct GnTile {
+  float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
+  template <typename TO8>
+  __device__ __forceinline__ void add(const TO8& o, int split) {  // chunk columns < split: the first group
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float f = (float)o[i];
+      if (i < split) {
+        s0 += f;
+        q0 += f * f;
+      } else {
+        s1 += f;
+        q1 += f * f;
+      }
+    }
+  }
+};
+// red: 2 * nthr float2 of LDS no other thread still reads; every thread of the workgroup calls this
+__device__ __forceinline__ void gn_tile_write(const GnTile& a, float2* red, int tid, int nthr, int vpr, int cpg,
+                                              int ncols, int n0, int m0, const fd_gemm_params& p) {
+  red[2 * tid] = make_float2(a.s0, a.q0);
+  red[2 * tid + 1] = make_float2(a.s1, a.q1);
+  __syncthreads();
+  if (tid < ncols / cpg) {
+    float s = 0.f, q = 0.f;
+    for (int c = tid * cpg / 8; c <= ((tid + 1) * cpg - 1) / 8; ++c) {
+      const int slot = (c * 8) / cpg == tid ? 0 : 1;
+      for (int k = c; k < nthr; k += vpr) {
+        const float2 v = red[2 * k + slot];
+        s += v.x;
+        q += v.y;
+      }
+    }
+    const long long blk = (long long)(m0 / p.gn_hw) * (p.gn_hw / 256) + (m0 % p.gn_hw) / 256;
+    ((float2*)p.gn_part)[blk * p.gn_groups + n0 / cpg + tid] = make_float2(s, q);
+  }
+}
+
 #define FD_LAUNCH_CHECK()                                  \
   do {                                                     \
     if (hipGetLastError() != hipSuccess) return FD_ERR_HIP; \

@@ -607,11 +607,12 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
   }
 }
 
-extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream);    // gemm8.hip
-extern "C" int fd_gemm256_try(const fd_gemm_params* p, void* stream);  // gemm256.hip
+extern "C" int fd_gemm8_try(fd_gemm_params* p, void* stream);    // gemm8.hip
+extern "C" int fd_gemm256_try(fd_gemm_params* p, void* stream);  // gemm256.hip
 
-extern "C" int fd_gemm(const fd_gemm_params* p, void* stream) {
+extern "C" int fd_gemm(fd_gemm_params* p, void* stream) {
   if (!p || !p->A || !p->B || !p->C) return FD_ERR_ARG;
+  p->gn_done = 0;  // set by the 256-row kernels when they wrote the GroupNorm statistics (gn_part)
   if (p->M <= 0 || p->N <= 0 || p->K <= 0 || (p->K % 64) != 0) return FD_ERR_SHAPE;
   if (p->act == FD_ACT_GEGLU && (p->N % 32) != 0) return FD_ERR_SHAPE;
   if (p->rowbias && p->rows_per_group <= 0) return FD_ERR_ARG;

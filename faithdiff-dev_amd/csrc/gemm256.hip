@@ -51,6 +51,8 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
   constexpr int LDE = BN + 4;
   constexpr int EROWS = 128;
   static_assert(EROWS * LDE * 4 <= NSL * SLOT, "epilogue staging");
+  constexpr int RED_OFF = ((EROWS * LDE * 4 + 15) / 16) * 16;  // GroupNorm statistics scratch (gn_part)
+  static_assert(RED_OFF + 16 * NTHR <= NSL * SLOT, "GroupNorm reduction scratch");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NSL * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -252,6 +254,11 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
                    (!rbias || ((p.rowbias_ld % 4 == 0) && ((((unsigned long long)rbias) & 15) == 0)));
   const bool interior = vec && (m0 + BM <= M);
   typedef __attribute__((ext_vector_type(8))) TO TO8;
+  // GroupNorm statistics (fd_gemm_params.gn_part; host: interior, group-aligned tiles): chunk tid % VPR per thread
+  const bool gn = p.gn_part != nullptr;
+  const int gcpg = gn ? p.N / p.gn_groups : 8;
+  const int gsplit = (((tid % VPR) * 8) / gcpg + 1) * gcpg - (tid % VPR) * 8;
+  GnTile gna;
 #pragma unroll 1
   for (int half = 0; half < BM / EROWS; ++half) {
     if (half) __syncthreads();  // the previous half's staging fully consumed
@@ -322,6 +329,7 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
           *(TO8*)(C + (long long)m * p.ldc + n) = o;
+          if (gn) gna.add(o, gsplit);
         }
       }
     } else {  // ragged last row tile / unaligned operands: scalar, bounds-checked
@@ -340,6 +348,7 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
       }
     }
   }
+  if (gn) gn_tile_write(gna, (float2*)(smem + RED_OFF), tid, NTHR, VPR, gcpg, BN, n0, m0, p);
 }
 
 int env256(const char* n, int d) {
@@ -353,7 +362,23 @@ int env256(const char* n, int d) {
 // N % 256 == 0, no GEGLU / LayerNorm fold / batching, and at least 192 tiles of 256 x 256 counted from the
 // per-TLC-tile row count m_ref (so batching tiles never changes the kernel choice: bitwise batch-invariant).
 // FD_GEMM256=0 disables it (A/B timing).
-extern "C" int fd_gemm256_try(const fd_gemm_params* p, void* stream) {
+extern "C" int fd_gemm256_try(fd_gemm_params* p0, void* stream) {
+  fd_gemm_params q = *p0;  // the kernel's copy: gn_part kept only where the statistics can be written
+  {
+    const fd_gemm_params* p = p0;
+    bool ok = p->gn_part && p->gn_groups > 0 && p->gn_hw > 0 && p->N % p->gn_groups == 0;
+    if (ok) {
+      const int cpg = p->N / p->gn_groups;
+      const unsigned long long al = (unsigned long long)p->C | (p->residual ? (unsigned long long)p->residual : 0) |
+                                    (p->bias ? (unsigned long long)p->bias : 0) |
+                                    (p->rowbias ? (unsigned long long)p->rowbias : 0);
+      ok = cpg >= 4 && 256 % cpg == 0 && p->M % 256 == 0 && p->gn_hw % 256 == 0 && p->M % p->gn_hw == 0 &&
+           (al & 15) == 0 && p->ldc % 8 == 0 && (!p->residual || p->ldr % 8 == 0) &&
+           (!p->rowbias || p->rowbias_ld % 4 == 0);
+    }
+    if (!ok) q.gn_part = nullptr;
+  }
+  const fd_gemm_params* p = &q;
   static int min_tiles = -1;
   if (min_tiles < 0) min_tiles = env256("FD_GEMM256_MIN_TILES", 192);
   const int enabled = env256("FD_GEMM256", 1);  // read per call: tests compare against gemm8 in one process
@@ -394,5 +419,6 @@ extern "C" int fd_gemm256_try(const fd_gemm_params* p, void* stream) {
       hipLaunchKernelGGL((gemm256_kernel<T, TO, false, 8>), grid, block, 0, s, *p, gm);
   }));
   FD_LAUNCH_CHECK();
+  if (rc == FD_OK) p0->gn_done = q.gn_part != nullptr;
   return rc == FD_OK ? 1 : rc;
 }

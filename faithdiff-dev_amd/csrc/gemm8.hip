@@ -69,6 +69,10 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   constexpr int SMEM = LNC_OFF + (LNF ? BM * 8 + BN * 4 : 0);
   static_assert(SMEM <= 163840, "LDS");
   static_assert(!GEGLU || (WN % 32 == 0), "GEGLU pairs must not straddle waves");
+  // GroupNorm output statistics (fd_gemm_params.gn_part): one 8-column chunk per thread, reduction scratch after the
+  // epilogue staging
+  constexpr int RED_OFF = ((EPB + 15) / 16) * 16;
+  constexpr bool GN_OK = !GEGLU && !LNF && BM == 256 && (NTHR % (BNO / 8)) == 0 && RED_OFF + 16 * NTHR <= SMEM;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   float2* const ln_tab = (float2*)(smem + LNC_OFF);
   float* const ln_cs = (float*)(smem + LNC_OFF + BM * 8);
@@ -476,6 +480,12 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
                    (GEGLU || !rbias || ((p.rowbias_ld % 4 == 0) && ((((unsigned long long)rbias) & 15) == 0)));
   const bool interior = vec && (m0 + BM <= M) && (n0o + BNO <= Nout);
   typedef __attribute__((ext_vector_type(8))) TO TO8;
+  // GroupNorm statistics: this thread's chunk (tid % VPR) is the same in every row pass (NTHR % VPR == 0);
+  // gsplit = its columns in the chunk's first group (the host only asks for interior, group-aligned tiles)
+  const bool gn = GN_OK && p.gn_part != nullptr;
+  const int gcpg = gn ? p.N / p.gn_groups : 8;
+  const int gsplit = (((tid % VPR) * 8) / gcpg + 1) * gcpg - (tid % VPR) * 8;
+  GnTile gna;
 #pragma unroll 1
   for (int half = 0; half < BM / EROWS; ++half) {
     __syncthreads();  // ring (half 0) / previous half's staging (half 1) fully consumed
@@ -581,6 +591,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
         *(TO8*)(C + (long long)m * p.ldc + n) = o;
+        if (gn) gna.add(o, gsplit);
       }
     }
     } else {  // edge tiles / unaligned operands: scalar, bounds-checked
@@ -604,6 +615,9 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         }
       }
     }
+  }
+  if constexpr (GN_OK) {
+    if (gn) gn_tile_write(gna, (float2*)(smem + RED_OFF), tid, NTHR, VPR, gcpg, BNO, n0o, m0, p);
   }
 }
 
@@ -777,10 +791,26 @@ extern "C" long long fd_gemm_ws_bytes(const fd_gemm_params* p) {
   return 65536LL * sizeof(unsigned) + (long long)pl.tiles * pl.S * slab;
 }
 
+// GroupNorm output statistics (fd_gemm_params.gn_part) from the 256 x 128 instance's vector epilogue: every
+// tile interior, inside one image and a whole number of groups wide.
+static bool gn_ok8(const fd_gemm_params* p, const Plan8& pl) {
+  if (!p->gn_part || pl.bm != 256 || pl.bn != 128 || p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out) return false;
+  if (p->gn_groups <= 0 || p->gn_hw <= 0 || p->N % p->gn_groups) return false;
+  const int cpg = p->N / p->gn_groups;
+  if (cpg < 4 || 128 % cpg || p->N % 128 || p->M % 256 || p->gn_hw % 256 || p->M % p->gn_hw) return false;
+  const unsigned long long al = (unsigned long long)p->C | (p->residual ? (unsigned long long)p->residual : 0) |
+                                (p->bias ? (unsigned long long)p->bias : 0) | (p->rowbias ? (unsigned long long)p->rowbias : 0);
+  return (al & 15) == 0 && p->ldc % 8 == 0 && (!p->residual || p->ldr % 8 == 0) &&
+         (!p->rowbias || p->rowbias_ld % 4 == 0);
+}
+
 // Returns 1 and launches when the eight-wave kernel takes this GEMM, 0 when it does not apply, < 0 on error.
-extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream) {
+extern "C" int fd_gemm8_try(fd_gemm_params* p0, void* stream) {
   Plan8 pl;
-  if (!plan8(p, &pl)) return 0;
+  if (!plan8(p0, &pl)) return 0;
+  fd_gemm_params q = *p0;  // the kernel's copy: gn_part kept only where this instance writes the statistics
+  if (!gn_ok8(p0, pl)) q.gn_part = nullptr;
+  const fd_gemm_params* p = &q;
   if (pl.S > 1) {
     const long long need = 65536LL * sizeof(unsigned) + (long long)pl.tiles * pl.S * pl.bm * pl.bn * 4;
     if (!p->ws || p->ws_bytes < need) return FD_ERR_ARG;
@@ -803,5 +833,6 @@ extern "C" int fd_gemm8_try(const fd_gemm_params* p, void* stream) {
     FD_G8(64, 160, 4, 2, 3);
   }
 #undef FD_G8
+  if (rc == FD_OK) p0->gn_done = q.gn_part != nullptr;
   return rc == FD_OK ? 1 : rc;
 }

@@ -234,6 +234,29 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
   return FD_OK;
 }
 
+// GroupNorm whose statistics the producing GEMM / conv epilogue already wrote (fd_gemm_params.gn_part, gn_done):
+// part[(img * HW/256 + b) * groups + g] = (sum, sumsq) of the 256-row block b.  Finalize (fp64 fold, fixed order)
+// into stats (nimg * groups float2, caller's) + apply: the gn_partial pass (one full read of x) is gone.
+extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW,
+                                      int C, int groups, float eps, int silu, const void* part, void* stats,
+                                      int dtype, void* stream) {
+  if (!x || !y || !part || !stats) return FD_ERR_ARG;
+  if (nimg <= 0 || HW <= 0 || HW % 256 || C <= 0 || groups <= 0 || groups > 64 || C % groups || C % 8 ||
+      C > GN_MAXC)
+    return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)part, (float2*)stats, HW,
+                     C, groups, HW / 256, eps);
+  FD_LAUNCH_CHECK();
+  int rpb = 1;
+  while ((long long)nimg * ((HW + rpb - 1) / rpb) > 1024) rpb *= 2;
+  const int nblk = (HW + rpb - 1) / rpb;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
+                                          (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb, silu));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // LayerNorm: one wave per row, 4 rows per 256-thread block; row kept in registers (C <= 2048).
 // Q8: instead of y, write the row quantized to e4m3 for fd_gemm_e4m3 (the use_fp8 model): the LayerNorm output is

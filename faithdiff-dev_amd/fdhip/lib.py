@@ -35,6 +35,7 @@ class GemmParams(ctypes.Structure):
         ("A2", c_vp), ("C1", c_int),
         ("m_ref", c_int), ("ws", c_vp), ("ws_bytes", c_ll),
         ("ln_out", c_vp), ("ln_in", c_vp), ("ln_c", c_vp), ("ln_eps", c_f),
+        ("gn_part", c_vp), ("gn_groups", c_int), ("gn_hw", c_int), ("gn_done", c_int),
     ]
 
 
@@ -46,6 +47,8 @@ _SIGS = {
                                  c_int, c_int, c_vp]),
     "fd_group_norm_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),
     "fd_group_norm": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_int, c_int, c_vp, c_vp]),
+    "fd_group_norm_partials": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_int, c_vp, c_vp,
+                                       c_int, c_vp]),
     "fd_gemm_e4m3": (c_int, [c_vp, c_ll, c_vp, c_vp, c_ll, c_f, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_ll,
                              c_int, c_int, c_vp]),
     "fd_layer_norm_e4m3": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp]),

@@ -139,9 +139,29 @@ def _launch_gemm(p, what):
     _timed("gemm", flops, 0.0, lambda: L.check(L.load().fd_gemm(ctypes.byref(p), L.stream()), what), label)
 
 
+class GnStats:
+    """GroupNorm statistics asked of the GEMM / conv that produces the GroupNorm's input (fd_gemm_params.gn_part):
+    pass it as ``gn=`` to gemm / conv3x3 and as ``stats=`` to group_norm.  ``done`` is set at launch when the
+    chosen kernel wrote them (256-row tiles, group-aligned, H*W % 256 == 0); otherwise group_norm computes its own.
+    The decision depends only on shapes, so it is the same in every replay of a captured graph."""
+
+    def __init__(self, nimg, HW, groups, device):
+        self.nimg, self.HW, self.groups = nimg, HW, groups
+        self.part = torch.empty((max(nimg * (HW // 256) * groups * 2, 2),), dtype=torch.float32, device=device)
+        self.done = False
+
+    def attach(self, p):
+        self.done = False
+        if self.HW % 256 == 0 and p.M == self.nimg * self.HW:
+            p.gn_part, p.gn_groups, p.gn_hw = self.part.data_ptr(), self.groups, self.HW
+
+    def collect(self, p):
+        self.done = bool(p.gn_part) and bool(p.gn_done)
+
+
 def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=1, alpha=1.0, act="none",
          out_dtype=None, batch=1, M=None, N=None, K=None, lda=None, ldw=None, ldc=None, ldr=None,
-         stride_a=0, stride_w=0, stride_c=0, stride_r=0, ln_out=None, ln_in=None, ln_c=None, ln_eps=1e-5):
+         stride_a=0, stride_w=0, stride_c=0, stride_r=0, ln_out=None, ln_in=None, ln_c=None, ln_eps=1e-5, gn=None):
     """out[M, N (N/2 for geglu)] = epi(alpha * a[M, K] @ w[N, K]^T); strides default to the tensors'.
     ln_out: fp32 [M, N/160, 2] -- also write per-row (sum, sumsq) partials of the stored output (LayerNorm
     producer).  ln_in / ln_c: fold LayerNorm(a) into this GEMM (w = W * gamma, ln_c = rowsum(w), bias =
@@ -177,8 +197,12 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
         p.ln_out = ln_out.data_ptr()
     if ln_in is not None:
         p.ln_in, p.ln_c, p.ln_eps = ln_in.data_ptr(), ln_c.data_ptr(), ln_eps
+    if gn is not None and batch == 1:
+        gn.attach(p)
     _attach_ws(p, a.device)
     _launch_gemm(p, "fd_gemm")
+    if gn is not None:
+        gn.collect(p)
     return out
 
 
@@ -255,7 +279,7 @@ def fold_layer_norm(w, gamma, beta, bias=None, dtype=torch.bfloat16):
 
 
 def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C1=None, out=None, rowbias=None,
-            residual=None, act="none", out_dtype=None, upsample_size=None):
+            residual=None, act="none", out_dtype=None, upsample_size=None, gn=None):
     """Implicit-GEMM 3x3 conv on NHWC x [nimg*H*W, Cin] (or concat(x, x2) along C) with packed weight wp.
     upsample=True: nearest-resize to upsample_size (default 2H x 2W) folded into the gather."""
     Cout, K = wp.shape
@@ -287,8 +311,12 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
     p.conv, p.nimg, p.Hin, p.Win, p.Cin = 1, nimg, H, W, Cin
     p.Hout, p.Wout, p.stride, p.pad, p.upsample = Hout, Wout, stride, pad, int(upsample)
     p.A2 = x2.data_ptr() if x2 is not None else None
+    if gn is not None:
+        gn.attach(p)
     _attach_ws(p, x.device)
     _launch_gemm(p, "fd_gemm(conv)")
+    if gn is not None:
+        gn.collect(p)
     return out
 
 
@@ -306,9 +334,20 @@ def conv_direct(x, w, bias, nimg, H, W, Cin, ksize=3, stride=1, pad=1, in_scale=
 
 
 # --------------------------------------------------------------------------------------- norms
-def group_norm(x, gamma, beta, nimg, HW, C, groups=32, eps=1e-5, silu=False, out=None):
+def group_norm(x, gamma, beta, nimg, HW, C, groups=32, eps=1e-5, silu=False, out=None, stats=None):
+    """GroupNorm (+SiLU) of NHWC x.  stats: a GnStats the producer of x filled (gn=...): the statistics pass is
+    skipped (fd_group_norm_partials)."""
     if out is None:
         out = torch.empty_like(x)
+    if stats is not None and stats.done:
+        if (stats.nimg, stats.HW, stats.groups) != (nimg, HW, groups):
+            raise ValueError("group_norm: stats were gathered for a different shape")
+        st = _gn_ws(nimg * groups * 8, x.device)
+        _timed("group_norm", 0, 2.0 * nimg * HW * C * x.element_size(), lambda: L.check(
+            L.load().fd_group_norm_partials(L.ptr(x), L.ptr(out), L.ptr(gamma), L.ptr(beta), nimg, HW, C, groups, eps,
+                                            int(silu), L.ptr(stats.part), L.ptr(st), L.dtype_code(x.dtype),
+                                            L.stream()), "fd_group_norm_partials"))
+        return out
     nb = L.load().fd_group_norm_ws_bytes(nimg, HW, C, groups)
     ws = _gn_ws(nb, x.device)
     _timed("group_norm", 0, 2.0 * nimg * HW * C * x.element_size(), lambda: L.check(

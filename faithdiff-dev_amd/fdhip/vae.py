@@ -56,21 +56,26 @@ class _Trunk:
                     out=(self.w(p + ".to_out.0.weight"), self.f32(p + ".to_out.0.bias")))
 
 
-def run_resnet(r, x, n, H, W, dtype, device):
+def run_resnet(r, x, n, H, W, dtype, device, stats=None):
+    """ResnetBlock2D.  stats: GroupNorm statistics of x written by its producer (ops.GnStats), None = computed by
+    the GroupNorm.  Returns (out, GnStats of out from conv2's epilogue, for the next GroupNorm)."""
     HW = H * W
-    h = ops.group_norm(x, *r["n1"], n, HW, r["cin"], 32, 1e-6, silu=True)
-    h = ops.conv3x3(h, *r["c1"], n, H, W)
-    ops.group_norm(h, *r["n2"], n, HW, r["cout"], 32, 1e-6, silu=True, out=h)
+    h = ops.group_norm(x, *r["n1"], n, HW, r["cin"], 32, 1e-6, silu=True, stats=stats)
+    s1 = ops.GnStats(n, HW, 32, x.device)
+    h = ops.conv3x3(h, *r["c1"], n, H, W, gn=s1)
+    ops.group_norm(h, *r["n2"], n, HW, r["cout"], 32, 1e-6, silu=True, out=h, stats=s1)
     sc = ops.gemm(x, r["sc"][0], bias=r["sc"][1]) if "sc" in r else x
-    return ops.conv3x3(h, *r["c2"], n, H, W, residual=sc)
+    s2 = ops.GnStats(n, HW, 32, x.device)
+    return ops.conv3x3(h, *r["c2"], n, H, W, residual=sc, gn=s2), s2
 
 
-def run_attn(a, x, n, H, W):
+def run_attn(a, x, n, H, W, stats=None):
     """Single-head d=C attention with residual (diffusers Attention, AttnProcessor2_0): GroupNorm -> fused QKV
-    projection -> fd_flash_attn_d512 (no [T, T] buffers) -> out projection + residual."""
+    projection -> fd_flash_attn_d512 (no [T, T] buffers) -> out projection + residual.  stats / returns: as
+    run_resnet."""
     C = a["out"][0].shape[0]
     T = H * W
-    h = ops.group_norm(x, *a["gn"], n, T, C, 32, 1e-6, silu=False)
+    h = ops.group_norm(x, *a["gn"], n, T, C, 32, 1e-6, silu=False, stats=stats)
     qkv = ops.gemm(h, a["qkv"][0], bias=a["qkv"][1])  # [n*T, 3C]
     out = torch.empty((n * T, C), dtype=x.dtype, device=x.device)
     if C == 512:
@@ -87,7 +92,8 @@ def run_attn(a, x, n, H, W):
             ops.softmax_rows(S, P, T, T, 1.0, ldp=Tp)
             ops.transpose(q[:, 2 * C:], 3 * C, Vt, Tp, T, C)
             ops.gemm(P, Vt, out=out[i * T:(i + 1) * T], K=Tp)
-    return ops.gemm(out, a["out"][0], bias=a["out"][1], residual=x)
+    so = ops.GnStats(n, T, 32, x.device)
+    return ops.gemm(out, a["out"][0], bias=a["out"][1], residual=x, gn=so), so
 
 
 class HipEncoder:
@@ -131,17 +137,19 @@ class HipEncoder:
         """x: NHWC [n*H*W, 3] (dtype) in [-1, 1].  Returns NHWC [n*(H/8)*(W/8), 8 or 512]."""
         h = ops.conv_direct(x, *self.conv_in, n, H, W, 3, 3, 1, 1, out_dtype=self.dtype)
         hh, ww = H, W
+        st = None  # GroupNorm statistics of h from its producer (ops.GnStats)
         for rs, ds in self.blocks:
             for r in rs:
-                h = run_resnet(r, h, n, hh, ww, self.dtype, self.device)
+                h, st = run_resnet(r, h, n, hh, ww, self.dtype, self.device, st)
             if ds is not None:
-                h = ops.conv3x3(h, *ds, n, hh, ww, stride=2, pad=0)
+                st = ops.GnStats(n, (hh // 2) * (ww // 2), 32, h.device)
+                h = ops.conv3x3(h, *ds, n, hh, ww, stride=2, pad=0, gn=st)
                 hh, ww = hh // 2, ww // 2
-        h = run_resnet(self.mid[0], h, n, hh, ww, self.dtype, self.device)
-        h = run_attn(self.mid[1], h, n, hh, ww)
-        h = run_resnet(self.mid[2], h, n, hh, ww, self.dtype, self.device)
+        h, st = run_resnet(self.mid[0], h, n, hh, ww, self.dtype, self.device, st)
+        h, st = run_attn(self.mid[1], h, n, hh, ww, st)
+        h, st = run_resnet(self.mid[2], h, n, hh, ww, self.dtype, self.device, st)
         if self.with_out:
-            h = ops.group_norm(h, *self.norm_out, n, hh * ww, 512, 32, 1e-6, silu=True)
+            h = ops.group_norm(h, *self.norm_out, n, hh * ww, 512, 32, 1e-6, silu=True, stats=st)
             h = ops.conv3x3(h, *self.conv_out, n, hh, ww)
             h = ops.conv_direct(h, *self.quant, n, hh, ww, 8, 1, 1, 0, out_dtype=self.dtype)
         return h
@@ -176,15 +184,16 @@ class HipDecoder:
         """z: NHWC [n*h*w, 4] (already divided by scaling_factor).  Returns NHWC [n*8h*8w, 3] (dtype)."""
         x = ops.conv_direct(z, *self.post_quant, n, h, w, 4, 1, 1, 0, out_dtype=self.dtype)
         x = ops.conv_direct(x, *self.conv_in, n, h, w, 4, 3, 1, 1, out_dtype=self.dtype)
-        x = run_resnet(self.mid[0], x, n, h, w, self.dtype, self.device)
-        x = run_attn(self.mid[1], x, n, h, w)
-        x = run_resnet(self.mid[2], x, n, h, w, self.dtype, self.device)
+        x, st = run_resnet(self.mid[0], x, n, h, w, self.dtype, self.device)
+        x, st = run_attn(self.mid[1], x, n, h, w, st)
+        x, st = run_resnet(self.mid[2], x, n, h, w, self.dtype, self.device, st)
         hh, ww = h, w
         for rs, us in self.blocks:
             for r in rs:
-                x = run_resnet(r, x, n, hh, ww, self.dtype, self.device)
+                x, st = run_resnet(r, x, n, hh, ww, self.dtype, self.device, st)
             if us is not None:
-                x = ops.conv3x3(x, *us, n, hh, ww, upsample=True)
+                st = ops.GnStats(n, 4 * hh * ww, 32, x.device)
+                x = ops.conv3x3(x, *us, n, hh, ww, upsample=True, gn=st)
                 hh, ww = hh * 2, ww * 2
-        x = ops.group_norm(x, *self.norm_out, n, hh * ww, 128, 32, 1e-6, silu=True)
+        x = ops.group_norm(x, *self.norm_out, n, hh * ww, 128, 32, 1e-6, silu=True, stats=st)
         return ops.conv3x3(x, *self.conv_out, n, hh, ww)

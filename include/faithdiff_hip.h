@@ -91,9 +91,20 @@ typedef struct fd_gemm_params {
   const float* ln_in;
   const float* ln_c;
   float ln_eps;
+  /* GroupNorm statistics of the output for the GroupNorm that consumes it (VAE / UNet resnets: conv2 -> next
+   * norm1, conv1 -> norm2; replaces the gn_partial pass of fd_group_norm).  Request: gn_part != NULL,
+   * gn_groups = G, gn_hw = rows per image.  When the chosen kernel can produce them (256-row tiles, every tile
+   * inside one image: gn_hw % 256 == 0, its columns a whole number of groups, the vector epilogue; no GEGLU /
+   * LayerNorm fold) fd_gemm writes, per image i, 256-row block b and group g, (sum, sum of squares) of the
+   * STORED outputs to gn_part[(i * gn_hw / 256 + b) * G + g] (float2) and sets gn_done = 1, else 0 (then the
+   * consumer runs the full fd_group_norm).  Consumer: fd_group_norm_partials. */
+  float* gn_part;
+  int gn_groups;
+  int gn_hw;
+  int gn_done;
 } fd_gemm_params;
 
-int fd_gemm(const fd_gemm_params* p, void* stream);
+int fd_gemm(fd_gemm_params* p, void* stream);  /* writes only p->gn_done */
 /* Workspace fd_gemm needs for this launch (0 = none). */
 long long fd_gemm_ws_bytes(const fd_gemm_params* p);
 
@@ -114,6 +125,12 @@ int fd_conv2d_direct(const void* x, const float* w, const float* bias, void* y, 
 long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups);
 int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
                   int groups, float eps, int silu, int dtype, void* ws, void* stream);
+/* fd_group_norm when the producing fd_gemm wrote the statistics (fd_gemm_params.gn_part with gn_done = 1):
+ * part [nimg][HW / 256][groups] float2 (sum, sumsq); stats: nimg * groups float2 of caller memory.  HW % 256 == 0.
+ * Saves the statistics pass over x (one full read).  Same arithmetic as fd_group_norm except the summation
+ * order of the statistics. */
+int fd_group_norm_partials(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
+                           int groups, float eps, int silu, const void* part, void* stats, int dtype, void* stream);
 
 /* LayerNorm fused with the per-row e4m3 quantization of fd_quant_rows_e4m3 (use_fp8 model): the row is
  * normalised, rounded to dtype, then q[m][:] = e4m3_RNE(y * 448 / amax_m), scale[m] = amax_m / 448 -- bitwise

@@ -346,3 +346,30 @@ def test_flash_attn_d512(dtype, n, T):
     q, k, v = x[..., :C], x[..., C:2 * C], x[..., 2 * C:]
     ref = F.scaled_dot_product_attention(q[:, None], k[:, None], v[:, None])[:, 0].reshape(n * T, C)
     assert rel_l2(o, ref) < 1.5 * TOL[dtype], rel_l2(o, ref)
+
+
+@pytest.mark.parametrize("nimg,H,W,Cin,Cout,up,expect", [
+    (1, 128, 128, 256, 512, False, True),   # gemm8 256x128 (the 512-ch VAE level), cpg 16
+    (1, 128, 128, 128, 256, True, True),    # gemm256 upsample conv (256^2 out), cpg 8
+    (2, 128, 128, 128, 256, False, True),   # gemm256, two images
+    (1, 256, 256, 128, 128, False, True),   # gemm8 256x128, cpg 4 (chunks straddle groups)
+    (2, 16, 16, 320, 320, False, False),    # cpg 10: statistics left to the GroupNorm
+    (1, 24, 20, 128, 128, False, False)])   # H*W % 256 != 0
+def test_conv_groupnorm_statistics_from_epilogue(nimg, H, W, Cin, Cout, up, expect):
+    """A conv asked for its output's GroupNorm statistics (ops.GnStats -> fd_gemm_params.gn_part) + group_norm
+    from them (fd_group_norm_partials) == group_norm computing its own statistics, up to the summation order."""
+    from fdhip import ops
+    x = rnd(nimg * H * W, Cin, dtype=torch.float16)
+    w = (torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)).to(torch.float16)
+    b = torch.randn(Cout, device=DEV) * 0.3
+    res = rnd(nimg * H * W * (4 if up else 1), Cout, dtype=torch.float16)
+    Ho, Wo = (2 * H, 2 * W) if up else (H, W)
+    st = ops.GnStats(nimg, Ho * Wo, 32, DEV)
+    y = ops.conv3x3(x, ops.pack_conv3x3(w), b, nimg, H, W, upsample=up, residual=res, gn=st)
+    assert st.done == expect
+    g, be = torch.randn(Cout, device=DEV), torch.randn(Cout, device=DEV)
+    got = ops.group_norm(y, g, be, nimg, Ho * Wo, Cout, 32, 1e-6, silu=True, stats=st)
+    want = ops.group_norm(y, g, be, nimg, Ho * Wo, Cout, 32, 1e-6, silu=True)
+    ref = F.silu(F.group_norm(y.float().view(nimg, Ho * Wo, Cout).permute(0, 2, 1), 32, g, be, 1e-6)).permute(0, 2, 1)
+    assert rel_l2(got, want) < 2e-3
+    assert rel_l2(got, ref.reshape(-1, Cout)) < 6e-3
