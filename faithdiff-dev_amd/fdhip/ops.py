@@ -10,12 +10,22 @@ import torch
 from . import lib as L
 
 _GN_WS = {}
+# Every workspace buffer ever handed out stays allocated: a hipGraph captured while it was current keeps its
+# address and writes there on every replay, so freeing it on growth (and letting the caching allocator hand the
+# memory to another tensor) would let an old graph's replay corrupt that tensor.  Workspaces never grow inside a
+# capture (the graph cache runs every shape eagerly first, which sizes them).
+_WS_KEEP = []
 
 
 def _gn_ws(nbytes, device):
     key = device
     ws = _GN_WS.get(key)
     if ws is None or ws.numel() < nbytes:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"GroupNorm workspace too small inside graph capture ({nbytes} B): run the shape "
+                               "once eagerly or call ops.reserve_gn_workspace first")
+        if ws is not None:
+            _WS_KEEP.append(ws)
         ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _GN_WS[key] = ws
     return ws
@@ -53,6 +63,7 @@ def reserve_gemm_workspace(nbytes, device):
     if ws is None or ws.numel() < nbytes:
         if ws is not None:
             torch.cuda.synchronize(key)
+            _WS_KEEP.append(ws)  # graphs captured with it may replay later (its tile counters stay zero)
         _GEMM_WS[key] = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=key)
     return _GEMM_WS[key]
 

@@ -127,3 +127,40 @@ def test_call_tile_parallel_two_ranks_one_gpu_bitwise():
     for rank, lat, img in res:
         assert (lat == lat_ref).all(), f"rank {rank}: latents differ from the single-process run"
         assert (img == img_ref).all(), f"rank {rank}: image differs from the single-process run"
+
+
+def test_c3_49_tiles_tile_batch_bitwise():
+    """BASELINE configs[2] shape on the GPU: a 4096^2 input restored at target 1024 (latent 512^2 -> 49 TLC tiles,
+    tiled VAE encode / decode and tiled denoise encoder at their default 1024-px tiles), one Euler step, through
+    the product __call__.  The tiles are batched 13 and 4 per UNet forward: every latent and pixel must be equal
+    (a tile's rows never depend on which tiles share its forward; m_ref keeps the kernel choices per tile)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from _det import det_tensor, synthetic_degraded
+    pipe, _ = _reference()
+    vae = pipe.vae
+    saved = (vae.tile_sample_min_size, vae.tile_latent_min_size, pipe.tile_batch)
+    vae.tile_sample_min_size, vae.tile_latent_min_size = 1024, 128
+    S = 4096
+    img = synthetic_degraded(S, S, 9)
+    noise, post = det_tensor((1, 4, S // 8, S // 8), 41), det_tensor((1, 4, S // 8, S // 8), 42)
+    res = []
+    try:
+        for tb in (13, 4):
+            pipe.tile_batch = tb
+            cap = {}
+
+            def cb(p, i, t, kw):
+                cap["lat"] = kw["latents"].detach().float().cpu().clone()
+                return {}
+            out = pipe(lr_img=img, prompt="a tiled floor", negative_prompt="", num_inference_steps=1,
+                       guidance_scale=5.0, start_point="lr", height=S, width=S, overlap=0.5,
+                       target_size=(1024, 1024), latents=noise, posterior_noise=post, callback_on_step_end=cb,
+                       output_type="pil").images
+            res.append((cap["lat"], np.asarray(out[0])))
+    finally:
+        vae.tile_sample_min_size, vae.tile_latent_min_size, pipe.tile_batch = saved
+    assert res[0][0].shape == (1, 4, 512, 512) and res[0][1].shape == (S, S, 3)
+    assert torch.equal(res[0][0], res[1][0])
+    assert (res[0][1] == res[1][1]).all()
+    assert res[0][1].std() > 1.0
