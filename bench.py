@@ -337,18 +337,26 @@ def cpu_baseline(size):
 
 
 def run_pipeline_image(pipe, img, H, W, steps, target, seed=42):
-    """One product ``pipe(...)`` call as test_wo_llava.py:86 makes it; returns (s, EventTimer)."""
+    """One product ``pipe(...)`` call as test_wo_llava.py:86 makes it; returns (s, EventTimer).  The final latents
+    are checked for non-finite values after the timed call (tm.finite)."""
     tm = EventTimer()
     gen = torch.Generator(device=pipe.device).manual_seed(seed)
+    last = {}
+
+    def keep(p, i, t, kw):  # keeps a reference only; inspected after the clock stops
+        last["lat"] = kw["latents"]
+        return {}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     tm("call_start", 0)
     pipe(lr_img=img, prompt="A high quality photo restored from a degraded capture.", negative_prompt="",
          num_inference_steps=steps, guidance_scale=5.0, generator=gen, start_point="lr", height=H, width=W,
-         overlap=0.5, target_size=target, timer=tm)
+         overlap=0.5, target_size=target, timer=tm, callback_on_step_end=keep)
     tm("call_end", 0)
     torch.cuda.synchronize()
-    return time.perf_counter() - t0, tm
+    el = time.perf_counter() - t0
+    tm.finite = bool(torch.isfinite(last["lat"]).all().item()) if "lat" in last else None
+    return el, tm
 
 
 def pipeline_leg(pipe, size, steps=20):
@@ -361,7 +369,7 @@ def pipeline_leg(pipe, size, steps=20):
             "s_per_image": round(s, 4), "loop_ms": round(sum(st), 2),
             "step_ms_median": round(float(np.median(st)), 3), "step_ms_min": round(min(st), 3),
             "decode_ms": round(tm.span_ms("decode_start", "decode"), 2),
-            "pre_loop_ms": round(tm.span_ms("call_start", "loop_start"), 2)}
+            "pre_loop_ms": round(tm.span_ms("call_start", "loop_start"), 2), "latents_finite": tm.finite}
 
 
 def c3_run(pipe, world, rank, dev, size, steps, warm=True):
@@ -390,7 +398,8 @@ def c3_run(pipe, world, rank, dev, size, steps, warm=True):
             "step_ms_median": round(float(np.median(st)), 2),
             "pre_loop_ms": round(tm.span_ms("call_start", "loop_start"), 1),
             "decode_ms": round(tm.span_ms("decode_start", "decode"), 1),
-            "all_gather_bytes_per_step": (ntiles + (-ntiles) % world) * 4 * 128 * 128 * 4 if world > 1 else 0}
+            "all_gather_bytes_per_step": (ntiles + (-ntiles) % world) * 4 * 128 * 128 * 4 if world > 1 else 0,
+            "latents_finite": tm.finite}
 
 
 def roofline_leg(loop, fp8):
