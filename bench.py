@@ -21,6 +21,9 @@ Workloads (``--workload``; all ranks time exactly --steps steps between barrier 
                     ranks together through the product pipeline with ``enable_tile_parallel`` (tiles sharded,
                     one all_gather_into_tensor per step over RCCL, sharded tiled decode): s/image, tile-steps/s;
   c3            the C3 image is the timed unit: value = tile-steps/s of the whole job (strong scaling);
+  c4            BASELINE configs[3], 8K-output reading: one 8192^2 image (2048^2 input after the 4x upscale,
+                225 TLC tiles) through the same tile-sharded path on the use_fp8 model (e4m3 MFMA Linears):
+                value = tile-steps/s of the whole job (strong scaling);
   c5            BASELINE configs[4]: 8 images of 1024^2 x 50 steps split over the ranks: value = images/s.
 
 roofline: the dominant kernel family is the MFMA GEMM (gemm8_kernel + gemm_kernel: every projection, FF and
@@ -60,7 +63,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("c2", "c3", "c5"), default="c2")
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2")
     ap.add_argument("--size", type=int, default=1024, help="C2 image side (latent = size/8)")
     ap.add_argument("--fp8", action="store_true", help="use_fp8 model (quantize_8bit weights; transformer Linears "
                                                        "on the e4m3 MFMA): the C4 arithmetic")
@@ -71,6 +74,7 @@ def parse(argv=None):
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--c3-size", type=int, default=4096)
     ap.add_argument("--c3-steps", type=int, default=20)
+    ap.add_argument("--c4-size", type=int, default=8192, help="C4 output side (8K output reading of configs[3])")
     ap.add_argument("--c5-images", type=int, default=8)
     ap.add_argument("--c5-steps", type=int, default=50)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof windows)")
@@ -372,8 +376,9 @@ def pipeline_leg(pipe, size, steps=20):
             "pre_loop_ms": round(tm.span_ms("call_start", "loop_start"), 2), "latents_finite": tm.finite}
 
 
-def c3_run(pipe, world, rank, dev, size, steps, warm=True):
-    """BASELINE configs[2]: one size^2 image (49 TLC tiles at 4096^2) restored by all ranks together."""
+def c3_run(pipe, world, rank, dev, size, steps, warm=True, tag="C3"):
+    """BASELINE configs[2]: one size^2 image (49 TLC tiles at 4096^2) restored by all ranks together (configs[3]
+    at 8192^2, 225 tiles, with the use_fp8 model)."""
     from FaithDiff.pipelines.tlc import TileGrid
     if world > 1 and pipe.process_group is None:
         pipe.enable_tile_parallel()
@@ -391,7 +396,7 @@ def c3_run(pipe, world, rank, dev, size, steps, warm=True):
     s = max_over_ranks(s, world, dev)
     st = tm.step_ms()
     loop_s = max_over_ranks(sum(st) / 1e3, world, dev)
-    return {"workload": f"C3: {size}x{size} tiled restoration, {ntiles} TLC tiles x {steps} Euler steps, tiled VAE "
+    return {"workload": f"{tag}: {size}x{size} tiled restoration, {ntiles} TLC tiles x {steps} Euler steps, tiled VAE "
                         f"encode/decode, tiles sharded over {world} rank(s), one all_gather_into_tensor per step",
             "ntiles": ntiles, "steps": steps, "n_ranks": world, "s_per_image": round(s, 3),
             "loop_s": round(loop_s, 3), "tile_steps_per_s": round(ntiles * steps / loop_s, 3),
@@ -479,6 +484,8 @@ def vae_leg(pipe, loop):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    if args.workload == "c4":
+        args.fp8 = True  # configs[3] names fp8 UNet weights on the fp8 MFMA
     rc = maybe_launch(args, argv)
     if rc is not None:
         return rc
@@ -491,18 +498,22 @@ def main(argv=None):
               "vs_baseline": None, "dtype": "fp8-e4m3+bf16" if args.fp8 else "bf16",
               "data": "synthetic (seeded random-init SDXL+FaithDiff weights, synthetic latents/conditions/images)"}
 
-    if args.workload == "c3":
-        c3_run(pipe, world, rank, dev, args.c3_size, 1, warm=False)  # warm-up: graphs captured
+    if args.workload in ("c3", "c4"):
+        size, tag = (args.c3_size, "C3") if args.workload == "c3" else (args.c4_size, "C4")
+        c3_run(pipe, world, rank, dev, size, 1, warm=False, tag=tag)  # warm-up: graphs captured
         reps = []
         barrier(world)
         for _ in range(max(1, args.steps // 20)):
-            reps.append(c3_run(pipe, world, rank, dev, args.c3_size, args.c3_steps, warm=False))
+            reps.append(c3_run(pipe, world, rank, dev, size, args.c3_steps, warm=False, tag=tag))
         r = reps[-1]
-        result.update({"metric": "C3 tile-steps/sec @4096px 20-step (49 TLC tiles, tile-sharded over RCCL)",
+        what = (f"C3 tile-steps/sec @{size}px 20-step ({r['ntiles']} TLC tiles, tile-sharded over RCCL)"
+                if tag == "C3" else f"C4 tile-steps/sec @{size}px output 20-step, fp8 UNet ({r['ntiles']} TLC "
+                "tiles, tile-sharded over RCCL)")
+        result.update({"metric": what,
                        "value": r["tile_steps_per_s"], "unit": "tile-steps/s", "scaling": "strong",
                        "ms_per_step": round(r["loop_s"] / r["steps"] * 1e3, 2),
                        "config": {"workload": r["workload"], "s_per_image": r["s_per_image"],
-                                  "parallelism": f"tile-sharded x{world}"}, "c3": r})
+                                  "parallelism": f"tile-sharded x{world}"}, tag.lower(): r})
     elif args.workload == "c5":
         ims = list(range(rank, args.c5_images, world))
         img = synthetic_image(args.size, args.size, 7)

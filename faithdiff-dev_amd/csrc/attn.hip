@@ -1,8 +1,8 @@
 // Attention kernels for gfx950.
 //
 // flash_attn_d64: head_dim 64 flash attention (SDPA replacement for the 140 attn1/attn2 calls of a
-// UNet forward).  One workgroup = NWV waves (4 by default = 128 queries; 2-wave workgroups measured
-// no faster at Lq = 1024 and 10 % slower at 4096) of one (batch, head); each wave owns 32 queries.  K/V tiles of 64 keys are staged by global_load_lds into a double buffer.  The score
+// UNet forward).  One workgroup = NWV waves (4 by default; 2-wave workgroups measured no faster at Lq = 1024
+// and 10 % slower at 4096) of one (batch, head); each wave owns 16 * NQB queries (16 or 32, by launch size).  K/V tiles of 64 keys are staged by global_load_lds into a double buffer.  The score
 // tile is computed transposed, S^T = K Q^T (A = K rows from LDS, B = Q fragments held in VGPRs),
 // so each lane owns one query column: the row max needs only two cross-lane shuffles, and the
 // accumulator, packed to bf16/f16 in registers, is directly the B operand of O^T = V^T P^T (guide
@@ -37,8 +37,11 @@ __device__ __forceinline__ float xor_max_16_32(float x) {
 #ifndef FD_FLASH_TR_EARLY
 #define FD_FLASH_TR_EARLY 1
 #endif
-template <typename T, int NWV>
-__global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1, 2))) flash_attn_d64_kernel(
+// NQB: 16-query blocks per wave (2 = 32 queries, the register-heavy default; 1 = 16 queries in about half the
+// VGPRs, so four waves share a SIMD and one wave's softmax VALU runs under another's MFMAs)
+template <typename T, int NWV, int NQB>
+__global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NQB == 1 ? 4 : 1, NQB == 1 ? 4 : 2)))
+flash_attn_d64_kernel(
     const T* __restrict__ Q, long long ldq, long long qbs, const T* __restrict__ K, long long ldk, long long kbs,
     const T* __restrict__ V, long long ldv, long long vbs, T* __restrict__ O, long long ldo, long long obs,
     int Lq, int Lk, int kv_mod, int causal, float scale_log2, int heads, int swz) {
@@ -53,7 +56,7 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // 1-D grid; the q-blocks of one (batch, head) are contiguous after the XCD remap, so the head's K/V
   // stream is fetched into one L2 instead of all eight.
-  constexpr int QB = 32 * NWV;  // queries per workgroup
+  constexpr int QB = 16 * NQB * NWV;  // queries per workgroup
   const int nq = (Lq + QB - 1) / QB;
   const int pid = swz ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const int qblk = pid % nq, bh = pid / nq;
@@ -62,13 +65,13 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
   const T* Qb = Q + (long long)b * qbs + h * 64;
   const T* Kb = K + (long long)kvb * kbs + h * 64;
   const T* Vb = V + (long long)kvb * vbs + h * 64;
-  const int q0 = qblk * QB + wave * 32;
+  const int q0 = qblk * QB + wave * 16 * NQB;
   const int fr = lane & 15, fg = lane >> 4;
 
   // Q fragments (B operand): lane holds Q[q0 + qb*16 + fr][ds*32 + 8*fg .. +7]
-  V8 qf[2][2];
+  V8 qf[NQB][2];
 #pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
+  for (int qb = 0; qb < NQB; ++qb) {
     int q = q0 + qb * 16 + fr;
     q = q < Lq ? q : Lq - 1;
 #pragma unroll
@@ -132,34 +135,38 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
     }
   }
 
-  f32x4 o[4][2];
+  f32x4 o[4][NQB];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) o[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float mrow[2] = {-INFINITY, -INFINITY};
+    for (int j = 0; j < NQB; ++j) o[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float mrow[NQB];
+#pragma unroll
+  for (int j = 0; j < NQB; ++j) mrow[j] = -INFINITY;
   // softmax denominators on the MFMA pipe: lsum[qb] += ones(16 x 32) . P^T -- every row of the 16 x 16
   // block is the running sum for query column fr, of the same bf16 P the numerator uses (32 VALU adds
   // per tile traded for 4 MFMAs)
-  f32x4 lsum[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+  f32x4 lsum[NQB];
+#pragma unroll
+  for (int j = 0; j < NQB; ++j) lsum[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   V8 ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (T)1.0f;
 
-  typedef f32x4 Sc[4][2];
+  typedef f32x4 Sc[4][NQB];
   // S^T(tile in buffer BUF) = K Q^T  (16 MFMAs)
   auto qk = [&](auto bufc, Sc& sd) {
     constexpr int BUF = decltype(bufc)::value;
     const unsigned char* sk = smem + BUF * 16384;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      sd[kb][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      sd[kb][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qb = 0; qb < NQB; ++qb) sd[kb][qb] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds) {
         const V8 kf = *(const V8*)(sk + kro[ds] + kb * 2048);
-        sd[kb][0] = mfma16x16x32(kf, qf[0][ds], sd[kb][0]);
-        sd[kb][1] = mfma16x16x32(kf, qf[1][ds], sd[kb][1]);
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) sd[kb][qb] = mfma16x16x32(kf, qf[qb][ds], sd[kb][qb]);
       }
     }
   };
@@ -206,18 +213,15 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
         for (int i = 0; i < 4; ++i) {
           const int key = t * 64 + kb * 16 + fg * 4 + i;
           // ragged tail; causal (CLIP text encoders): query q0 + qb*16 + fr sees keys <= itself
-          if (key >= Lk || (causal && key > q0 + fr)) {
-            sc[kb][0][i] = -INFINITY;
-          }
-          if (key >= Lk || (causal && key > q0 + 16 + fr)) {
-            sc[kb][1][i] = -INFINITY;
-          }
+#pragma unroll
+          for (int qb = 0; qb < NQB; ++qb)
+            if (key >= Lk || (causal && key > q0 + qb * 16 + fr)) sc[kb][qb][i] = -INFINITY;
         }
     }
     // ---- online softmax (one query per lane column; keys over fg groups, kb, i)
-    V8 pf[2][2];
+    V8 pf[NQB][2];
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
+    for (int qb = 0; qb < NQB; ++qb) {
       float mx = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
@@ -267,14 +271,14 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
         typedef __attribute__((ext_vector_type(8))) short s16x8;
         const s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         const V8 vf = __builtin_bit_cast(V8, w);
-        o[db][0] = mfma16x16x32(vf, pf[0][s2], o[db][0]);
-        o[db][1] = mfma16x16x32(vf, pf[1][s2], o[db][1]);
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) o[db][qb] = mfma16x16x32(vf, pf[qb][s2], o[db][qb]);
       }
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      lsum[0] = mfma16x16x32(ones, pf[0][s2], lsum[0]);
-      lsum[1] = mfma16x16x32(ones, pf[1][s2], lsum[1]);
+#pragma unroll
+      for (int qb = 0; qb < NQB; ++qb) lsum[qb] = mfma16x16x32(ones, pf[qb][s2], lsum[qb]);
     }
     if (t + 1 < nt) {
       // tile t+1 landed (tile t+2, if issued, may still fly); every wave done reading tile t
@@ -307,7 +311,7 @@ __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(1
 
   // ---- finalise: lane holds O^T[d = db*16 + 4*fg + j][q = qb*16 + fr]
 #pragma unroll
-  for (int qb = 0; qb < 2; ++qb) {
+  for (int qb = 0; qb < NQB; ++qb) {
     const float inv = 1.0f / lsum[qb][0];
     const int q = q0 + qb * 16 + fr;
     if (q >= Lq) continue;
@@ -330,28 +334,46 @@ extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const 
   if (!q || !k || !v || !o) return FD_ERR_ARG;
   if (batch <= 0 || heads <= 0 || Lq <= 0 || Lk <= 0 || kv_mod < 0) return FD_ERR_SHAPE;
   if ((ldq | ldk | ldv | ldo) & 7) return FD_ERR_SHAPE;
-  static int swz = -1, nwv = 0;
+  static int swz = -1, nwv = 0, nqb = 0;
   if (swz < 0) {
     const char* e = getenv("FD_FLASH_SWZ");
     swz = e ? atoi(e) : 1;
-    e = getenv("FD_FLASH_WAVES");  // 4 (128 queries per workgroup, default) or 2 (64)
-    nwv = (e && atoi(e) == 2) ? 2 : 4;
+    e = getenv("FD_FLASH_WAVES");  // waves per workgroup: 4 (default), 2 or 8
+    nwv = e ? atoi(e) : 4;
+    e = getenv("FD_FLASH_QPW");  // queries per wave: 32 or 16 (default: by launch size, below)
+    nqb = e ? (atoi(e) == 16 ? 1 : 2) : 0;
+    if (nwv != 2 && nwv != 8) nwv = 4;
   }
-  const int QB = 32 * nwv;
+  // 16 queries per wave (half the VGPRs: three waves per SIMD, one wave's softmax under another's MFMAs) while
+  // the 32-query grid would give at most 4 workgroups per CU (scripts/attn_var.sh: C2's L = 1024 28.3 -> 24.4 us,
+  // L = 4096 134 -> 127 us, cross-attention 8.6 -> 7.6 us); past that the 32-query kernel's fewer K/V fragment
+  // reads per flop win (26 CFG-batched tiles: 200 vs 215 us).  Every query sees the same operations in either
+  // form, so the choice changes no bit.
+  int nq = nqb;
+  if (nq == 0) nq = (long long)((Lq + 127) / 128) * heads * batch <= 1024 ? 1 : 2;
+  const int nw = (nwv == 8 && nq == 2) ? 4 : nwv;
+  const int QB = 16 * nq * nw;
   const long long nblk = (long long)((Lq + QB - 1) / QB) * heads * batch;
   if (nblk > 0x7fffffff) return FD_ERR_SHAPE;
-  dim3 grid((unsigned)nblk), block(64 * nwv);
+  dim3 grid((unsigned)nblk), block(64 * nw);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  if (nwv == 4) {
-    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, 4>), grid, block, 0, s, (const T*)q, ldq, qbs,
-                                            (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk,
-                                            kv_mod, causal, sl2, heads, swz));
+#define FD_FLASH(NW_, NQ_)                                                                                      \
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, NW_, NQ_>), grid, block, 0, s, (const T*)q, ldq, \
+                                          qbs, (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk, \
+                                          kv_mod, causal, sl2, heads, swz))
+  if (nq == 2 && nw == 4) {
+    FD_FLASH(4, 2);
+  } else if (nq == 2) {
+    FD_FLASH(2, 2);
+  } else if (nw == 4) {
+    FD_FLASH(4, 1);
+  } else if (nw == 8) {
+    FD_FLASH(8, 1);
   } else {
-    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, 2>), grid, block, 0, s, (const T*)q, ldq, qbs,
-                                            (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk,
-                                            kv_mod, causal, sl2, heads, swz));
+    FD_FLASH(2, 1);
   }
+#undef FD_FLASH
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

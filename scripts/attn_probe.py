@@ -12,6 +12,8 @@ from fdhip import lib as L  # noqa: E402
 
 L.require_device()
 SHAPES = [(2, 20, 1024, 1024), (2, 10, 4096, 4096), (2, 20, 1024, 77), (2, 10, 4096, 77)]
+if len(sys.argv) > 1:  # extra shapes as BxHxLqxLk
+    SHAPES = [tuple(int(v) for v in a.split("x")) for a in sys.argv[1:]]
 tag = {k: v for k, v in os.environ.items() if k.startswith("FD_FLASH")}
 REP = 20
 for B, H, Lq, Lk in SHAPES:

@@ -207,6 +207,26 @@ def test_flash_attn(dtype, B, heads, Lq, Lk, kv_mod):
     assert rel_l2(o, ref) < 1.5 * TOL[dtype], rel_l2(o, ref)
 
 
+@pytest.mark.parametrize("Lk", [1024, 77])
+def test_flash_attn_query_split_bitwise(Lk):
+    """A 2-image launch (16 queries per wave) and the same images inside a 26-image launch (32 per wave, the
+    CFG-batched TLC tiles of C3) give the same bits: the kernel form is chosen by launch size."""
+    from fdhip import ops
+    B, heads, Lq = 26, 20, 1024
+    C = heads * 64
+    q = rnd(B, Lq, C)
+    kv = rnd(B, Lk, 2 * C)
+    k, v = kv[..., :C], kv[..., C:]
+    big = torch.empty(B, Lq, C, dtype=torch.bfloat16, device=DEV)
+    ops.flash_attn(q, k, v, big, B, heads, Lq, Lk, C, 2 * C, 2 * C, C, Lq * C, Lk * 2 * C, Lk * 2 * C, Lq * C,
+                   kv_mod=0, scale=0.125)
+    for b0 in (0, 12, 24):
+        small = torch.empty(2, Lq, C, dtype=torch.bfloat16, device=DEV)
+        ops.flash_attn(q[b0:b0 + 2], k[b0:b0 + 2], v[b0:b0 + 2], small, 2, heads, Lq, Lk, C, 2 * C, 2 * C, C,
+                       Lq * C, Lk * 2 * C, Lk * 2 * C, Lq * C, kv_mod=0, scale=0.125)
+        assert torch.equal(small, big[b0:b0 + 2])
+
+
 @pytest.mark.parametrize("same", [True, False])
 def test_mha_seq_axis(same):
     from fdhip import ops
