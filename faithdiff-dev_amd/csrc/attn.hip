@@ -12,6 +12,7 @@
 // mha_seq_axis: the information transformer's MultiheadAttention over the batch axis (L = CFG pair).
 // softmax_rows: fp32 row softmax for the single-head d=512 VAE mid attention (GEMM + softmax + GEMM).
 #include <type_traits>
+#include <utility>
 
 #include "fd_common.h"
 
@@ -34,12 +35,33 @@ __device__ __forceinline__ float xor_max_16_32(float x) {
   return vmax_raw(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
+#ifndef FLASH_NBUF
+#define FLASH_NBUF 3
+#endif
 #ifndef FD_FLASH_TR_EARLY
 #define FD_FLASH_TR_EARLY 1
 #endif
 // NQB: 16-query blocks per wave (2 = 32 queries, the register-heavy default; 1 = 16 queries in about half the
 // VGPRs, so four waves share a SIMD and one wave's softmax VALU runs under another's MFMAs)
-template <typename T, int NWV, int NQB>
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// s_waitcnt vmcnt(PER * n) for a run-time n in [0, NMAX]
+template <int PER, int NMAX>
+__device__ __forceinline__ void wait_vm_tiles(int n) {
+  if constexpr (NMAX > 0) {
+    if (n >= NMAX) {
+      wait_vm<PER * NMAX>();
+      return;
+    }
+    wait_vm_tiles<PER, NMAX - 1>(n);
+  } else {
+    wait_vm<0>();
+  }
+}
+
+template <typename T, int NWV, int NQB, int NBUF>
 __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NQB == 1 ? 4 : 1, NQB == 1 ? 4 : 2)))
 flash_attn_d64_kernel(
     const T* __restrict__ Q, long long ldq, long long qbs, const T* __restrict__ K, long long ldk, long long kbs,
@@ -47,10 +69,9 @@ flash_attn_d64_kernel(
     int Lq, int Lk, int kv_mod, int causal, float scale_log2, int heads, int swz) {
   typedef typename VecT<T>::v8 V8;
   constexpr bool TR_EARLY = FD_FLASH_TR_EARLY;
-  // 3-deep K/V ring: tile t+2 is issued while tile t is consumed (counted vmcnt, raw s_barrier), so each
-  // tile's load has two tiles of compute to land in.  (A software-pipelined variant -- scores of tile t+1
-  // under tile t's softmax, 4-deep ring -- measured 1.3x slower: 256 VGPRs and 4x the code.)
-  constexpr int NBUF = 3;
+  // NBUF-deep K/V ring: tile t+NBUF-1 is issued while tile t is consumed (counted vmcnt, raw s_barrier), so
+  // each tile's load has NBUF-1 tiles of compute to land in.  (A software-pipelined variant -- scores of tile
+  // t+1 under tile t's softmax, 4-deep ring -- measured 1.3x slower: 256 VGPRs and 4x the code.)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NBUF * 2 * 64 * 128];  // [buf][K|V][64 rows][128 B]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -176,23 +197,25 @@ flash_attn_d64_kernel(
   // the asm reads are retired by an explicit lgkmcnt(0) + sched_barrier before the P.V MFMAs
   auto read_vtr = [&](auto bufc, s16x4 (&vtr)[4][2][2]) {
     constexpr int BUF = decltype(bufc)::value;
+    // ds_read offsets are 16-bit: buffers from 32 KiB on move their base into the address register
+    constexpr int HI = BUF * 16384 >= 32768 ? BUF * 16384 : 0, LO = BUF * 16384 - HI;
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
-      const unsigned va = (unsigned)(unsigned long)(LDS_PTR(smem + vro[db]));
+      const unsigned va = (unsigned)(unsigned long)(LDS_PTR(smem + vro[db])) + HI;
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[db][s2][0]) : "v"(va),
-                     "i"(BUF * 16384 + 8192 + s2 * 4096));
+                     "i"(LO + 8192 + s2 * 4096));
         asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[db][s2][1]) : "v"(va),
-                     "i"(BUF * 16384 + 8192 + s2 * 4096 + 2048));
+                     "i"(LO + 8192 + s2 * 4096 + 2048));
       }
     }
   };
   const int nfull = Lk / 64;  // tiles with no key past Lk
-  stage(0, 0);
-  if (nt > 1) stage(1, 1);
-  if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < nt) stage(i, i);
+  wait_vm_tiles<PER, NBUF - 2>(min(NBUF - 1, nt) - 1);  // tile 0 landed
   __builtin_amdgcn_s_barrier();
 
   // one 64-key tile in ring buffer BUF (compile-time, so every LDS address is base + immediate);
@@ -200,8 +223,8 @@ flash_attn_d64_kernel(
   auto iter = [&](auto bufc, auto maskc, int t) {
     constexpr int BUF = decltype(bufc)::value;
     constexpr bool MASK = decltype(maskc)::value;
-    // buffer (BUF+2)%3 was last read in the previous tile, which every wave finished before the barrier
-    if (t + 2 < nt) stage(t + 2, (BUF + 2) % 3);
+    // buffer (BUF+NBUF-1)%NBUF was last read in the previous tile, which every wave finished before the barrier
+    if (t + NBUF - 1 < nt) stage(t + NBUF - 1, (BUF + NBUF - 1) % NBUF);
     Sc sc;
     qk(bufc, sc);
     s16x4 vtr[4][2][2];
@@ -230,14 +253,19 @@ flash_attn_d64_kernel(
       mx = xor_max_16_32(mx);
       const float mnew = fmaxf(mrow[qb], mx * scale_log2);
       float pv[4][4];
+      typedef __attribute__((ext_vector_type(2))) float f2;
+      const f2 sc2 = {scale_log2, scale_log2}, mn2 = {-mnew, -mnew};
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < 4; i += 2) {
+          // the exponent arguments two at a time (v_pk_fma_f32: the same fma per element, half the VALU issues);
           // raw v_exp_f32 (no denormal range fix-up: results below 2^-126 flush to 0, irrelevant to a softmax
           // numerator already divided by a sum >= 1)
-          const float e = __builtin_amdgcn_exp2f(fmaf(sc[kb][qb][i], scale_log2, -mnew));
-          pv[kb][i] = e;
+          const f2 x = {sc[kb][qb][i], sc[kb][qb][i + 1]};
+          const f2 y = __builtin_elementwise_fma(x, sc2, mn2);
+          pv[kb][i] = __builtin_amdgcn_exp2f(y[0]);
+          pv[kb][i + 1] = __builtin_amdgcn_exp2f(y[1]);
         }
       // exact skip of the O / l rescale when no query of this wave raised its running max (most tiles
       // after the first few): alpha would be exactly 1
@@ -281,32 +309,28 @@ flash_attn_d64_kernel(
       for (int qb = 0; qb < NQB; ++qb) lsum[qb] = mfma16x16x32(ones, pf[qb][s2], lsum[qb]);
     }
     if (t + 1 < nt) {
-      // tile t+1 landed (tile t+2, if issued, may still fly); every wave done reading tile t
-      if (t + 2 < nt) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // tile t+1 landed (tiles t+2 .. t+NBUF-1, where issued, may still fly); every wave done reading tile t
+      if (t + NBUF - 1 < nt) wait_vm<PER * (NBUF - 2)>();
+      else wait_vm_tiles<PER, NBUF - 2>(nt - 2 - t);
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_s_barrier();
     }
   };
-  typedef std::integral_constant<int, 0> B0;
-  typedef std::integral_constant<int, 1> B1;
-  typedef std::integral_constant<int, 2> B2;
   typedef std::integral_constant<bool, false> NM;
   typedef std::integral_constant<bool, true> YM;
   int t = 0;
-  for (; !causal && t + 3 <= nfull; t += 3) {
-    iter(B0(), NM(), t);
-    iter(B1(), NM(), t + 1);
-    iter(B2(), NM(), t + 2);
+  for (; !causal && t + NBUF <= nfull; t += NBUF) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      (iter(std::integral_constant<int, I>(), NM(), t + I), ...);
+    }(std::make_integer_sequence<int, NBUF>());
   }
-  // the remaining 0-2 full tiles and the ragged tail (buffer index t % 3 continues the ring)
+  // the remaining full tiles and the ragged tail (buffer index t % NBUF continues the ring)
   for (; t < nt; ++t) {
     const bool m = causal || t >= nfull;
-    switch (t % 3) {
-      case 0: if (m) iter(B0(), YM(), t); else iter(B0(), NM(), t); break;
-      case 1: if (m) iter(B1(), YM(), t); else iter(B1(), NM(), t); break;
-      default: if (m) iter(B2(), YM(), t); else iter(B2(), NM(), t); break;
-    }
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      ((t % NBUF == I ? (m ? iter(std::integral_constant<int, I>(), YM(), t)
+                           : iter(std::integral_constant<int, I>(), NM(), t)), 0 : 0), ...);
+    }(std::make_integer_sequence<int, NBUF>());
   }
 
   // ---- finalise: lane holds O^T[d = db*16 + 4*fg + j][q = qb*16 + fr]
@@ -359,7 +383,7 @@ extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const 
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
 #define FD_FLASH(NW_, NQ_)                                                                                      \
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, NW_, NQ_>), grid, block, 0, s, (const T*)q, ldq, \
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, NW_, NQ_, FLASH_NBUF>), grid, block, 0, s, (const T*)q, ldq, \
                                           qbs, (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk, \
                                           kv_mod, causal, sl2, heads, swz))
   if (nq == 2 && nw == 4) {
