@@ -644,6 +644,11 @@ int choose_split(int m_ref, int N, int K, int bn) {
   const long long tiles = (long long)((m_ref + 255) / 256) * ((N + bn - 1) / bn);
   if (N % bn != 0) return 0;
   if (tiles >= 192) return 1;
+  // mid K on the 32^2 level (ff out 2048 x 1280 x 5120, the K = 5760 conv): three splits of 80 tiles beat the
+  // 4-wave 64 x 160 kernel with cold weights, 47.1 -> 41.1 us / 61.2 -> 45.0 us, and stay ahead when 13 TLC tiles
+  // share the launch (C3: 520 -> 454 us); N = 640 at 64^2 (160 tiles) gains nothing (profiles/r02e_ksplit.jsonl)
+  static const int midk = env_i("FD_GEMM8_MIDK", 3);  // 0 = off (A/B), else the split count
+  if (midk > 0 && K >= 4096 && K < 8192 && N >= 1280 && tiles <= 96) return midk;
   if (K < 8192) return 0;
   int s = (int)(256 / tiles);
   if (s > nk / 8) s = nk / 8;

@@ -30,12 +30,13 @@ g = torch.Generator(device="cuda").manual_seed(0)
 for s in SHAPES:
     if s.startswith("conv"):
         H, W, Cin, Cout = (int(x) for x in s[4:].split("x"))
-        x = torch.rand(2 * H * W, Cin, device="cuda", generator=g).to(bf) * 2 - 1
+        NI = int(os.environ.get("PROBE_NIMG", "2"))  # images in the launch (C3 batches 13 tiles x 2 CFG rows)
+        x = torch.rand(NI * H * W, Cin, device="cuda", generator=g).to(bf) * 2 - 1
         wp = ((torch.rand(Cout, 9 * Cin, device="cuda", generator=g) * 2 - 1) / (9 * Cin) ** 0.5).to(bf)
         b = torch.zeros(Cout, device="cuda")
-        out = torch.empty(2 * H * W, Cout, device="cuda", dtype=bf)
-        fn = lambda: ops.conv3x3(x, wp, b, 2, H, W, out=out)  # noqa: E731
-        flops = 2 * 2 * H * W * Cout * 9 * Cin
+        out = torch.empty(NI * H * W, Cout, device="cuda", dtype=bf)
+        fn = lambda: ops.conv3x3(x, wp, b, NI, H, W, out=out)  # noqa: E731
+        flops = 2 * NI * H * W * Cout * 9 * Cin
     else:
         dims, act = (s.split(":") + ["none"])[:2]
         M, N, K = (int(v) for v in dims.split("x"))
@@ -50,7 +51,9 @@ for s in SHAPES:
             return ops.gemm(a, ws_[ctr[0] % len(ws_)], out=out, act=act)
         flops = 2 * M * N * K
     st = torch.cuda.Stream()
-    with torch.cuda.stream(st):
+    # PROBE_GROUPS=n: the launch batches n TLC tiles (ops.tile_groups), so the planner sees m_ref = M / n as in
+    # a batched UNet forward
+    with torch.cuda.stream(st), ops.tile_groups(int(os.environ.get("PROBE_GROUPS", "1"))):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
