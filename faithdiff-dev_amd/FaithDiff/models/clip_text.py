@@ -130,12 +130,12 @@ class CLIPTextModel:
 
     @torch.no_grad()
     def __call__(self, input_ids, output_hidden_states=False, **kwargs):
-        out = self.hip().forward(input_ids)
-        o = _Output([self._first(out).float()])
-        o.hidden_states = tuple(h.float() for h in out["hidden_states"]) if output_hidden_states else None
-        o.last_hidden_state = out["last_hidden_state"].float()
-        o.pooler_output = out["pooled"].float()
-        o.text_embeds = out["text_embeds"].float() if "text_embeds" in out else None
+        out = self.hip().forward_f32(input_ids)  # fp32, one private copy per call (graph-replayed forward)
+        o = _Output([self._first(out)])
+        o.hidden_states = tuple(out["hidden_states"]) if output_hidden_states else None
+        o.last_hidden_state = out["last_hidden_state"]
+        o.pooler_output = out["pooled"]
+        o.text_embeds = out.get("text_embeds")
         return o
 
 

@@ -311,7 +311,12 @@ class FaithDiffStableDiffusionXLPipeline:
                                  f"{type(img)}")
             if img.size != (width, height):
                 img = img.resize((width, height), resample=PIL.Image.LANCZOS)
-            arr = np.asarray(img.convert("RGB"), dtype=np.float32) / 255.0 * 2.0 - 1.0
+            # the uint8 pixels go to the device (a quarter of the fp32 bytes) and are mapped there with the
+            # same fp32 operations numpy would do (x / 255 * 2 - 1, each correctly rounded): ~4 ms of host
+            # numpy per 1024^2 image otherwise
+            u8 = torch.from_numpy(np.ascontiguousarray(np.asarray(img.convert("RGB"), dtype=np.uint8)))
+            x = u8.reshape(-1, 3).to(self.device).to(torch.float32)
+            return (x / 255.0 * 2.0 - 1.0).to(torch.float16)
         x = torch.from_numpy(np.ascontiguousarray(arr)).reshape(-1, 3)
         return x.to(self.device, torch.float16)
 

@@ -630,7 +630,9 @@ extern "C" int fd_gemm(fd_gemm_params* p, void* stream) {
     const int r256 = fd_gemm256_try(p, stream);  // large-M, N % 256 == 0: 256 x 256 tiles
     if (r256 < 0) return r256;
     if (r256 == 1) return FD_OK;
-    const int r8 = fd_gemm8_try(p, stream);
+  }
+  {
+    const int r8 = fd_gemm8_try(p, stream);  // LN-fold producers only on its 160-column tiles (plan8)
     if (r8 < 0) return r8;
     if (r8 == 1) return FD_OK;
   }

@@ -486,6 +486,12 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   const int gcpg = gn ? p.N / p.gn_groups : 8;
   const int gsplit = (((tid % VPR) * 8) / gcpg + 1) * gcpg - (tid % VPR) * 8;
   GnTile gna;
+  // LN-fold producer (fd_gemm_params.ln_out) on the 160-column tiles: per-row (sum, sumsq) of the values as stored,
+  // over the tile's 160 columns -- the partial layout of the 4-wave 64 x 160 producer (gemm.hip), which the
+  // consumers read -- summed 8-column chunk by chunk in column order.  Chunk slots after the epilogue staging.
+  constexpr bool LNO_OK = (BN == 160) && !GEGLU && !CONV && (EPB + EROWS * VPR * 8 <= SMEM) && EROWS <= NTHR;
+  const bool lno = LNO_OK && p.ln_out != nullptr;
+  float2* const lnslot = (float2*)(smem + EPB);
 #pragma unroll 1
   for (int half = 0; half < BM / EROWS; ++half) {
     __syncthreads();  // ring (half 0) / previous half's staging (half 1) fully consumed
@@ -592,13 +598,27 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
         *(TO8*)(C + (long long)m * p.ldc + n) = o;
         if (gn) gna.add(o, gsplit);
+        if (LNO_OK && lno) {
+          float ls = 0.f, lq = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float f = (float)o[i];
+            ls += f;
+            lq += f * f;
+          }
+          lnslot[e] = make_float2(ls, lq);
+        }
       }
     }
     } else {  // edge tiles / unaligned operands: scalar, bounds-checked
       for (int e = tid; e < EROWS * VPR; e += NTHR) {
         const int r = e / VPR, cv = e % VPR;
         const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
-        if (m >= M || n >= Nout) continue;
+        if (m >= M || n >= Nout) {
+          if (LNO_OK && lno) lnslot[e] = make_float2(0.f, 0.f);
+          continue;
+        }
+        float ls = 0.f, lq = 0.f;
         for (int i = 0; i < 8 && n + i < Nout; ++i) {
           float x = ep[r * LDE + cv * 8 + i];
           if (!GEGLU) {
@@ -611,8 +631,26 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
             x = act_f(x, act);
           }
           if (R) x += (float)R[(long long)m * p.ldr + n + i];
-          C[(long long)m * p.ldc + n + i] = (TO)x;
+          const TO o1 = (TO)x;
+          C[(long long)m * p.ldc + n + i] = o1;
+          ls += (float)o1;
+          lq += (float)o1 * (float)o1;
         }
+        if (LNO_OK && lno) lnslot[e] = make_float2(ls, lq);
+      }
+    }
+    if (LNO_OK && lno) {  // this half's rows: 20 chunk slots each, summed in column order
+      __syncthreads();
+      const int mr = m0 + half * EROWS + tid;
+      if (tid < EROWS && mr < M) {
+        float ls = 0.f, lq = 0.f;
+#pragma unroll
+        for (int c = 0; c < VPR; ++c) {
+          const float2 v2 = lnslot[tid * VPR + c];
+          ls += v2.x;
+          lq += v2.y;
+        }
+        ((float2*)p.ln_out)[(long long)mr * (N / 160) + n0 / 160] = make_float2(ls, lq);
       }
     }
   }
@@ -709,6 +747,22 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if (!enabled || p->batch > 1 || p->K < 128) return 0;
   Plan8 q;
+  if (p->ln_out) {
+    // LN-fold producer: only a 160-column tile writes the partial layout the consumers read.  Long K (the ff out
+    // of the 32^2 level, 2048 x 1280 x 5120 at C2): 128 x 160 tiles with K split in two (pairwise combine),
+    // 0.64x the operand bytes per CU of the 4-wave 64 x 160 producer (probe with cold weights 47.1 -> 40.6 us,
+    // profiles/r02e_m2048_split.jsonl); anything else stays on that producer (return 0).
+    static const int lnp = env_i("FD_GEMM8_LNP", 1);
+    if (!lnp || p->act == FD_ACT_GEGLU || p->conv || p->N % 160 || p->K < 4096 || m_ref < 128) return 0;
+    if ((long long)((m_ref + 63) / 64) * (p->N / 160) > 256) return 0;
+    q.bm = 128;
+    q.bn = 160;
+    q.nw = 4;
+    q.waves_m = 2;
+    q.ns = 3;
+    q.S = 2;
+    goto planned;
+  }
   // 256 x 128 tiles (4 x 2 waves of 64 x 64).  256 x 160 (98 vs 85 flop/B) spills at the 256-VGPR cap of
   // two waves per SIMD with register-double-buffered fragments; kept out until it fits.
   q.bm = 256;

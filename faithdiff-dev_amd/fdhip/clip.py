@@ -9,12 +9,18 @@ gelu for bigG) -> fc2, both residual; final LayerNorm; pooled = final-LN row at 
 legacy eos_token_id == 2 path of both SDXL configs; EOS 49407 is the largest id, so this is the first EOS);
 text_projection without bias.  Each Linear is one fd_gemm (bias / activation / residual in the epilogue), the
 attention one causal fd_flash_attn, the embeddings one fd_embed_tokens; activations bf16 (the reference: fp16).
+
+The forward (~220 launches for bigG) is replayed as one hipGraph per (batch, length) from its second call on
+(fdhip/graphs.py): encode_prompt runs each encoder twice per image (prompt, negative prompt), and eager ctypes
+launches made it ~8 ms of a 1024^2 pipe() call.  The EOS row is picked on the device (argmax of the ids), so
+nothing in the forward needs the host.
 """
 import torch
 
 from . import arch
 from . import lib as L
 from . import ops
+from .graphs import GraphCache
 
 
 class HipCLIPTextModel:
@@ -40,18 +46,70 @@ class HipCLIPTextModel:
                 fc2=(W(f"{q}.mlp.fc2.weight"), Fp(f"{q}.mlp.fc2.bias"))))
         self.fln = (Fp("text_model.final_layer_norm.weight"), Fp("text_model.final_layer_norm.bias"))
         self.proj = W("text_projection.weight") if cfg.get("proj") else None
+        self.graphs = GraphCache(max_graphs=4)
 
     @torch.no_grad()
     def forward(self, input_ids):
         """input_ids [B, T] (any int dtype, host or device).  Returns a dict: hidden_states (list of [B, T, D] in
         the compute dtype: the embeddings, then each layer's output, as transformers' output_hidden_states),
-        last_hidden_state, pooled ([B, D], final-LN EOS row), text_embeds ([B, proj] with a projection)."""
+        last_hidden_state, pooled ([B, D], final-LN EOS row), text_embeds ([B, proj] with a projection).
+        The tensors are the graph's static outputs from the second call of a shape on: valid until the next
+        call (CLIPTextModel.__call__ copies them out as fp32 straight away)."""
         ids = torch.as_tensor(input_ids)
         B, T = ids.shape
+        ids_d = ids.to(device=self.device, dtype=torch.int32).contiguous().reshape(-1)
+        outs = self.graphs.run(("clip", B, T), lambda i: self._forward_dev(i, B, T), [ids_d])
+        nl = self.cfg["layers"]
+        out = dict(hidden_states=list(outs[:nl + 1]), last_hidden_state=outs[nl + 1], pooled=outs[nl + 2])
+        if self.proj is not None:
+            out["text_embeds"] = outs[nl + 3]
+        return out
+
+    @torch.no_grad()
+    def forward_f32(self, input_ids):
+        """forward() with every output as fp32 (what the transformers surface returns), all of them packed into one
+        buffer inside the graph and copied out of its static memory by a single clone -- instead of ~50 separate
+        conversions per call.  The returned tensors are views of that private copy."""
+        ids = torch.as_tensor(input_ids)
+        B, T = ids.shape
+        ids_d = ids.to(device=self.device, dtype=torch.int32).contiguous().reshape(-1)
+        shapes = []
+
+        def packed(i):
+            outs = self._forward_dev(i, B, T)
+            flat = torch.empty(sum(o.numel() for o in outs), dtype=torch.float32, device=self.device)
+            off = 0
+            for o in outs:
+                flat[off:off + o.numel()].view(o.shape).copy_(o)
+                off += o.numel()
+            return flat
+        for o in self._out_shapes(B, T):
+            shapes.append(o)
+        flat = self.graphs.run(("clip32", B, T), packed, [ids_d]).clone()
+        views, off = [], 0
+        for shp in shapes:
+            n = 1
+            for d in shp:
+                n *= d
+            views.append(flat[off:off + n].view(shp))
+            off += n
+        nl = self.cfg["layers"]
+        out = dict(hidden_states=views[:nl + 1], last_hidden_state=views[nl + 1], pooled=views[nl + 2])
+        if self.proj is not None:
+            out["text_embeds"] = views[nl + 3]
+        return out
+
+    def _out_shapes(self, B, T):
+        D = self.cfg["D"]
+        shp = [(B, T, D)] * (self.cfg["layers"] + 1) + [(B, T, D), (B, D)]
+        if self.proj is not None:
+            shp.append((B, self.proj.shape[0]))
+        return shp
+
+    def _forward_dev(self, ids_d, B, T):
+        """Device-only body of forward (capturable): a tuple (hidden states..., last, pooled[, text_embeds])."""
         D = self.cfg["D"]
         H = D // 64
-        eos = ids.argmax(dim=-1).tolist()
-        ids_d = ids.to(device=self.device, dtype=torch.int32).contiguous().reshape(-1)
         M = B * T
         h = torch.empty((M, D), dtype=self.dtype, device=self.device)
         ops.embed_tokens(ids_d, self.tok, self.pos, h, B, T)
@@ -73,11 +131,14 @@ class HipCLIPTextModel:
             hidden.append(h.reshape(B, T, D))
         last = torch.empty_like(h)
         ops.layer_norm(h, *self.fln, 1e-5, out=last)
-        pooled = torch.stack([last[b * T + eos[b]] for b in range(B)], 0).contiguous()
-        out = dict(hidden_states=hidden, last_hidden_state=last.reshape(B, T, D), pooled=pooled)
+        # pooled = the final-LN row at argmax(input_ids) (first EOS), selected on the device
+        eos = ids_d.view(B, T).argmax(dim=-1).to(torch.int64)
+        rows = torch.arange(B, device=self.device, dtype=torch.int64) * T + eos
+        pooled = last.index_select(0, rows).contiguous()
+        outs = hidden + [last.reshape(B, T, D), pooled]
         if self.proj is not None:
-            out["text_embeds"] = ops.gemm(pooled, self.proj)
-        return out
+            outs.append(ops.gemm(pooled, self.proj))
+        return tuple(outs)
 
 
 def random_clip(cfg, seed, device="cpu"):

@@ -80,3 +80,44 @@ def test_encode_prompt_dropin_shapes_and_negative():
     assert npe.abs().sum() > 0 and not torch.equal(pe, npe)
     pe2, _, _, _ = pipe.encode_prompt("a photo of a red car, highly detailed", negative_prompt="")
     assert torch.equal(pe, pe2)
+
+
+def test_clip_graph_replay_is_bitwise():
+    """The text encoder runs as a hipGraph from its second call of a shape on (fdhip/graphs.py): replays with
+    other token ids give bitwise what the eager forward gives, the EOS row picked on the device included."""
+    from fdhip import arch
+    from fdhip.clip import HipCLIPTextModel, random_clip
+    cfg = arch.CLIP_G  # with the projection (text_embeds)
+    sd = random_clip(cfg, seed=9)
+    hip = HipCLIPTextModel(sd, cfg, "cuda", torch.bfloat16)
+    ids = make_ids(0, seed=3)
+    a, b = ids[:1], ids[1:]  # B = 1, as encode_prompt calls it: a short and a long prompt
+
+    def snap(o):
+        return [t.clone() for t in o["hidden_states"]] + [o["last_hidden_state"].clone(), o["pooled"].clone(),
+                                                           o["text_embeds"].clone()]
+    ref_b = snap(hip.forward(b))  # eager (first use of the shape)
+    hip.graphs.enabled = False
+    ref_a = snap(hip.forward(a))  # eager
+    hip.graphs.enabled = True
+    got_a = snap(hip.forward(a))  # second use: captured, replayed
+    got_b = snap(hip.forward(b))  # replay
+    got_a2 = snap(hip.forward(a))  # replay
+    assert len(hip.graphs) == 1
+    for x, y in zip(got_a, ref_a):
+        assert torch.equal(x, y)
+    for x, y in zip(got_b, ref_b):
+        assert torch.equal(x, y)
+    for x, y in zip(got_a2, ref_a):
+        assert torch.equal(x, y)
+    assert not torch.equal(got_a[-1], got_b[-1])
+    # the fp32 surface (CLIPTextModel.__call__): outputs packed in the graph, one private copy per call
+    for _ in range(3):  # eager, capture + replay, replay
+        fa = hip.forward_f32(a)
+        fb = hip.forward_f32(b)
+        fa_l = list(fa["hidden_states"]) + [fa["last_hidden_state"], fa["pooled"], fa["text_embeds"]]
+        fb_l = list(fb["hidden_states"]) + [fb["last_hidden_state"], fb["pooled"], fb["text_embeds"]]
+        for x, y in zip(fa_l, ref_a):
+            assert x.dtype == torch.float32 and torch.equal(x, y.float())
+        for x, y in zip(fb_l, ref_b):
+            assert torch.equal(x, y.float())

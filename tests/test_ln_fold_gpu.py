@@ -54,12 +54,40 @@ def test_partials(M, C):
     assert rel_l2(st, ref) < 1e-5, rel_l2(st, ref)
 
 
+@pytest.mark.parametrize("M", [2048, 2000])
+@pytest.mark.parametrize("C", [640, 1280])
+def test_partials_long_k(M, C):
+    """K >= 4096 (the ff out, 2048 x 1280 x 5120): the producer is the 8-wave family's 128 x 160 tile with K split
+    in two (plan8); its epilogue writes the same per-160-column partials (M = 2000: a ragged last row tile)."""
+    h, st = _producer(M, C, K0=5120)
+    torch.cuda.synchronize()
+    hf = h.float().view(M, C // 160, 160)
+    ref = torch.stack([hf.sum(-1), (hf * hf).sum(-1)], -1)
+    assert torch.isfinite(st).all()
+    assert rel_l2(st, ref) < 1e-5, rel_l2(st, ref)
+
+
+def test_long_k_producer_output_matches_torch():
+    from fdhip import ops
+    M, C, K0 = 2048, 1280, 5120
+    att, wo = rnd(M, K0), rnd(C, K0, scale=K0 ** -0.5)
+    bo = torch.randn(C, device=DEV) * 0.1
+    res = rnd(M, C, scale=2.0)
+    st = torch.zeros((M, C // 160, 2), device=DEV)
+    h = ops.gemm(att, wo, bias=bo, residual=res, out=res.clone(), ln_out=st)
+    y = att.float() @ wo.float().T + bo + res.float()
+    assert rel_l2(h, y) < 6e-3, rel_l2(h, y)
+    h2 = ops.gemm(att, wo, bias=bo, residual=res, out=res.clone())  # no partials: the 3-split 256 x 128 plan
+    assert rel_l2(h2, y) < 6e-3, rel_l2(h2, y)
+
+
 @pytest.mark.parametrize("M", [2048, 120])
 @pytest.mark.parametrize("C", [640, 1280])
+@pytest.mark.parametrize("K0", [640, 5120])
 @pytest.mark.parametrize("kind", ["qkv", "q", "geglu"])
-def test_consumer_matches_layer_norm_then_linear(M, C, kind):
+def test_consumer_matches_layer_norm_then_linear(M, C, K0, kind):
     from fdhip import ops
-    h, st = _producer(M, C)
+    h, st = _producer(M, C, K0)
     gamma = 1.0 + 0.2 * torch.randn(C, device=DEV)
     beta = 0.2 * torch.randn(C, device=DEV)
     n = {"qkv": 3 * C, "q": C, "geglu": 8 * C}[kind]

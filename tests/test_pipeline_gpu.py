@@ -203,3 +203,17 @@ def test_c2_headline_matches_golden():
 
 
 C2_BARS = {"step1": 63.0, "final": 60.0, "image": 49.5}  # measured 69.1 / 66.1 / 55.6 dB (r02), 6 dB under
+
+
+def test_preprocess_on_device_matches_numpy():
+    """_preprocess maps the uint8 pixels on the device; every one of the 256 values per channel lands on the fp16
+    bits of the host formula VaeImageProcessor uses (np.float32 x / 255 * 2 - 1, then fp16)."""
+    import types
+    from FaithDiff.pipelines.pipeline_FaithDiff_tlc import FaithDiffStableDiffusionXLPipeline as P
+    v = np.arange(256, dtype=np.uint8)
+    arr = np.stack([v, v[::-1], np.roll(v, 77)], -1).reshape(16, 16, 3)
+    img = Image.fromarray(arr)
+    got = P._preprocess(types.SimpleNamespace(device=torch.device("cuda", 0)), img, 16, 16)
+    want = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0 * 2.0 - 1.0).reshape(-1, 3).to(torch.float16)
+    assert got.dtype == torch.float16 and got.shape == (256, 3)
+    assert torch.equal(got.cpu(), want)
