@@ -183,9 +183,11 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
     lda = a.stride(-2) if lda is None else lda
     M = (a.numel() // a.shape[-1]) // batch if M is None else M
     nout = N // 2 if act == "geglu" else N
-    odt = out_dtype or a.dtype
+    odt = out_dtype or (out.dtype if out is not None else a.dtype)  # a given out buffer fixes the output type
     if out is None:
         out = torch.empty((batch, M, nout) if batch > 1 else (M, nout), dtype=odt, device=a.device)
+    elif out.dtype != odt:
+        raise ValueError(f"gemm: out dtype {out.dtype} != out_dtype {odt}")
     p = L.GemmParams()
     p.A, p.B, p.C = a.data_ptr(), w.data_ptr(), out.data_ptr()
     p.lda, p.ldb = lda, ldw

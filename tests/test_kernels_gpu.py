@@ -53,6 +53,22 @@ def test_gemm_plain(dtype, M, N, K):
     assert rel_l2(out, ref) < TOL[dtype], rel_l2(out, ref)
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K", [(1280, 320), (13760, 1280), (1282, 2816)])
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
+def test_gemm_few_rows_gemv(M, N, K, odt):
+    """M <= 4 (time / add-embedding MLPs at the CFG pair, time_emb_proj, text projection): the weight-streaming
+    GEMV path of fd_gemm, with alpha, bias, SiLU and a residual in its epilogue; N not a multiple of 4 included."""
+    from fdhip import ops
+    a, w = rnd(M, K), rnd(N, K, scale=K ** -0.5)
+    bias = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV).to(odt)
+    out = torch.empty(M, N, device=DEV, dtype=odt)
+    ops.gemm(a, w, bias=bias, residual=res, act="silu", alpha=0.5, out=out)
+    ref = F.silu(0.5 * (a.float() @ w.float().T) + bias) + res.float()
+    assert rel_l2(out, ref) < (6e-3 if odt == torch.bfloat16 else 1e-5), rel_l2(out, ref)
+
+
 @pytest.mark.parametrize("act", ["silu", "gelu", "quickgelu"])
 def test_gemm_act_residual_rowbias(act):
     from fdhip import ops
