@@ -5,9 +5,16 @@
 // coalesced (16-B vectors along C), and writes per-group (sum, sumsq) partials; (2) gn_finalize: one
 // wave per (image, group) folds them in fp64 (E[x^2]-E[x]^2 in double) into (mean, rstd); (3) gn_apply: every
 // block builds per-channel scale/shift in LDS and streams its rows: y = x*scale[c] + shift[c] (+ SiLU).
+#include <stdlib.h>
+
 #include "fd_common.h"
 
 #define GN_MAXC 2560
+
+static int env_gn(const char* n, int d) {
+  const char* v = getenv(n);
+  return v ? atoi(v) : d;
+}
 
 static inline int gn_rows_per_chunk(int nimg, int HW) {
   // chunk count chosen from HW alone: the per-(image, group) reduction order -- and so
@@ -16,7 +23,8 @@ static inline int gn_rows_per_chunk(int nimg, int HW) {
   // Large images (the VAE at 512^2 / 1024^2: HW up to 1M rows) get up to 1024 chunks of >= 64 rows: 256 chunks
   // of 4096 rows left one 4-wave block per CU, latency-bound at ~4 TB/s.
   (void)nimg;
-  const int target = HW / 64 > 1024 ? 1024 : (HW / 64 < 256 ? 256 : HW / 64);
+  static const int lo = env_gn("FD_GN_MIN_CHUNKS", 256);  // A/B knob: chunk floor for small images
+  const int target = HW / 64 > 1024 ? 1024 : (HW / 64 < lo ? lo : HW / 64);
   int r = 1;
   while ((HW + r - 1) / r > target) r *= 2;
   return r;
@@ -213,8 +221,9 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
   const int NV = (C / 8 > 256) ? 2 : 1;
   if (NV == 2 && (C % 16)) return FD_ERR_SHAPE;
   // apply: ~1024 blocks in total, each a run of whole rows
+  static const int apply_blocks = env_gn("FD_GN_APPLY_BLOCKS", 1024);
   int rpb = 1;
-  while ((long long)nimg * ((HW + rpb - 1) / rpb) > 1024) rpb *= 2;
+  while ((long long)nimg * ((HW + rpb - 1) / rpb) > apply_blocks) rpb *= 2;
   const int nblk = (HW + rpb - 1) / rpb;
   if (NV == 1) {
     FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_partial_kernel<T, 1>), dim3(nch, nimg), dim3(256), 0, s, (const T*)x,
@@ -248,8 +257,9 @@ extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)part, (float2*)stats, HW,
                      C, groups, HW / 256, eps);
   FD_LAUNCH_CHECK();
+  static const int apply_blocks = env_gn("FD_GN_APPLY_BLOCKS", 1024);
   int rpb = 1;
-  while ((long long)nimg * ((HW + rpb - 1) / rpb) > 1024) rpb *= 2;
+  while ((long long)nimg * ((HW + rpb - 1) / rpb) > apply_blocks) rpb *= 2;
   const int nblk = (HW + rpb - 1) / rpb;
   FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
                                           (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb, silu));

@@ -46,9 +46,15 @@ for s in SHAPES:
         out = torch.empty(M, N // 2 if act == "geglu" else N, device="cuda", dtype=bf)
         ctr = [0]
 
-        def fn(a=a, ws_=ws_, out=out, act=act):
+        # PROBE_RES=1: residual add (in place, as the UNet's residual-stream GEMMs); PROBE_LNO=1: also write the
+        # LayerNorm-fold partials (ln_out)
+        res = out if os.environ.get("PROBE_RES") == "1" else None
+        lno = (torch.empty((M, N // 160, 2), device="cuda") if os.environ.get("PROBE_LNO") == "1" and N % 160 == 0
+               else None)
+
+        def fn(a=a, ws_=ws_, out=out, act=act, res=res, lno=lno):
             ctr[0] += 1
-            return ops.gemm(a, ws_[ctr[0] % len(ws_)], out=out, act=act)
+            return ops.gemm(a, ws_[ctr[0] % len(ws_)], out=out, act=act, residual=res, ln_out=lno)
         flops = 2 * M * N * K
     st = torch.cuda.Stream()
     # PROBE_GROUPS=n: the launch batches n TLC tiles (ops.tile_groups), so the planner sees m_ref = M / n as in
