@@ -40,5 +40,16 @@ def FaithDiff_pipeline(sdxl_path, VAE_FP16_path, FaithDiff_path, use_fp8=False, 
     return pipe
 
 
-def create_bsrnet(bsrnet_path):
-    raise NotImplementedError("BSRNet pre-pass is outside the denoising hot path (SURVEY 2.1: OUT)")
+def create_bsrnet(bsrnet_path, seed=0):
+    """create_FaithDiff_model.py:39-42: RRDBNet(3, 3, 64, 23, 32, sf=4) with its weights loaded strictly -- from a
+    local .pth (torch.load(weights_only=True)) or .safetensors file, or seeded random weights for 'random-init'."""
+    from .models.bsrnet_arch import BSRNet
+    from .models.unet_2d_condition_vae_extension import _load_file
+    from fdhip import arch
+    bsrnet = BSRNet(in_nc=3, out_nc=3, nf=64, nb=23, gc=32, sf=4)
+    if bsrnet_path == RANDOM_INIT:
+        sd = arch.random_init(arch.bsrnet_param_shapes(23), seed=seed + 31, gain=0.25)
+    else:
+        sd = _load_file(str(bsrnet_path))
+    bsrnet.load_state_dict(sd, strict=True)
+    return bsrnet

@@ -93,6 +93,38 @@ extern "C" int fd_add_strided(const void* x, long long ldx, const void* a, long 
   return FD_OK;
 }
 
+// y[m][n] = alpha * x[m][n] + beta * z[m][n], general row strides (y may alias z: the RRDB residual
+// out * 0.2 + x of the BSRNet pre-pass, bsrnet_arch.py:72-76).  Vectorised when every row is 16-B aligned.
+template <typename T>
+__global__ void axpby_kernel(const T* __restrict__ x, long long ldx, const T* z, long long ldz, T* y,
+                             long long ldy, int M, int N, float alpha, float beta) {
+  typedef typename VecT<T>::v8 V8;
+  const int nv = N / 8;
+  const long long total = (long long)M * nv;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const long long m = e / nv;
+    const int c = (int)(e - m * nv) * 8;
+    const V8 a = *(const V8*)(x + m * ldx + c);
+    const V8 b = *(const V8*)(z + m * ldz + c);
+    V8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (T)(alpha * (float)a[i] + beta * (float)b[i]);
+    *(V8*)(y + m * ldy + c) = o;
+  }
+}
+
+extern "C" int fd_axpby(const void* x, long long ldx, const void* z, long long ldz, void* y, long long ldy, int M,
+                        int N, float alpha, float beta, int dtype, void* stream) {
+  if (!x || !z || !y) return FD_ERR_ARG;
+  if (M <= 0 || N <= 0 || N % 8 || (ldx | ldz | ldy) & 7) return FD_ERR_SHAPE;
+  if (((unsigned long long)x | (unsigned long long)z | (unsigned long long)y) & 15) return FD_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((axpby_kernel<T>), grid1d((long long)M * (N / 8)), dim3(256), 0, s,
+                                          (const T*)x, ldx, (const T*)z, ldz, (T*)y, ldy, M, N, alpha, beta));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // layout transposes.  NCHW [n][C][HW] <-> NHWC [n][HW][C]; 32x32 LDS tiles.
 template <typename TI, typename TO, bool TO_NHWC>

@@ -49,12 +49,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float quickgelu_f(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+// LeakyReLU(negative_slope = 0.2) of the BSRNet pre-pass (bsrnet_arch.py:52, nn.LeakyReLU(0.2))
+__device__ __forceinline__ float lrelu_f(float x) { return x >= 0.f ? x : 0.2f * x; }
 
 __device__ __forceinline__ float act_f(float v, int act) {
   switch (act) {
     case FD_ACT_SILU: return silu_f(v);
     case FD_ACT_GELU: return gelu_f(v);
     case FD_ACT_QUICKGELU: return quickgelu_f(v);
+    case FD_ACT_LRELU: return lrelu_f(v);
     default: return v;
   }
 }

@@ -438,6 +438,9 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
           } else if (act == FD_ACT_QUICKGELU) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[it][i] = quickgelu_f(v[it][i]);
+          } else if (act == FD_ACT_LRELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = lrelu_f(v[it][i]);
           }
         }
         if (R) {

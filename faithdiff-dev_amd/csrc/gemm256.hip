@@ -320,6 +320,9 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
           } else if (act == FD_ACT_QUICKGELU) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[it][i] = quickgelu_f(v[it][i]);
+          } else if (act == FD_ACT_LRELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[it][i] = lrelu_f(v[it][i]);
           }
           if (R) {
 #pragma unroll

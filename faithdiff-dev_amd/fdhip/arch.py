@@ -333,3 +333,22 @@ def vae_decode_flops(h, w):
         prev = c
     f += 2.0 * hh * ww * 3 * 9 * rch[-1]
     return f
+
+
+# BSRNet pre-pass (FaithDiff/models/bsrnet_arch.py:77-98, RRDBNet(in_nc=3, out_nc=3, nf=64, nb=23, gc=32, sf=4)):
+# the reference's state-dict keys and shapes.
+def bsrnet_param_shapes(nb=23, nf=64, gc=32, in_nc=3, out_nc=3):
+    d = {}
+
+    def conv(name, cin, cout):
+        d[name + ".weight"] = (cout, cin, 3, 3)
+        d[name + ".bias"] = (cout,)
+    conv("conv_first", in_nc, nf)
+    for i in range(nb):
+        for j in (1, 2, 3):
+            for k in range(1, 6):
+                conv(f"RRDB_trunk.{i}.RDB{j}.conv{k}", nf + (k - 1) * gc, gc if k < 5 else nf)
+    for n in ("trunk_conv", "upconv1", "upconv2", "HRconv"):
+        conv(n, nf, nf)
+    conv("conv_last", nf, out_nc)
+    return d

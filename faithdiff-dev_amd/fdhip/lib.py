@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FD_LIB_PATH") or os.path.join(_HERE, "libfaithdiff_hip.so")
 
 FD_BF16, FD_F16, FD_F32 = 0, 1, 2
-ACT = {"none": 0, "silu": 1, "gelu": 2, "quickgelu": 3, "geglu": 4}
+ACT = {"none": 0, "silu": 1, "gelu": 2, "quickgelu": 3, "geglu": 4, "lrelu": 5}
 _ERR = {-1: "FD_ERR_SHAPE", -2: "FD_ERR_DTYPE", -3: "FD_ERR_ARCH", -4: "FD_ERR_HIP", -5: "FD_ERR_ARG"}
 
 c_vp, c_int, c_ll, c_f, c_char_p = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_char_p
@@ -63,6 +63,7 @@ _SIGS = {
     "fd_concat_channels": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_ll, c_int, c_vp]),
     "fd_unary": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_vp]),
     "fd_add_strided": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_int, c_int, c_vp]),
+    "fd_axpby": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_f, c_f, c_int, c_vp]),
     "fd_nchw_to_nhwc": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_f, c_int, c_int, c_vp]),
     "fd_nhwc_to_nchw": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_f, c_int, c_int, c_vp]),
     "fd_transpose": (c_int, [c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_int, c_ll, c_ll, c_int, c_vp]),

@@ -292,9 +292,10 @@ def fold_layer_norm(w, gamma, beta, bias=None, dtype=torch.bfloat16):
 
 
 def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C1=None, out=None, rowbias=None,
-            residual=None, act="none", out_dtype=None, upsample_size=None, gn=None):
+            residual=None, act="none", out_dtype=None, upsample_size=None, gn=None, lda=None, alpha=1.0):
     """Implicit-GEMM 3x3 conv on NHWC x [nimg*H*W, Cin] (or concat(x, x2) along C) with packed weight wp.
-    upsample=True: nearest-resize to upsample_size (default 2H x 2W) folded into the gather."""
+    upsample=True: nearest-resize to upsample_size (default 2H x 2W) folded into the gather.  lda: pixel stride
+    of x when it is a channel slice of a wider buffer (default Cin); alpha scales the accumulator (before bias)."""
     Cout, K = wp.shape
     Cin = K // 9
     Hl, Wl = ((2 * H, 2 * W) if upsample_size is None else tuple(upsample_size)) if upsample else (H, W)
@@ -309,7 +310,7 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
     p = L.GemmParams()
     p.A, p.B, p.C = x.data_ptr(), wp.data_ptr(), out.data_ptr()
     p.C1 = 0 if x2 is None else C1
-    p.lda = Cin if x2 is None else C1
+    p.lda = (Cin if lda is None else lda) if x2 is None else C1
     p.ldb, p.ldc = K, out.stride(-2)
     p.M, p.N, p.K, p.batch = M, Cout, K, 1
     p.bias = bias.data_ptr() if bias is not None else None
@@ -319,7 +320,7 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
         p.rowbias, p.rowbias_ld, p.rows_per_group = rowbias.data_ptr(), rowbias.stride(0), Hout * Wout
     else:
         p.rows_per_group = 1
-    p.alpha, p.act = 1.0, L.ACT[act]
+    p.alpha, p.act = alpha, L.ACT[act]
     p.dtype, p.out_dtype = L.dtype_code(x.dtype), L.dtype_code(odt)
     p.conv, p.nimg, p.Hin, p.Win, p.Cin = 1, nimg, H, W, Cin
     p.Hout, p.Wout, p.stride, p.pad, p.upsample = Hout, Wout, stride, pad, int(upsample)
@@ -439,6 +440,15 @@ def unary(x, out, act="none"):
 def add_strided(x, ldx, a, lda, out, ldy, M, N):
     L.check(L.load().fd_add_strided(L.ptr(x), ldx, L.ptr(a), lda, L.ptr(out), ldy, M, N, L.dtype_code(x.dtype),
                                     L.dtype_code(out.dtype), L.stream()), "fd_add_strided")
+    return out
+
+
+def axpby(x, z, out, alpha, beta, M=None, N=None):
+    """out = alpha * x + beta * z over [M, N] with each tensor's own row stride (out may alias z)."""
+    M = x.shape[0] if M is None else M
+    N = x.shape[-1] if N is None else N
+    L.check(L.load().fd_axpby(L.ptr(x), x.stride(0), L.ptr(z), z.stride(0), L.ptr(out), out.stride(0), M, N,
+                              float(alpha), float(beta), L.dtype_code(x.dtype), L.stream()), "fd_axpby")
     return out
 
 

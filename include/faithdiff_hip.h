@@ -31,7 +31,7 @@ typedef enum {
 } fd_status;
 
 enum { FD_BF16 = 0, FD_F16 = 1, FD_F32 = 2 };
-enum { FD_ACT_NONE = 0, FD_ACT_SILU = 1, FD_ACT_GELU = 2, FD_ACT_QUICKGELU = 3, FD_ACT_GEGLU = 4 };
+enum { FD_ACT_NONE = 0, FD_ACT_SILU = 1, FD_ACT_GELU = 2, FD_ACT_QUICKGELU = 3, FD_ACT_GEGLU = 4, FD_ACT_LRELU = 5 };
 
 /* ---------------------------------------------------------------------------------------------
  * GEMM / implicit-GEMM convolution on MFMA (v_mfma_f32_16x16x32_{bf16,f16}), operands staged through
@@ -209,6 +209,10 @@ int fd_unary(const void* x, void* y, long long n, int act, int dtype, int out_dt
 /* y[m][n] = x[m][n] (+ a[m][n] if a != NULL), general row strides; dtype cast allowed. */
 int fd_add_strided(const void* x, long long ldx, const void* a, long long lda, void* y, long long ldy, int M, int N,
                    int dtype, int out_dtype, void* stream);
+/* y[m][n] = alpha * x[m][n] + beta * z[m][n] (bf16/f16, N % 8 == 0, 16-B aligned rows; y may alias z).
+ * Replaces the RRDB residual `out * 0.2 + x` of the BSRNet pre-pass (bsrnet_arch.py:72-76). */
+int fd_axpby(const void* x, long long ldx, const void* z, long long ldz, void* y, long long ldy, int M, int N,
+             float alpha, float beta, int dtype, void* stream);
 /* NCHW <-> NHWC transposes (dtype in, out_dtype out; scale applied). */
 int fd_nchw_to_nhwc(const void* x, void* y, int nimg, int C, int HW, float scale, int dtype, int out_dtype,
                     void* stream);
