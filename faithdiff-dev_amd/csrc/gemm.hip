@@ -383,13 +383,16 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   typedef __attribute__((ext_vector_type(8))) TO TO8;
   const bool lno = LNP && p.ln_out != nullptr;
   float2* lnslot = (float2*)(smem + LNS_OFF);
-  if (vec && m0 + BM <= M && n0o + BNO <= Nout) {
+  // vector epilogue for every tile with whole rows; a tile that runs past N (Nout % 8 == 0 under vec) skips its
+  // 8-column chunks beyond N (the BSRNet dense convs: N = 32 on 64-column tiles)
+  const bool full_n = n0o + BNO <= Nout;
+  if (vec && m0 + BM <= M) {
     float v[ITER][8], bv[ITER][8], rv[ITER][8];
     TO8 res[ITER];
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int e = tid + it * NTHR;
-      if (TOT % NTHR == 0 || e < TOT) {
+      if ((TOT % NTHR == 0 || e < TOT) && (full_n || n0o + (e - (e / VPR) * VPR) * 8 < Nout)) {
         const int r = e / VPR, cv = e - (e / VPR) * VPR;
         const int m = m0 + r, n = n0o + cv * 8;
         *(f32x4*)&v[it][0] = *(const f32x4*)(ep + r * LDE + cv * 8);
@@ -412,7 +415,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int e = tid + it * NTHR;
-      if (TOT % NTHR == 0 || e < TOT) {
+      if ((TOT % NTHR == 0 || e < TOT) && (full_n || n0o + (e - (e / VPR) * VPR) * 8 < Nout)) {
         const int r = e / VPR, cv = e - (e / VPR) * VPR;
         const int m = m0 + r, n = n0o + cv * 8;
         if (!GEGLU) {
@@ -611,46 +614,52 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------ M <= 4
-// Rows-of-a-few GEMM (the UNet's time / add-embedding MLPs and the per-resnet time_emb_proj at M = CFG rows = 2,
-// the text projection): a weight-streaming GEMV.  One wave per output column n streams W[n][0..K) once in 16-B
-// vectors (every lane a contiguous run of 8 k), multiplies by the M <= 4 rows of A (L1/L2-resident) in fp32,
-// wave-reduces, and runs the fused epilogue (alpha, bias, activation, residual).  The 64-row MFMA tile it replaces
-// wasted 62 of 64 rows and covered N = 1280 with 20 workgroups (~18 us per launch for 3 MB of weights).
-template <typename T, typename TO, int MR>
+// Rows-of-a-few GEMM (the UNet's time / add-embedding MLPs and the per-resnet time_emb_proj at M = CFG rows = 2 per
+// TLC tile, the text projection): a weight-streaming GEMV.  One wave per output column n streams W[n][0..K) in 16-B
+// vectors (every lane a contiguous run of 8 k), multiplies by the rows of A four at a time in fp32, wave-reduces,
+// and runs the fused epilogue (alpha, bias, activation, residual).  Chosen by the per-tile row count (m_ref <= 4),
+// so a forward batching n tiles (M = 2n rows) takes the same kernel, and every row is summed in the same order
+// whatever M is: batching stays bitwise.  The 64-row MFMA tile it replaces wasted 62 of 64 rows and covered
+// N = 1280 with 20 workgroups (~18 us per launch for 3 MB of weights).
+template <typename T, typename TO>
 __global__ void __launch_bounds__(256) gemv_rows_kernel(const fd_gemm_params p) {
   typedef typename VecT<T>::v8 V8;
+  constexpr int MR = 4;
   const int lane = threadIdx.x & 63;
   const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (n >= p.N) return;
   const T* __restrict__ A = (const T*)p.A;
   const T* __restrict__ W = (const T*)p.B + (long long)n * p.ldb;
-  float acc[MR];
-#pragma unroll
-  for (int m = 0; m < MR; ++m) acc[m] = 0.f;
   const int nv = p.K / 8;
-  for (int v = lane; v < nv; v += 64) {
-    const V8 w = *(const V8*)(W + v * 8);
+  for (int mb = 0; mb < p.M; mb += MR) {
+    float acc[MR];
 #pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      if (m < p.M) {
-        const V8 a = *(const V8*)(A + (long long)m * p.lda + v * 8);
+    for (int m = 0; m < MR; ++m) acc[m] = 0.f;
+    for (int v = lane; v < nv; v += 64) {
+      const V8 w = *(const V8*)(W + v * 8);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[m] += (float)a[i] * (float)w[i];
+      for (int m = 0; m < MR; ++m) {
+        if (mb + m < p.M) {
+          const V8 a = *(const V8*)(A + (long long)(mb + m) * p.lda + v * 8);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[m] += (float)a[i] * (float)w[i];
+        }
       }
     }
-  }
 #pragma unroll
-  for (int m = 0; m < MR; ++m) acc[m] = wave_sum(acc[m]);
-  if (lane < p.M) {
-    float x = 0.f;
+    for (int m = 0; m < MR; ++m) acc[m] = wave_sum(acc[m]);
+    const int row = mb + lane;
+    if (lane < MR && row < p.M) {
+      float x = 0.f;
 #pragma unroll
-    for (int m = 0; m < MR; ++m)
-      if (m == lane) x = acc[m];
-    x *= p.alpha;
-    if (p.bias) x += p.bias[n];
-    x = act_f(x, p.act);
-    if (p.residual) x += (float)((const TO*)p.residual)[(long long)lane * p.ldr + n];
-    ((TO*)p.C)[(long long)lane * p.ldc + n] = (TO)x;
+      for (int m = 0; m < MR; ++m)
+        if (m == lane) x = acc[m];
+      x *= p.alpha;
+      if (p.bias) x += p.bias[n];
+      x = act_f(x, p.act);
+      if (p.residual) x += (float)((const TO*)p.residual)[(long long)row * p.ldr + n];
+      ((TO*)p.C)[(long long)row * p.ldc + n] = (TO)x;
+    }
   }
 }
 
@@ -658,15 +667,13 @@ __global__ void __launch_bounds__(256) gemv_rows_kernel(const fd_gemm_params p) 
 template <typename T, typename TO>
 static int try_gemv_rows(const fd_gemm_params* p, hipStream_t s) {
   static const int on = env_int("FD_GEMV", 1);
-  if (!on || p->M > 4 || p->conv || (p->batch > 1) || p->rowbias || p->ln_in || p->ln_out || p->gn_part ||
-      p->act == FD_ACT_GEGLU || p->A2 || (p->K % 8) || (p->lda % 8) || (p->ldb % 8))
+  const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
+  if (!on || m_ref > 4 || p->M > 4096 || p->conv || (p->batch > 1) || p->rowbias || p->ln_in || p->ln_out ||
+      p->gn_part || p->act == FD_ACT_GEGLU || p->A2 || (p->K % 8) || (p->lda % 8) || (p->ldb % 8))
     return 0;
   if ((((unsigned long long)p->A) | ((unsigned long long)p->B)) & 15) return 0;
   dim3 grid((p->N + 3) / 4), block(256);
-  if (p->M <= 2)
-    hipLaunchKernelGGL((gemv_rows_kernel<T, TO, 2>), grid, block, 0, s, *p);
-  else
-    hipLaunchKernelGGL((gemv_rows_kernel<T, TO, 4>), grid, block, 0, s, *p);
+  hipLaunchKernelGGL((gemv_rows_kernel<T, TO>), grid, block, 0, s, *p);
   return hipGetLastError() == hipSuccess ? 1 : -1;
 }
 

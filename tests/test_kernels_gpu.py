@@ -69,6 +69,20 @@ def test_gemm_few_rows_gemv(M, N, K, odt):
     assert rel_l2(out, ref) < (6e-3 if odt == torch.bfloat16 else 1e-5), rel_l2(out, ref)
 
 
+def test_gemm_few_rows_batched_tiles_bitwise():
+    """The GEMV is chosen by the per-tile row count (m_ref = CFG pair = 2): 13 tiles batched into one launch (M = 26,
+    as C3's tile batches) give every row bitwise what one tile's launch gives."""
+    from fdhip import ops
+    K, N = 1280, 13760
+    a, w = rnd(26, K), rnd(N, K, scale=K ** -0.5)
+    bias = torch.randn(N, device=DEV)
+    with ops.tile_groups(13):
+        big = ops.gemm(a, w, bias=bias, act="silu", out_dtype=torch.float32)
+    for t in (0, 5, 12):
+        one = ops.gemm(a[2 * t:2 * t + 2].contiguous(), w, bias=bias, act="silu", out_dtype=torch.float32)
+        assert torch.equal(big[2 * t:2 * t + 2], one)
+
+
 @pytest.mark.parametrize("act", ["silu", "gelu", "quickgelu"])
 def test_gemm_act_residual_rowbias(act):
     from fdhip import ops
