@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(64) gn_finalize_kernel(const float2* __restric
   }
 }
 
-template <typename T, int NV>
+template <typename T, int NV, int U = 4>
 __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                        const float2* __restrict__ stats, const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, int HW, int C, int groups,
@@ -160,7 +160,6 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
   long long e = eb + t;
   // the block's first U vectors are requested before the stats / gamma / beta round trips, and each
   // batch of U is in flight together (a load-compute-store loop exposes one HBM latency per vector)
-  constexpr int U = 4;
   V8 val[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
@@ -237,8 +236,15 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)ws, stats, HW, C, groups,
                      nch, eps);
   FD_LAUNCH_CHECK();
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
-                                          (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb, silu));
+  static const int apply_u = env_gn("FD_GN_APPLY_U", 4);  // vectors in flight per thread (A/B knob: 4 or 8)
+  if (apply_u == 8) {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1, 8>), dim3(nblk, nimg), dim3(256), 0, s,
+                                            (const T*)x, (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb,
+                                            silu));
+  } else {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
+                                            (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb, silu));
+  }
   FD_LAUNCH_CHECK();
   return FD_OK;
 }
@@ -261,8 +267,15 @@ extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma
   int rpb = 1;
   while ((long long)nimg * ((HW + rpb - 1) / rpb) > apply_blocks) rpb *= 2;
   const int nblk = (HW + rpb - 1) / rpb;
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
-                                          (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb, silu));
+  static const int apply_u = env_gn("FD_GN_APPLY_U", 4);  // vectors in flight per thread (A/B knob: 4 or 8)
+  if (apply_u == 8) {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1, 8>), dim3(nblk, nimg), dim3(256), 0, s,
+                                            (const T*)x, (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb,
+                                            silu));
+  } else {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
+                                            (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb, silu));
+  }
   FD_LAUNCH_CHECK();
   return FD_OK;
 }
