@@ -55,7 +55,7 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_FP8_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02e_gemm_traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02f_gemm_traffic.json")
 
 
 def parse(argv=None):
