@@ -43,7 +43,8 @@ def rnd(*shape, dtype=torch.bfloat16, scale=1.0):
 # ------------------------------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,N,K", [(8192, 640, 640), (2048, 1280, 1280), (2048, 3840, 1280), (77, 1280, 2048),
-                                   (2, 1280, 320), (300, 200, 128), (32768, 320, 640), (1000, 4, 2880)])
+                                   (2, 1280, 320), (300, 200, 128), (32768, 320, 640), (1000, 4, 2880),
+                                   (8192, 32, 1152), (5000, 24, 640)])
 def test_gemm_plain(dtype, M, N, K):
     from fdhip import ops
     a, w = rnd(M, K, dtype=dtype), rnd(N, K, dtype=dtype, scale=K ** -0.5)
