@@ -13,6 +13,8 @@ values: x2 / x4 of this or an earlier block, or the buffer's initial zeros).  Le
 scale (alpha = 0.2 with a pre-scaled bias) and the residual add are in the conv epilogue; the RRDB's own
 out * 0.2 + x is one fd_axpby.  Nearest x2 upsampling is folded into upconv1 / upconv2's gather.
 """
+import math
+
 import torch
 
 from . import lib as L
@@ -108,7 +110,6 @@ class HipRRDBNet:
     def deg_remove(self, x, tile_size=512, tile_pad=16):
         """bsrnet_arch.py:116-175: tiles of tile_size (tile_pad context each side, clipped at the border) upscaled
         one by one, the unpadded part pasted into a zero image."""
-        import math
         b, c, h, w = x.shape
         x = x.to(self.device, torch.float32)
         out = torch.zeros((b, c, h * 4, w * 4), device=self.device, dtype=torch.float32)
