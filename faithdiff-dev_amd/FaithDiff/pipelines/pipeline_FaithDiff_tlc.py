@@ -218,25 +218,32 @@ class FaithDiffStableDiffusionXLPipeline:
         prompt = [prompt] if isinstance(prompt, str) else prompt
         batch_size = len(prompt) if prompt is not None else prompt_embeds.shape[0]
 
-        def run(texts_per_encoder, skip):
-            embs, pooled = [], None
-            for texts, tok, enc in zip(texts_per_encoder, tokenizers, encoders):
-                ids = tok(texts, padding="max_length", max_length=tok.model_max_length, truncation=True,
-                          return_tensors="pt").input_ids
+        def run(texts_per_encoder, skips):
+            """One forward per encoder over every text group given (each group: len(texts) rows); group g keeps
+            hidden_states[-2] (skip None) or [-(skip + 2)] and the final encoder's pooled row (:587-615).  The
+            prompt and the negative prompt go through as one batch (the reference encodes them in two passes,
+            :587-615 / :651-675): half the weight streaming and launches, the same rows."""
+            sizes = [len(t) for t in texts_per_encoder[0]]
+            embs, pooled = [[] for _ in sizes], None
+            for groups, tok, enc in zip(texts_per_encoder, tokenizers, encoders):
+                ids = torch.cat([tok(texts, padding="max_length", max_length=tok.model_max_length, truncation=True,
+                                     return_tensors="pt").input_ids for texts in groups], 0)
                 out = enc(ids, output_hidden_states=True)
                 pooled = out[0]  # only the final encoder's pooled output is kept (:607-608)
-                embs.append(out.hidden_states[-2] if skip is None else out.hidden_states[-(skip + 2)])
-            return torch.cat(embs, dim=-1), pooled
+                r0 = 0
+                for g, (n, skip) in enumerate(zip(sizes, skips)):
+                    h = out.hidden_states[-2] if skip is None else out.hidden_states[-(skip + 2)]
+                    embs[g].append(h[r0:r0 + n])
+                    r0 += n
+            res, r0 = [], 0
+            for g, n in enumerate(sizes):
+                res.append((torch.cat(embs[g], dim=-1), pooled[r0:r0 + n]))
+                r0 += n
+            return res
 
-        if prompt_embeds is None:
-            prompt_2 = prompt_2 or prompt
-            prompt_2 = [prompt_2] if isinstance(prompt_2, str) else prompt_2
-            prompt_embeds, pooled_prompt_embeds = run([prompt, prompt_2], clip_skip)
         zero_out = negative_prompt is None and self.config.force_zeros_for_empty_prompt
-        if do_classifier_free_guidance and negative_prompt_embeds is None and zero_out:
-            negative_prompt_embeds = torch.zeros_like(prompt_embeds)
-            negative_pooled_prompt_embeds = torch.zeros_like(pooled_prompt_embeds)
-        elif do_classifier_free_guidance and negative_prompt_embeds is None:
+        encode_neg = do_classifier_free_guidance and negative_prompt_embeds is None and not zero_out
+        if encode_neg:
             negative_prompt = negative_prompt or ""
             negative_prompt_2 = negative_prompt_2 or negative_prompt
             negative_prompt = batch_size * [negative_prompt] if isinstance(negative_prompt, str) else negative_prompt
@@ -249,7 +256,20 @@ class FaithDiffStableDiffusionXLPipeline:
                 raise ValueError(f"`negative_prompt`: {negative_prompt} has batch size {len(negative_prompt)}, but "
                                  f"`prompt`: {prompt} has batch size {batch_size}. Please make sure that passed "
                                  "`negative_prompt` matches the batch size of `prompt`.")
-            negative_prompt_embeds, negative_pooled_prompt_embeds = run([negative_prompt, negative_prompt_2], None)
+        if prompt_embeds is None:
+            prompt_2 = prompt_2 or prompt
+            prompt_2 = [prompt_2] if isinstance(prompt_2, str) else prompt_2
+            if encode_neg:
+                (prompt_embeds, pooled_prompt_embeds), (negative_prompt_embeds, negative_pooled_prompt_embeds) = run(
+                    [[prompt, negative_prompt], [prompt_2, negative_prompt_2]], [clip_skip, None])
+                return prompt_embeds, negative_prompt_embeds, pooled_prompt_embeds, negative_pooled_prompt_embeds
+            (prompt_embeds, pooled_prompt_embeds), = run([[prompt], [prompt_2]], [clip_skip])
+        if do_classifier_free_guidance and negative_prompt_embeds is None and zero_out:
+            negative_prompt_embeds = torch.zeros_like(prompt_embeds)
+            negative_pooled_prompt_embeds = torch.zeros_like(pooled_prompt_embeds)
+        elif encode_neg:
+            (negative_prompt_embeds, negative_pooled_prompt_embeds), = run(
+                [[negative_prompt], [negative_prompt_2]], [None])
         return prompt_embeds, negative_prompt_embeds, pooled_prompt_embeds, negative_pooled_prompt_embeds
 
     def check_inputs(self, lr_img, prompt, prompt_2, height, width, callback_steps, negative_prompt=None,

@@ -217,3 +217,18 @@ def test_preprocess_on_device_matches_numpy():
     want = torch.from_numpy(np.asarray(img, dtype=np.float32) / 255.0 * 2.0 - 1.0).reshape(-1, 3).to(torch.float16)
     assert got.dtype == torch.float16 and got.shape == (256, 3)
     assert torch.equal(got.cpu(), want)
+
+
+def test_encode_prompt_batches_prompt_and_negative():
+    """encode_prompt runs the prompt and the negative prompt through each text encoder as one batch; each row
+    matches encoding it alone (CFG off) to bf16 rounding, and the pooled rows are the right ones."""
+    pipe = pipe_and_oracle()[0]
+    pe, npe, ppe, nppe = pipe.encode_prompt("a restored photo of a cat", do_classifier_free_guidance=True,
+                                            negative_prompt="blurry, noisy")
+    a, _, pa, _ = pipe.encode_prompt("a restored photo of a cat", do_classifier_free_guidance=False)
+    b, _, pb, _ = pipe.encode_prompt("blurry, noisy", do_classifier_free_guidance=False)
+    for x, y in ((pe, a), (ppe, pa), (npe, b), (nppe, pb)):
+        assert x.shape == y.shape
+        r = ((x.float() - y.float()).norm() / y.float().norm()).item()
+        assert r < 2e-2, r
+    assert ((pe.float() - npe.float()).norm() / pe.float().norm()).item() > 0.05
