@@ -46,7 +46,7 @@ class HipCLIPTextModel:
                 fc2=(W(f"{q}.mlp.fc2.weight"), Fp(f"{q}.mlp.fc2.bias"))))
         self.fln = (Fp("text_model.final_layer_norm.weight"), Fp("text_model.final_layer_norm.bias"))
         self.proj = W("text_projection.weight") if cfg.get("proj") else None
-        self.graphs = GraphCache(max_graphs=4)
+        self.graphs = GraphCache(max_graphs=4, min_uses=1)  # one call per encoder per image: capture at once
 
     @torch.no_grad()
     def forward(self, input_ids):

@@ -5,7 +5,8 @@ removes the host from the denoise loop (pipeline_FaithDiff_tlc.py:1330-1376 laun
 per tile).  ``GraphCache.run(key, fn, inputs)``:
 
   * the first call with a given key runs ``fn`` eagerly (it also sizes the split-K / GroupNorm workspaces,
-    which must not grow inside a capture);
+    which must not grow inside a capture); with ``min_uses=1`` that same first call then captures and replays
+    (for forwards called once per image, e.g. the text encoders);
   * the second call captures ``fn`` on static copies of the inputs into a private memory pool;
   * every later call copies the inputs into those static buffers (a few MB at most) and replays.
 
@@ -43,6 +44,8 @@ class GraphCache:
             self._uses[key] += 1
             if self._uses[key] < self.min_uses:
                 return fn(*inputs)
+            if self.min_uses <= 1 and self._uses[key] == 1:
+                fn(*inputs)  # min_uses = 1: one eager run sizes the workspaces, then capture in the same call
             ent = self._capture(key, fn, inputs)
         else:
             self._graphs.move_to_end(key)
