@@ -146,11 +146,15 @@ def max_over_ranks(x, world, dev):
 
 
 # ------------------------------------------------------------------------------------------------ model
-def build_pipe(dev, fp8):
+def build_pipe(dev, fp8, world=1):
+    """The product factory; with N ranks it is built collectively (process_group=WORLD): rank 0 alone reads / draws
+    the weights and broadcasts them over RCCL before anything is packed (pipe.last_broadcast_bytes)."""
     from CKPT_PTH import FAITHDIFF_PATH, SDXL_PATH, VAE_FP16_PATH  # 'random-init' sentinels offline
     from FaithDiff.create_FaithDiff_model import FaithDiff_pipeline
+    t0 = time.perf_counter()
     pipe = FaithDiff_pipeline(SDXL_PATH, VAE_FP16_PATH, FAITHDIFF_PATH, use_fp8=fp8, fp8_mfma=fp8 or None, seed=0,
-                              init_device=dev)
+                              init_device=dev, process_group=dist.group.WORLD if world > 1 else None)
+    pipe.build_s = time.perf_counter() - t0
     pipe = pipe.to(dev)
     pipe.unet.release_host_weights()
     return pipe
@@ -493,10 +497,13 @@ def main(argv=None):
     from fdhip import lib as L
     L.require_device()
     dev = torch.device("cuda", local)
-    pipe = build_pipe(dev, args.fp8)
+    pipe = build_pipe(dev, args.fp8, world)
     result = {"n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
               "vs_baseline": None, "dtype": "fp8-e4m3+bf16" if args.fp8 else "bf16",
               "data": "synthetic (seeded random-init SDXL+FaithDiff weights, synthetic latents/conditions/images)"}
+    if world > 1:  # rank 0 drew the weights, every other rank received them (FaithDiff_pipeline(process_group=))
+        result["weights_broadcast"] = {"bytes": pipe.last_broadcast_bytes, "build_s": round(pipe.build_s, 2),
+                                       "backend": dist.get_backend()}
 
     if args.workload in ("c3", "c4"):
         size, tag = (args.c3_size, "C3") if args.workload == "c3" else (args.c4_size, "C4")

@@ -9,34 +9,47 @@ pickle execution).  Extra keyword arguments (defaults keep the reference call wo
 ``seed`` (random-init seed), ``unet_dtype`` (bf16 per the north star; fp16 also supported),
 ``init_device`` ('cpu' for host-generated weights shared with the CPU oracle, 'cuda' for fast init),
 ``fp8_mfma`` (with ``use_fp8``: opt in to the e4m3 MFMA for the transformer Linears; default None = the
-FD_FP8_MFMA env var, default off = the reference's 16-bit arithmetic on e4m3 weights).
+FD_FP8_MFMA env var, default off = the reference's 16-bit arithmetic on e4m3 weights), ``process_group`` (a
+torch.distributed group whose ranks all call this together: rank 0 of the group alone reads the checkpoints (or
+draws the random init), the others read nothing and receive every weight by broadcast over RCCL / gloo --
+``pipe.last_broadcast_bytes``; the tokenizers' vocabulary files are still read by every rank).
 """
 import torch
 
 from utils.system import quantize_8bit
 
-from .models.unet_2d_condition_vae_extension import RANDOM_INIT, AutoencoderKL, UNet2DConditionModel
+from .models.unet_2d_condition_vae_extension import RANDOM_INIT, RECEIVE, AutoencoderKL, UNet2DConditionModel
 from .pipelines.pipeline_FaithDiff_tlc import FaithDiffStableDiffusionXLPipeline
 from .schedulers import DDPMScheduler
 
 
 def FaithDiff_pipeline(sdxl_path, VAE_FP16_path, FaithDiff_path, use_fp8=False, seed=0,
-                       unet_dtype=torch.bfloat16, init_device="cpu", fp8_mfma=None):
+                       unet_dtype=torch.bfloat16, init_device="cpu", fp8_mfma=None, process_group=None):
     dtype = torch.float16
+    tok_path = sdxl_path
+    if process_group is not None:
+        import torch.distributed as dist
+        if dist.get_rank(process_group) != 0:  # a receiver: reads no weights, rank 0 broadcasts them below
+            sdxl_path = VAE_FP16_path = FaithDiff_path = RECEIVE
     vae = AutoencoderKL.from_pretrained(VAE_FP16_path, seed=seed, init_device=init_device).to(dtype=dtype)
     unet = UNet2DConditionModel.from_pretrained(sdxl_path, subfolder="unet", variant="fp16", seed=seed,
                                                 init_device=init_device)
     fd_path = FaithDiff_path
-    if fd_path != RANDOM_INIT and not str(fd_path).endswith((".bin", ".safetensors")):
+    if fd_path not in (RANDOM_INIT, RECEIVE) and not str(fd_path).endswith((".bin", ".safetensors")):
         fd_path = f"{fd_path}/FaithDiff.bin"
     unet.load_additional_layers(weight_path=fd_path, dtype=dtype, init_device=init_device)
     if use_fp8:
         quantize_8bit(unet, fp8_mfma=fp8_mfma)
     unet.to(dtype=unet_dtype)
+    from .models.clip_text import load_tokenizer
     pipe = FaithDiffStableDiffusionXLPipeline.from_pretrained(
         sdxl_path, vae=vae, add_sample=True, denoise_encoder=unet.denoise_encoder, DDPM_scheduler=DDPMScheduler(),
-        add_watermarker=False, torch_dtype=dtype, variant="fp16", unet=unet, seed=seed)
+        add_watermarker=False, torch_dtype=dtype, variant="fp16", unet=unet, seed=seed,
+        tokenizer=load_tokenizer(tok_path, "tokenizer", pad_token_id=49407),
+        tokenizer_2=load_tokenizer(tok_path, "tokenizer_2", pad_token_id=0))
     pipe.unet = unet
+    if process_group is not None:
+        pipe.broadcast_weights(process_group)
     return pipe
 
 

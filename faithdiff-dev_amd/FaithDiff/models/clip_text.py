@@ -64,10 +64,12 @@ def load_tokenizer(path, subfolder, pad_token_id):
 
 
 def _load_weights(path, subfolder, cfg, seed):
-    from .unet_2d_condition_vae_extension import RANDOM_INIT, _check_keys, _load_file
+    from .unet_2d_condition_vae_extension import RANDOM_INIT, RECEIVE, _check_keys, _empty, _load_file
     shapes = arch.clip_param_shapes(cfg)
     if path == RANDOM_INIT:
         return arch.random_init(shapes, seed=seed)
+    if path == RECEIVE:
+        return _empty(shapes)
     d = os.path.join(str(path), subfolder)
     for n in ("model.fp16.safetensors", "model.safetensors", "pytorch_model.fp16.bin", "pytorch_model.bin"):
         if os.path.exists(os.path.join(d, n)):
@@ -129,8 +131,10 @@ class CLIPTextModel:
         return out["last_hidden_state"]
 
     @torch.no_grad()
-    def __call__(self, input_ids, output_hidden_states=False, **kwargs):
-        out = self.hip().forward_f32(input_ids)  # fp32, one private copy per call (graph-replayed forward)
+    def __call__(self, input_ids, output_hidden_states=False, row_groups=1, **kwargs):
+        """transformers' call surface.  row_groups (this build's addition, used by encode_prompt): the rows are
+        that many independent prompt batches, each computed bitwise as if encoded alone."""
+        out = self.hip().forward_f32(input_ids, groups=row_groups)  # fp32, one private copy per call
         o = _Output([self._first(out)])
         o.hidden_states = tuple(out["hidden_states"]) if output_hidden_states else None
         o.last_hidden_state = out["last_hidden_state"]

@@ -20,6 +20,13 @@ from fdhip import arch, ops
 from fdhip import lib as L
 
 RANDOM_INIT = "random-init"
+# Path sentinel for a rank that builds a pipeline collectively (FaithDiff_pipeline(process_group=...)) and is not
+# the source: it reads nothing and allocates the architecture's tensors, which rank 0 then broadcasts.
+RECEIVE = "receive-from-rank0"
+
+
+def _empty(shapes, device="cpu"):
+    return {k: torch.empty(s, dtype=torch.float32, device=device) for k, s in shapes.items()}
 
 
 def _load_file(path):
@@ -81,6 +88,8 @@ class UNet2DConditionModel:
         shapes = arch.unet_param_shapes(with_extras=False)
         if path == RANDOM_INIT:
             sd = arch.random_init(shapes, seed=seed, device=init_device)
+        elif path == RECEIVE:
+            sd = _empty(shapes, init_device)
         else:
             sd = _load_file(_find_weights(path, subfolder, variant))
             _check_keys(sd, shapes, True, "UNet2DConditionModel")
@@ -92,6 +101,8 @@ class UNet2DConditionModel:
         den_shapes = arch.encoder_param_shapes("denoise_encoder.", with_out=False)
         if weight_path is None or weight_path == RANDOM_INIT:
             extra = arch.random_init({**ext_shapes, **den_shapes}, seed=self._seed + 7, device=init_device)
+        elif weight_path == RECEIVE:
+            extra = _empty({**ext_shapes, **den_shapes}, init_device)
         else:
             extra = _load_file(weight_path)
         self.load_state_dict(extra, strict=True)
@@ -307,6 +318,8 @@ class AutoencoderKL:
         shapes = arch.vae_param_shapes()
         if path == RANDOM_INIT:
             sd = arch.random_init(shapes, seed=seed + 3, device=init_device)
+        elif path == RECEIVE:
+            sd = _empty(shapes, init_device)
         else:
             sd = _load_file(_find_weights(path, subfolder or ""))
             _check_keys(sd, shapes, True, "AutoencoderKL")

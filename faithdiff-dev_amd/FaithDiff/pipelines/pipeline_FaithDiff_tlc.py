@@ -31,7 +31,7 @@ from fdhip import ops
 
 from ..schedulers import DDPMScheduler, EulerDiscreteScheduler
 from .pipeline_output import FaithDiffStableDiffusionXLPipelineOutput
-from .tile_parallel import TileShard, broadcast, run_tile_loop
+from .tile_parallel import TileShard, broadcast, broadcast_state_dict, run_tile_loop, staging_device
 from .tlc import TileGrid
 
 
@@ -92,6 +92,8 @@ class FaithDiffStableDiffusionXLPipeline:
         self.tile_batch = int(os.environ.get("FD_TILE_BATCH", "13"))
         self.process_group = None    # torch.distributed group for tile parallelism (None: single GPU)
         self.last_timings = {}
+        self._weights_group = None   # the group broadcast_weights last synchronised the weights over
+        self.last_broadcast_bytes = 0
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -148,11 +150,46 @@ class FaithDiffStableDiffusionXLPipeline:
 
     def enable_tile_parallel(self, group=None):
         """Shard TLC tiles over the ranks of `group` (default WORLD) with one all-gather per step; the tiled VAE
-        encode / decode and the tiled denoise encoder shard their tiles the same way (fdhip.tiling.map_tiles)."""
+        encode / decode and the tiled denoise encoder shard their tiles the same way (fdhip.tiling.map_tiles).
+        First makes every rank's weights rank 0's (broadcast_weights), unless the pipeline was built or synced over
+        this group already: the tiles of one image must all see the same model."""
         self.process_group = group if group is not None else dist.group.WORLD
+        if self._weights_group is not self.process_group:
+            self.broadcast_weights(self.process_group)
         for m in (self.vae, self.denoise_encoder):
             if m is not None:
                 m.process_group = self.process_group
+
+    def _weight_owners(self):
+        te = None if isinstance(self.text_encoder, SyntheticTextEncoder) else self.text_encoder
+        return [("unet", self.unet), ("vae", self.vae), ("denoise_encoder", self.denoise_encoder),
+                ("text_encoder", te), ("text_encoder_2", self.text_encoder_2)]
+
+    def broadcast_weights(self, group=None, src=0):
+        """Every component's weights (UNet + FaithDiff extras, VAE, denoise encoder, both text encoders) become
+        rank `src`'s over `group` -- one manifest + bucketed broadcasts per component over RCCL (gloo on CPU),
+        before anything is packed for the kernels (packed modules built earlier are dropped and rebuilt from the
+        received weights on next use).  Returns the bytes broadcast (also in ``last_broadcast_bytes``)."""
+        group = group if group is not None else dist.group.WORLD
+        if dist.get_world_size(group) == 1:  # nothing to synchronise
+            self._weights_group, self.last_broadcast_bytes = group, 0
+            return 0
+        dev = staging_device(group)
+        total = 0
+        for name, m in self._weight_owners():
+            sd = getattr(m, "_sd", None)
+            if sd is None:
+                continue
+            if not sd:
+                raise RuntimeError(f"broadcast_weights: the {name} host weights were released "
+                                   "(release_host_weights) before they were synchronised over the group")
+            total += broadcast_state_dict(sd, group, src, device=dev)
+            for attr in ("_hip", "_enc", "_dec"):
+                if getattr(m, attr, None) is not None:
+                    setattr(m, attr, None)
+        self._weights_group = group
+        self.last_broadcast_bytes = total
+        return total
 
     # ------------------------------------------------------------------ properties (:915-948)
     @property
@@ -222,13 +259,16 @@ class FaithDiffStableDiffusionXLPipeline:
             """One forward per encoder over every text group given (each group: len(texts) rows); group g keeps
             hidden_states[-2] (skip None) or [-(skip + 2)] and the final encoder's pooled row (:587-615).  The
             prompt and the negative prompt go through as one batch (the reference encodes them in two passes,
-            :587-615 / :651-675): half the weight streaming and launches, the same rows."""
+            :587-615 / :651-675): half the weight streaming and launches, and -- run as row groups of equal size
+            -- bitwise the rows each pass gives alone."""
             sizes = [len(t) for t in texts_per_encoder[0]]
             embs, pooled = [[] for _ in sizes], None
             for groups, tok, enc in zip(texts_per_encoder, tokenizers, encoders):
                 ids = torch.cat([tok(texts, padding="max_length", max_length=tok.model_max_length, truncation=True,
                                      return_tensors="pt").input_ids for texts in groups], 0)
-                out = enc(ids, output_hidden_states=True)
+                rg = len(sizes) if len(set(sizes)) == 1 else 1
+                out = enc(ids, output_hidden_states=True, row_groups=rg) if hasattr(enc, "hip") else \
+                    enc(ids, output_hidden_states=True)
                 pooled = out[0]  # only the final encoder's pooled output is kept (:607-608)
                 r0 = 0
                 for g, (n, skip) in enumerate(zip(sizes, skips)):

@@ -38,16 +38,37 @@ class TileShard:
         return buf[:self.ntiles]
 
 
+def _dtype_of(name):
+    return getattr(torch, name.split(".")[-1])
+
+
 def broadcast_state_dict(sd, group=None, src=0, device=None, bucket_bytes=256 << 20):
-    """Make every rank's weights rank `src`'s, in place (weights broadcast once over RCCL/xGMI,
-    instead of every rank reading the checkpoint; with same-seed random init it is a no-op consistency pass).
-    Tensors go through `device` (the rank's GPU under RCCL, CPU under gloo) in flat buckets of one dtype, in
-    sorted key order, so every rank issues the same collectives."""
+    """Make every rank's weights rank `src`'s, in place, and return the bytes broadcast (weights go
+    out once over RCCL/xGMI instead of every rank reading the checkpoint; create_FaithDiff_model.py:13-22 loads
+    them per process).  Rank `src` first broadcasts a manifest (key, dtype, shape); a receiving rank allocates
+    whatever it lacks or holds with another dtype / shape (it may start from an empty dict, having read nothing)
+    and drops keys the source does not have.  The tensors then go through `device` (the rank's GPU under RCCL,
+    the CPU under gloo) in flat buckets of one dtype, in sorted key order, so every rank issues the same
+    collectives."""
     if group is None and (not dist.is_initialized() or dist.get_world_size() == 1):
-        return sd
+        return 0
     src_global = dist.get_global_rank(group, src) if group is not None else src
+    me = dist.get_rank(group)
     keys = sorted(k for k, v in sd.items() if torch.is_tensor(v))
-    by_dtype = {}
+    man = [[(k, str(sd[k].dtype), tuple(sd[k].shape)) for k in keys] if me == src else None]
+    mdev = device if device is not None and torch.device(device).type == "cuda" else None
+    dist.broadcast_object_list(man, src=src_global, group=group, device=mdev)
+    if me != src:
+        where = next((v.device for v in sd.values() if torch.is_tensor(v)), torch.device("cpu"))
+        want = {k: (_dtype_of(dt), shp) for k, dt, shp in man[0]}
+        for k in [k for k in sd if k not in want]:
+            del sd[k]
+        for k, (dt, shp) in want.items():
+            v = sd.get(k)
+            if not torch.is_tensor(v) or v.dtype != dt or tuple(v.shape) != tuple(shp):
+                sd[k] = torch.empty(shp, dtype=dt, device=where)
+        keys = sorted(want)
+    by_dtype, total = {}, 0
     for k in keys:
         by_dtype.setdefault(sd[k].dtype, []).append(k)
     for dt in sorted(by_dtype, key=str):
@@ -59,13 +80,21 @@ def broadcast_state_dict(sd, group=None, src=0, device=None, bucket_bytes=256 <<
             if bucket and (k is None or nbytes >= bucket_bytes):
                 flat = torch.cat([sd[b].reshape(-1) for b in bucket]).to(device or sd[bucket[0]].device)
                 broadcast(flat, src_global, group)
+                total += flat.numel() * flat.element_size()
                 off = 0
                 for b in bucket:
                     n = sd[b].numel()
                     sd[b].copy_(flat[off:off + n].view_as(sd[b]).to(sd[b].device))
                     off += n
                 bucket, nbytes = [], 0
-    return sd
+    return total
+
+
+def staging_device(group=None):
+    """Where broadcast_state_dict stages its buckets: the rank's GPU under RCCL ('nccl'), the host under gloo."""
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
 
 
 def run_tile_loop(nsteps, shard, tile_shape, compute, blend, device, dtype=torch.float32, on_step=None):

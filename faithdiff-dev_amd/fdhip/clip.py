@@ -10,10 +10,15 @@ legacy eos_token_id == 2 path of both SDXL configs; EOS 49407 is the largest id,
 text_projection without bias.  Each Linear is one fd_gemm (bias / activation / residual in the epilogue), the
 attention one causal fd_flash_attn, the embeddings one fd_embed_tokens; activations bf16 (the reference: fp16).
 
-The forward (~220 launches for bigG) is replayed as one hipGraph per (batch, length) from its second call on
-(fdhip/graphs.py): encode_prompt runs each encoder twice per image (prompt, negative prompt), and eager ctypes
-launches made it ~8 ms of a 1024^2 pipe() call.  The EOS row is picked on the device (argmax of the ids), so
-nothing in the forward needs the host.
+The forward (~220 launches for bigG) is replayed as one hipGraph per (batch, length, row groups)
+(fdhip/graphs.py, GraphCache(min_uses=1): the first call of a shape runs eagerly once to size the workspaces, then
+captures and replays in that same call): eager ctypes launches made encode_prompt ~8 ms of a 1024^2 pipe() call.
+The EOS row is picked on the device (argmax of the ids), so nothing in the forward needs the host.
+
+Batching: encode_prompt sends the prompt and the negative prompt through each encoder as ONE batch of ``groups``
+row groups (the reference makes one pass per prompt).  The forward runs under ops.tile_groups(groups), so every
+fd_gemm sees the per-group row count (m_ref) and picks the kernel, tile family and split-K a solo pass of one
+group would pick: each group's rows are bitwise what encoding it alone gives (GPU test).
 """
 import torch
 
@@ -49,16 +54,18 @@ class HipCLIPTextModel:
         self.graphs = GraphCache(max_graphs=4, min_uses=1)  # one call per encoder per image: capture at once
 
     @torch.no_grad()
-    def forward(self, input_ids):
-        """input_ids [B, T] (any int dtype, host or device).  Returns a dict: hidden_states (list of [B, T, D] in
-        the compute dtype: the embeddings, then each layer's output, as transformers' output_hidden_states),
-        last_hidden_state, pooled ([B, D], final-LN EOS row), text_embeds ([B, proj] with a projection).
-        The tensors are the graph's static outputs from the second call of a shape on: valid until the next
-        call (CLIPTextModel.__call__ copies them out as fp32 straight away)."""
+    def forward(self, input_ids, groups=1):
+        """input_ids [B, T] (any int dtype, host or device); groups: the B rows are that many independent batches
+        of B / groups rows each (bitwise what each group gives alone).  Returns a dict: hidden_states (list of
+        [B, T, D] in the compute dtype: the embeddings, then each layer's output, as transformers'
+        output_hidden_states), last_hidden_state, pooled ([B, D], final-LN EOS row), text_embeds ([B, proj] with a
+        projection).  The tensors are the graph's static outputs: valid until the next call of the same shape
+        (CLIPTextModel.__call__ uses forward_f32, which copies them out straight away)."""
         ids = torch.as_tensor(input_ids)
         B, T = ids.shape
+        groups = self._check_groups(B, groups)
         ids_d = ids.to(device=self.device, dtype=torch.int32).contiguous().reshape(-1)
-        outs = self.graphs.run(("clip", B, T), lambda i: self._forward_dev(i, B, T), [ids_d])
+        outs = self.graphs.run(("clip", B, T, groups), lambda i: self._forward_dev(i, B, T, groups), [ids_d])
         nl = self.cfg["layers"]
         out = dict(hidden_states=list(outs[:nl + 1]), last_hidden_state=outs[nl + 1], pooled=outs[nl + 2])
         if self.proj is not None:
@@ -66,17 +73,18 @@ class HipCLIPTextModel:
         return out
 
     @torch.no_grad()
-    def forward_f32(self, input_ids):
+    def forward_f32(self, input_ids, groups=1):
         """forward() with every output as fp32 (what the transformers surface returns), all of them packed into one
         buffer inside the graph and copied out of its static memory by a single clone -- instead of ~50 separate
         conversions per call.  The returned tensors are views of that private copy."""
         ids = torch.as_tensor(input_ids)
         B, T = ids.shape
+        groups = self._check_groups(B, groups)
         ids_d = ids.to(device=self.device, dtype=torch.int32).contiguous().reshape(-1)
         shapes = []
 
         def packed(i):
-            outs = self._forward_dev(i, B, T)
+            outs = self._forward_dev(i, B, T, groups)
             flat = torch.empty(sum(o.numel() for o in outs), dtype=torch.float32, device=self.device)
             off = 0
             for o in outs:
@@ -85,7 +93,7 @@ class HipCLIPTextModel:
             return flat
         for o in self._out_shapes(B, T):
             shapes.append(o)
-        flat = self.graphs.run(("clip32", B, T), packed, [ids_d]).clone()
+        flat = self.graphs.run(("clip32", B, T, groups), packed, [ids_d]).clone()
         views, off = [], 0
         for shp in shapes:
             n = 1
@@ -99,6 +107,13 @@ class HipCLIPTextModel:
             out["text_embeds"] = views[nl + 3]
         return out
 
+    @staticmethod
+    def _check_groups(B, groups):
+        groups = max(int(groups), 1)
+        if B % groups:
+            raise ValueError(f"{B} rows do not split into {groups} equal groups")
+        return groups
+
     def _out_shapes(self, B, T):
         D = self.cfg["D"]
         shp = [(B, T, D)] * (self.cfg["layers"] + 1) + [(B, T, D), (B, D)]
@@ -106,8 +121,14 @@ class HipCLIPTextModel:
             shp.append((B, self.proj.shape[0]))
         return shp
 
-    def _forward_dev(self, ids_d, B, T):
-        """Device-only body of forward (capturable): a tuple (hidden states..., last, pooled[, text_embeds])."""
+    def _forward_dev(self, ids_d, B, T, groups=1):
+        """Device-only body of forward (capturable): a tuple (hidden states..., last, pooled[, text_embeds]).  Every
+        launch sees the per-group row count (ops.tile_groups), so a batch of `groups` groups is bitwise each group's
+        solo forward."""
+        with ops.tile_groups(groups):
+            return self._forward_body(ids_d, B, T)
+
+    def _forward_body(self, ids_d, B, T):
         D = self.cfg["D"]
         H = D // 64
         M = B * T

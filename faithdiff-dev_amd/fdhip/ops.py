@@ -10,11 +10,16 @@ import torch
 from . import lib as L
 
 _GN_WS = {}
-# Every workspace buffer ever handed out stays allocated: a hipGraph captured while it was current keeps its
-# address and writes there on every replay, so freeing it on growth (and letting the caching allocator hand the
-# memory to another tensor) would let an old graph's replay corrupt that tensor.  Workspaces never grow inside a
-# capture (the graph cache runs every shape eagerly first, which sizes them).
-_WS_KEEP = []
+# Workspace lifetime: a hipGraph captured while a workspace buffer was current keeps its address and writes there
+# on every replay.  GraphCache therefore holds a reference to every live workspace (live_workspaces()) in each
+# entry it captures; when a workspace grows here, the old buffer is dropped from this module and stays allocated
+# exactly as long as some graph captured against it is alive.  Workspaces never grow inside a capture (the graph
+# cache runs every shape eagerly first, which sizes them), and they grow geometrically (2x).
+
+
+def live_workspaces():
+    """The current GroupNorm and split-K workspace buffers (GraphCache keeps them alive with a captured graph)."""
+    return list(_GN_WS.values()) + list(_GEMM_WS.values())
 
 
 def _gn_ws(nbytes, device):
@@ -24,9 +29,8 @@ def _gn_ws(nbytes, device):
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError(f"GroupNorm workspace too small inside graph capture ({nbytes} B): run the shape "
                                "once eagerly or call ops.reserve_gn_workspace first")
-        if ws is not None:
-            _WS_KEEP.append(ws)
-        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        grow = 0 if ws is None else 2 * ws.numel()
+        ws = torch.empty(max(nbytes, grow, 1 << 20), dtype=torch.uint8, device=device)
         _GN_WS[key] = ws
     return ws
 
@@ -57,14 +61,17 @@ class tile_groups:
 
 
 def reserve_gemm_workspace(nbytes, device):
-    """Pre-size the split-K workspace (zeroed: its head holds the tile counters).  Call before capture."""
+    """Pre-size the split-K workspace (zeroed: its head holds the tile counters).  Call before capture.  A graph
+    captured with the old buffer keeps it alive (GraphCache entries hold live_workspaces()); its counters stay
+    zero between launches (the last arriver of every tile resets its counter)."""
     key = torch.device(device)
     ws = _GEMM_WS.get(key)
     if ws is None or ws.numel() < nbytes:
+        grow = 0
         if ws is not None:
             torch.cuda.synchronize(key)
-            _WS_KEEP.append(ws)  # graphs captured with it may replay later (its tile counters stay zero)
-        _GEMM_WS[key] = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=key)
+            grow = 2 * ws.numel()
+        _GEMM_WS[key] = torch.zeros(max(nbytes, grow, 1 << 20), dtype=torch.uint8, device=key)
     return _GEMM_WS[key]
 
 
@@ -80,7 +87,7 @@ def _attach_ws(p, device):
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError(f"fd_gemm split-K workspace too small inside graph capture ({need} B): "
                                "run the forward once eagerly or call ops.reserve_gemm_workspace first")
-        ws = reserve_gemm_workspace(int(need * 1.25), device)
+        ws = reserve_gemm_workspace(need, device)
     p.ws, p.ws_bytes = ws.data_ptr(), ws.numel()
 
 

@@ -15,6 +15,22 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU oracle case")
 
 
+@pytest.fixture(autouse=True)
+def _parity_current_test(request):
+    """tests/golden/parity.py records every measured metric under the running test's id."""
+    import parity
+    parity.CURRENT["test"] = request.node.nodeid
+    yield
+    parity.CURRENT["test"] = None
+
+
+def pytest_sessionfinish(session, exitstatus):
+    import parity
+    path = parity.dump()
+    if path:
+        print(f"\nparity metrics of {len(parity.RECORDS)} tests -> {path}")
+
+
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

@@ -8,6 +8,8 @@ import os
 import numpy as np
 import pytest
 import torch
+
+import parity  # records every measured value (tests/golden/parity.py)
 import torch.nn.functional as F
 
 from oracle import bsrnet as ob
@@ -17,8 +19,7 @@ GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bsrne
 
 
 def rel(a, b):
-    a, b = a.float().cpu(), b.float().cpu()
-    return ((a - b).norm() / b.norm()).item()
+    return parity.rel_l2(a.float().cpu(), b.float().cpu())
 
 
 def test_lrelu_epilogue_and_axpby():

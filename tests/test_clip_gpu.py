@@ -8,12 +8,13 @@ Bars: hidden_states[-2] (what SDXL keeps) and last_hidden_state rel-L2 <= 2e-2, 
 import pytest
 import torch
 
+import parity  # records every measured value (tests/golden/parity.py)
+
 pytestmark = pytest.mark.gpu
 
 
 def rel(a, b):
-    a, b = a.float(), b.float()
-    return ((a - b).norm() / b.norm()).item()
+    return parity.rel_l2(a.float(), b.float())
 
 
 def make_ids(pad, seed=0):
@@ -83,8 +84,9 @@ def test_encode_prompt_dropin_shapes_and_negative():
 
 
 def test_clip_graph_replay_is_bitwise():
-    """The text encoder runs as a hipGraph from its second call of a shape on (fdhip/graphs.py): replays with
-    other token ids give bitwise what the eager forward gives, the EOS row picked on the device included."""
+    """The text encoder runs as a hipGraph (fdhip/graphs.py, min_uses=1: the first call of a shape runs eagerly once,
+    then captures and replays): replays with other token ids give bitwise what the eager forward gives (both
+    references built with the graph cache off), the EOS row picked on the device included."""
     from fdhip import arch
     from fdhip.clip import HipCLIPTextModel, random_clip
     cfg = arch.CLIP_G  # with the projection (text_embeds)
@@ -96,11 +98,11 @@ def test_clip_graph_replay_is_bitwise():
     def snap(o):
         return [t.clone() for t in o["hidden_states"]] + [o["last_hidden_state"].clone(), o["pooled"].clone(),
                                                            o["text_embeds"].clone()]
-    ref_b = snap(hip.forward(b))  # eager (first use of the shape)
     hip.graphs.enabled = False
+    ref_b = snap(hip.forward(b))  # eager
     ref_a = snap(hip.forward(a))  # eager
     hip.graphs.enabled = True
-    got_a = snap(hip.forward(a))  # second use: captured, replayed
+    got_a = snap(hip.forward(a))  # first use: eager sizing run, capture, replay
     got_b = snap(hip.forward(b))  # replay
     got_a2 = snap(hip.forward(a))  # replay
     assert len(hip.graphs) == 1
@@ -121,3 +123,21 @@ def test_clip_graph_replay_is_bitwise():
             assert x.dtype == torch.float32 and torch.equal(x, y.float())
         for x, y in zip(fb_l, ref_b):
             assert torch.equal(x, y.float())
+
+
+def test_clip_row_groups_are_bitwise_solo_passes():
+    """forward(ids of two prompts, groups=2) -- encode_prompt's batched prompt + negative pass -- gives each prompt's
+    rows bitwise as its own B = 1 forward (every GEMM planned on the per-group row count, ops.tile_groups)."""
+    from fdhip import arch
+    from fdhip.clip import HipCLIPTextModel, random_clip
+    for cfg, pad in ((arch.CLIP_L, 49407), (arch.CLIP_G, 0)):
+        hip = HipCLIPTextModel(random_clip(cfg, seed=4), cfg, "cuda", torch.bfloat16)
+        ids = make_ids(pad, seed=6)
+        both = hip.forward_f32(ids, groups=2)
+        solo = [hip.forward_f32(ids[i:i + 1]) for i in range(2)]
+        keys = ["last_hidden_state", "pooled"] + (["text_embeds"] if cfg["proj"] else [])
+        for i in range(2):
+            for k in keys:
+                assert torch.equal(both[k][i:i + 1], solo[i][k]), (cfg["D"], k, i)
+            for x, y in zip(both["hidden_states"], solo[i]["hidden_states"]):
+                assert torch.equal(x[i:i + 1], y)

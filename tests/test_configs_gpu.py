@@ -1,0 +1,98 @@
+"""BASELINE configs[3] (C4) and configs[4] (C5) through the product ``pipe(...)`` on the GPU.
+
+C4 -- "8K input 4x upscale, fp8 UNet weights on CDNA4 fp8 MFMA": the 8K-output reading:
+a 2048^2 degraded image resized x4 (test_wo_llava.py:78-81) to 8192^2, restored at target 1024 -> a 1024^2 latent
+cut into 225 TLC tiles, use_fp8 with the e4m3 MFMA (quantize_8bit, utils/system.py:13-32), tiled VAE encode /
+decode and tiled denoise encoder (1024-px tiles), one Euler step of the 20-step schedule.  The reference has no
+fixture at this size and the fp32 oracle cannot run it in seconds, so the checks are size-independent properties:
+every latent finite, tiles batched 13 and 4 per UNet forward give bitwise the same latents and pixels (a tile's rows
+never depend on which tiles share its forward), and the image is not flat.
+
+C5 -- "batch of 8 RealDeg-style 1024px inputs, 50-step": back-to-back pipe() calls on ONE pipeline with different
+images, prompts and noise, on the 50-step Euler schedule truncated by denoising_end (pipeline:1291-1302; 4 of the
+50 steps run).  The second image's output must be bitwise the output of a fresh pipeline (same seeded weights) that
+only ever saw that image: the graph caches (UNet, VAE, text encoders), the hoisted prompt K/V and condition
+embeddings and the scheduler state must carry nothing from one image to the next (the round-2 NaN bug class,
+commit 55c00ef).  Reference loop: pipeline_FaithDiff_tlc.py:1324-1442, test_wo_llava.py:53-97.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+from PIL import Image
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+from _det import det_tensor, synthetic_degraded  # noqa: E402
+
+import parity  # noqa: E402
+
+
+def _build(seed, use_fp8=False, fp8_mfma=None):
+    from CKPT_PTH import FAITHDIFF_PATH, SDXL_PATH, VAE_FP16_PATH
+    from FaithDiff.create_FaithDiff_model import FaithDiff_pipeline
+    return FaithDiff_pipeline(SDXL_PATH, VAE_FP16_PATH, FAITHDIFF_PATH, seed=seed, init_device="cuda",
+                              use_fp8=use_fp8, fp8_mfma=fp8_mfma).to("cuda:0")
+
+
+def _run(pipe, img, prompt, noise, post, size, target, **kw):
+    cap = {}
+
+    def cb(p, i, t, k):
+        cap["lat"] = k["latents"].detach().float().cpu().clone()
+        cap["steps"] = i + 1
+        return {}
+    out = pipe(lr_img=img, prompt=prompt, negative_prompt="", guidance_scale=5.0, start_point="lr", height=size,
+               width=size, overlap=0.5, target_size=target, latents=noise, posterior_noise=post,
+               callback_on_step_end=cb, output_type="pil", **kw).images
+    return cap["lat"], np.asarray(out[0]), cap["steps"]
+
+
+def test_c4_8k_fp8_225_tiles_tile_batch_bitwise():
+    S = 8192
+    pipe = _build(seed=5, use_fp8=True, fp8_mfma=True)
+    assert pipe.unet.hip().fp8_mfma
+    pipe.enable_vae_tiling()
+    img = synthetic_degraded(S // 4, S // 4, 11).resize((S, S), Image.LANCZOS)
+    noise, post = det_tensor((1, 4, S // 8, S // 8), 51), det_tensor((1, 4, S // 8, S // 8), 52)
+    from FaithDiff.pipelines.tlc import TileGrid
+    assert TileGrid(S // 8, S // 8, (128, 128), 0.5).ntiles == 225
+    res = []
+    for tb in (13, 4):
+        pipe.tile_batch = tb
+        res.append(_run(pipe, img, "an 8K photo of a tiled floor", noise, post, S, (1024, 1024),
+                        num_inference_steps=20, denoising_end=0.05))
+    (lat13, img13, n13), (lat4, img4, n4) = res
+    assert n13 == n4 == 1
+    assert lat13.shape == (1, 4, 1024, 1024) and img13.shape == (S, S, 3)
+    assert torch.isfinite(lat13).all()
+    assert torch.equal(lat13, lat4)
+    assert (img13 == img4).all()
+    parity.record("image_std", float(img13.std()), bar=">1")
+    assert img13.std() > 1.0
+
+
+def test_c5_back_to_back_images_bitwise_fresh_pipeline():
+    S = 1024
+    imgs = [synthetic_degraded(S, S, 21), synthetic_degraded(S, S, 22)]
+    prompts = ["a restored photo of a harbour at dusk", "blurry scan of a handwritten letter, restored"]
+    noise = [det_tensor((1, 4, S // 8, S // 8), 60 + i) for i in range(2)]
+    post = [det_tensor((1, 4, S // 8, S // 8), 70 + i) for i in range(2)]
+    kw = dict(num_inference_steps=50, denoising_end=0.08)
+    pipe = _build(seed=3)
+    lat_a, img_a, n_a = _run(pipe, imgs[0], prompts[0], noise[0], post[0], S, (1024, 1024), **kw)
+    lat_b, img_b, n_b = _run(pipe, imgs[1], prompts[1], noise[1], post[1], S, (1024, 1024), **kw)
+    assert n_a == n_b == 4  # 981, 961, 941, 921 of the 50-step schedule
+    del pipe
+    torch.cuda.empty_cache()
+    fresh = _build(seed=3)
+    lat_f, img_f, _ = _run(fresh, imgs[1], prompts[1], noise[1], post[1], S, (1024, 1024), **kw)
+    assert torch.isfinite(lat_b).all() and not torch.equal(lat_a, lat_b)
+    assert torch.equal(lat_b, lat_f), "second image of a reused pipeline differs from a fresh pipeline's"
+    assert (img_b == img_f).all()
+    # and the first image again on the fresh pipeline (its caches now hold image b): bitwise the first run
+    lat_a2, img_a2, _ = _run(fresh, imgs[0], prompts[0], noise[0], post[0], S, (1024, 1024), **kw)
+    assert torch.equal(lat_a, lat_a2) and (img_a == img_a2).all()

@@ -9,6 +9,7 @@ Bars (stated per test):
 """
 import pytest
 import torch
+from parity import rel_l2  # noqa: E402  (records every measured value)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -20,9 +21,6 @@ def _dev():
     lib.require_device()
 
 
-def rel_l2(a, b):
-    a, b = a.double(), b.double()
-    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
 def e4m3(x):
@@ -190,7 +188,6 @@ def test_fp8_mfma_pipeline_tracks_reference_arithmetic():
     Linears on the e4m3 MFMA, against the same pipeline on the same e4m3 weights with the reference's 16-bit
     arithmetic (quantize_8bit default): the activation quantization error over the Euler loop, measured as latent
     / image PSNR (bars FP8_PIPE_BARS, about 6 dB under the measured values)."""
-    import math
 
     import numpy as np
     from CKPT_PTH import FAITHDIFF_PATH, SDXL_PATH, VAE_FP16_PATH
@@ -219,11 +216,9 @@ def test_fp8_mfma_pipeline_tracks_reference_arithmetic():
     assert pipe.unet.hip().fp8_mfma
     lat8, img8 = run()
 
-    def psnr(a, b, peak):
-        mse = float(((a - b) ** 2).mean())
-        return 99.0 if mse == 0 else 10 * math.log10(peak ** 2 / mse)
-    p_lat = psnr(lat8, lat16, float(lat16.max() - lat16.min()))
-    p_img = psnr(img8, img16, 255.0)
+    import parity
+    p_lat = parity.psnr(lat8, lat16, float(lat16.max() - lat16.min()), "latent_psnr_db")
+    p_img = parity.psnr(img8, img16, 255.0, "image_psnr_db")
     print(f"use_fp8 pipeline, e4m3 MFMA vs 16-bit on e4m3 weights: latent PSNR {p_lat:.2f} dB, image {p_img:.2f} dB")
     assert p_lat >= FP8_PIPE_BARS["latent"] and p_img >= FP8_PIPE_BARS["image"]
 

@@ -6,14 +6,12 @@ import os
 import pytest
 import torch
 import torch.nn.functional as F
+from parity import rel_l2  # noqa: E402  (records every measured value)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def rel_l2(a, b):
-    a, b = a.float(), b.float()
-    return ((a - b).norm() / b.norm()).item()
 
 
 def both(fn):

@@ -11,6 +11,7 @@ import math
 import pytest
 import torch
 import torch.nn.functional as F
+from parity import rel_l2  # noqa: E402  (records every measured value)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -23,9 +24,6 @@ def _dev():
     torch.manual_seed(0)
 
 
-def rel_l2(a, b):
-    a, b = a.float(), b.float()
-    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
 def rnd(*shape, dtype=torch.bfloat16, scale=1.0):

@@ -10,6 +10,8 @@ import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
+from parity import rel_l2  # noqa: E402  (records every measured value)
+
 
 pytestmark = pytest.mark.gpu
 
@@ -23,14 +25,8 @@ def _dev():
     torch.manual_seed(0)
 
 
-def rel_l2(a, b):
-    a, b = a.float(), b.float()
-    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def maxrel(a, b):
-    a, b = a.float(), b.float()
-    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
 TOL = {torch.bfloat16: 6e-3, torch.float16: 1.5e-3}

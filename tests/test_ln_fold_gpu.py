@@ -10,6 +10,7 @@ N = C and for small M), edge tiles (M not a multiple of 64), and the partials th
 import pytest
 import torch
 import torch.nn.functional as F
+from parity import rel_l2  # noqa: E402  (records every measured value)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -22,9 +23,6 @@ def _dev():
     torch.manual_seed(0)
 
 
-def rel_l2(a, b):
-    a, b = a.float(), b.float()
-    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
 def rnd(*shape, dtype=torch.bfloat16, scale=1.0):

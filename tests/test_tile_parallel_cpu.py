@@ -137,3 +137,45 @@ def test_tile_parallel_bitwise_equals_single_rank(world, h, w):
     assert sum(c for _, c in covered) == shard1.ntiles
     for rank, out, begin, count in res:
         assert (out == ref.numpy()).all(), f"rank {rank} canvas differs"
+
+
+def _seeded_pipeline_worker(rank, world, port, q):
+    """FaithDiff_pipeline('random-init', seed=rank): the ranks start from different weights; enable_tile_parallel
+    makes them rank 0's before anything is packed."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import zlib
+        from CKPT_PTH import FAITHDIFF_PATH, SDXL_PATH, VAE_FP16_PATH
+        from FaithDiff.create_FaithDiff_model import FaithDiff_pipeline
+        pipe = FaithDiff_pipeline(SDXL_PATH, VAE_FP16_PATH, FAITHDIFF_PATH, seed=rank)
+        before = zlib.crc32(pipe.unet._sd["conv_in.weight"].numpy())
+        pipe.enable_tile_parallel()
+        dig = {}
+        for name, m in pipe._weight_owners():
+            if m is not None:
+                dig[name] = {k: zlib.crc32(v.contiguous().view(torch.uint8).numpy()) for k, v in m._sd.items()}
+        q.put((rank, before, dig, pipe.last_broadcast_bytes, pipe.vae.process_group is not None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_enable_tile_parallel_broadcasts_rank0_weights():
+    """SURVEY 8(e) "RCCL broadcast of weights" through the product surface, gloo world 2 on CPU: ranks built from
+    different seeds hold bitwise rank 0's UNet (+ extras), VAE, denoise encoder and both text encoders after
+    pipe.enable_tile_parallel() (the GPU leg, tests/test_tile_parallel_gpu.py, then checks the canvases)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seeded_pipeline_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (_, b0, d0, n0, t0), (_, b1, d1, n1, t1) = res
+    assert b0 != b1, "the ranks were meant to start from different weights"
+    assert set(d0) == {"unet", "vae", "denoise_encoder", "text_encoder", "text_encoder_2"}
+    assert d0 == d1 and n0 == n1 > 10e9 and t0 and t1

@@ -30,10 +30,10 @@ def _free_port():
     return p
 
 
-def _pipe():
+def _pipe(seed=1):
     from CKPT_PTH import FAITHDIFF_PATH, SDXL_PATH, VAE_FP16_PATH
     from FaithDiff.create_FaithDiff_model import FaithDiff_pipeline
-    pipe = FaithDiff_pipeline(SDXL_PATH, VAE_FP16_PATH, FAITHDIFF_PATH, seed=1, init_device="cuda").to("cuda:0")
+    pipe = FaithDiff_pipeline(SDXL_PATH, VAE_FP16_PATH, FAITHDIFF_PATH, seed=seed, init_device="cuda").to("cuda:0")
     # small VAE tiles so the decode is tiled (and sharded) at this size: 4 x 3 latent tiles of 32
     vae = pipe.vae
     vae.tile_sample_min_size, vae.tile_latent_min_size = 256, 32
@@ -70,10 +70,13 @@ def _worker(rank, world, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        pipe = _pipe()
+        # the ranks start from DIFFERENT random weights (seed 1 and 8): enable_tile_parallel broadcasts rank 0's
+        # (broadcast_weights) before anything is packed, so both must reproduce the seed-1 single-process run
+        pipe = _pipe(seed=1 + 7 * rank)
         pipe.enable_tile_parallel()
+        nbytes = pipe.last_broadcast_bytes
         lat, img = _call(pipe, "pil")
-        q.put((rank, lat, img))
+        q.put((rank, lat, img, nbytes))
     finally:
         dist.destroy_process_group()
 
@@ -124,7 +127,8 @@ def test_call_tile_parallel_two_ranks_one_gpu_bitwise():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    for rank, lat, img in res:
+    for rank, lat, img, nbytes in res:
+        assert nbytes > 10e9, f"rank {rank}: only {nbytes} bytes broadcast"
         assert (lat == lat_ref).all(), f"rank {rank}: latents differ from the single-process run"
         assert (img == img_ref).all(), f"rank {rank}: image differs from the single-process run"
 

@@ -129,3 +129,58 @@ def test_pickle_payloads_are_refused(weights, tmp_path):
     unet = UNet2DConditionModel(dict(weights["unet"]))
     with pytest.raises(Exception):
         unet.load_additional_layers(weight_path=str(p))
+
+
+def _pipe_digest(pipe):
+    """{component: {key: (dtype, shape, crc32 of the bytes)}} over every weight the pipeline holds."""
+    import zlib
+    out = {}
+    for name, m in pipe._weight_owners():
+        if m is None:
+            continue
+        out[name] = {k: (str(v.dtype), tuple(v.shape), zlib.crc32(v.detach().contiguous().view(torch.uint8).numpy()))
+                     for k, v in m._sd.items()}
+    return out
+
+
+def _collective_build_worker(rank, world, port, paths, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from FaithDiff.create_FaithDiff_model import FaithDiff_pipeline
+        # only rank 0 may read: every other rank gets paths that do not exist, so any read would raise
+        p = paths if rank == 0 else ("/nonexistent/sdxl", "/nonexistent/vae", "/nonexistent/fd")
+        pipe = FaithDiff_pipeline(*p, process_group=dist.group.WORLD)
+        q.put((rank, _pipe_digest(pipe), pipe.last_broadcast_bytes))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collective_build_only_rank0_reads(weights):
+    """FaithDiff_pipeline(..., process_group=WORLD) on 2 gloo ranks: rank 0 reads the local diffusers checkpoints, rank
+    1 reads nothing (its paths do not exist) and receives every weight by broadcast (manifest + dtype buckets,
+    tile_parallel.broadcast_state_dict) -- both end with the same keys, dtypes, shapes and bytes, which are the files'
+    (create_FaithDiff_model.py:13-22 loads them in every process instead)."""
+    import socket
+
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    paths = (weights["sdxl"], weights["vae"], weights["fd"])
+    procs = [ctx.Process(target=_collective_build_worker, args=(r, 2, port, paths, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (_, d0, n0), (_, d1, n1) = res
+    assert d0 == d1 and n0 == n1 > 5e9
+    import zlib
+    want = weights["vae_sd"]["decoder.conv_in.weight"]
+    assert d0["vae"]["decoder.conv_in.weight"][2] == zlib.crc32(want.contiguous().view(torch.uint8).numpy())
