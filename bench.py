@@ -367,6 +367,18 @@ def run_pipeline_image(pipe, img, H, W, steps, target, seed=42):
     return el, tm
 
 
+def run_batch(pipe, imgs, prompts, size, steps, seed=42):
+    """One product pipe(lr_img=[...], prompt=[...]) call over several images (C5); returns its EventTimer."""
+    tm = EventTimer()
+    gen = torch.Generator(device=pipe.device).manual_seed(seed)
+    tm("call_start", 0)
+    pipe(lr_img=imgs, prompt=prompts, negative_prompt="", num_inference_steps=steps, guidance_scale=5.0,
+         generator=gen, start_point="lr", height=size, width=size, overlap=0.5, target_size=(1024, 1024), timer=tm)
+    tm("call_end", 0)
+    torch.cuda.synchronize()
+    return tm
+
+
 def pipeline_leg(pipe, size, steps=20):
     img = synthetic_image(size, size, 5)
     run_pipeline_image(pipe, img, size, size, 2, (1024, 1024))  # warm: captures the UNet / VAE graphs
@@ -523,20 +535,26 @@ def main(argv=None):
                                   "parallelism": f"tile-sharded x{world}"}, tag.lower(): r})
     elif args.workload == "c5":
         ims = list(range(rank, args.c5_images, world))
-        img = synthetic_image(args.size, args.size, 7)
-        run_pipeline_image(pipe, img, args.size, args.size, 2, (1024, 1024))
+        imgs = [synthetic_image(args.size, args.size, 70 + i) for i in ims]
+        prompts = [f"A restored photograph, number {i}, sharp and clean." for i in ims]
+        run_batch(pipe, imgs, prompts, args.size, 2)  # warm: captures the batched UNet / VAE graphs
         barrier(world)
         t0 = time.perf_counter()
-        for i in ims:
-            run_pipeline_image(pipe, img, args.size, args.size, args.c5_steps, (1024, 1024), seed=100 + i)
+        tm = run_batch(pipe, imgs, prompts, args.size, args.c5_steps)
         barrier(world)
         t = max_over_ranks(time.perf_counter() - t0, world, dev)
-        result.update({"metric": "C5 images/sec, 1024px 50-step pipe(...) calls, batch of 8 split over ranks",
+        st = tm.step_ms()
+        result.update({"metric": "C5 images/sec, 1024px 50-step, batch of 8 split over ranks",
                        "value": round(args.c5_images / t, 4), "unit": "images/s", "scaling": "strong",
-                       "ms_per_step": round(t / (len(ims) * args.c5_steps) * 1e3, 2),
+                       "ms_per_step": round(float(np.median(st)), 2),
                        "config": {"workload": f"C5: {args.c5_images} images of {args.size}^2 x {args.c5_steps} "
-                                              "Euler steps, image-parallel replicas", "global_batch": args.c5_images,
-                                  "parallelism": f"replicas x{world}"}})
+                                              "Euler steps; each rank restores its images in ONE pipe(lr_img=[...]) "
+                                              "call (their CFG pairs share UNet forwards, each with its own prompt)",
+                                  "global_batch": args.c5_images, "images_per_rank": len(ims),
+                                  "parallelism": f"replicas x{world}"},
+                       "c5": {"s_total": round(t, 3), "loop_s": round(sum(st) / 1e3, 3),
+                              "pre_loop_s": round(tm.span_ms("call_start", "loop_start") / 1e3, 3),
+                              "decode_s": round(tm.span_ms("decode_start", "decode") / 1e3, 3)}})
     else:
         loop = C2Loop(pipe, args.size, rank)
         for i in range(args.warmup):

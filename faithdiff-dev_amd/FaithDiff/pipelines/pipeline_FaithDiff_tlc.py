@@ -266,7 +266,7 @@ class FaithDiffStableDiffusionXLPipeline:
             for groups, tok, enc in zip(texts_per_encoder, tokenizers, encoders):
                 ids = torch.cat([tok(texts, padding="max_length", max_length=tok.model_max_length, truncation=True,
                                      return_tensors="pt").input_ids for texts in groups], 0)
-                rg = len(sizes) if len(set(sizes)) == 1 else 1
+                rg = sum(sizes)  # every prompt its own group of 77 rows: bitwise its solo pass
                 out = enc(ids, output_hidden_states=True, row_groups=rg) if hasattr(enc, "hip") else \
                     enc(ids, output_hidden_states=True)
                 pooled = out[0]  # only the final encoder's pooled output is kept (:607-608)
@@ -405,6 +405,15 @@ class FaithDiffStableDiffusionXLPipeline:
                  target_size: Optional[Tuple[int, int]] = None, clip_skip: Optional[int] = None,
                  callback_on_step_end: Optional[Callable[[int, int, Dict], None]] = None,
                  callback_on_step_end_tensor_inputs: List[str] = ["latents"], add_sample: bool = True, **kwargs):
+        if isinstance(lr_img, (list, tuple)) and len(lr_img) > 1:
+            return self._call_images(lr_img, prompt, height=height, width=width,
+                                     num_inference_steps=num_inference_steps, start_point=start_point,
+                                     timesteps=timesteps, denoising_end=denoising_end, overlap=overlap,
+                                     guidance_scale=guidance_scale, negative_prompt=negative_prompt,
+                                     generator=generator, latents=latents, output_type=output_type,
+                                     return_dict=return_dict, guidance_rescale=guidance_rescale,
+                                     original_size=original_size, target_size=target_size,
+                                     callback_on_step_end=callback_on_step_end, add_sample=add_sample, **kwargs)
         callback = kwargs.pop("callback", None)
         callback_steps = kwargs.pop("callback_steps", None)
         posterior_noise = kwargs.pop("posterior_noise", None)  # explicit VAE posterior draw (parity tests)
@@ -560,6 +569,160 @@ class FaithDiffStableDiffusionXLPipeline:
         if not return_dict:
             return (image,)
         return FaithDiffStableDiffusionXLPipelineOutput(images=image)
+
+    @torch.no_grad()
+    def _call_images(self, imgs, prompt, height=None, width=None, num_inference_steps=50, start_point="noise",
+                     timesteps=None, denoising_end=None, overlap=0.5, guidance_scale=5.0, negative_prompt=None,
+                     generator=None, latents=None, output_type="pil", return_dict=True, guidance_rescale=0.0,
+                     original_size=None, target_size=None, callback_on_step_end=None, add_sample=True, **kwargs):
+        """Several images of one size in one call (BASELINE configs[4], C5: a batch of 1024^2 restorations; the
+        reference restores one image per pipe() call, test_wo_llava.py:53-97).  When each image is a single TLC
+        tile (target_size covers the image latent), the images' CFG pairs share UNet forwards (tile_batch images
+        per forward), each pair attending to its own prompt (HipUNet.set_context with several prompt pairs), with
+        the per-image work -- prompt encoding, preprocess, denoise encoder, VAE encode / decode, the CFG + Euler
+        step and the blend -- unchanged: every image is bitwise the result of its own pipe() call with the same
+        prompt, noise (``latents`` [n, 4, h, w]) and posterior draw (``posterior_noise`` [n, 4, h, w]); GPU test.
+        Images with several TLC tiles are restored one call at a time."""
+        nimg = len(imgs)
+        prompts = [prompt] * nimg if isinstance(prompt, str) or prompt is None else list(prompt)
+        negs = [negative_prompt] * nimg if negative_prompt is None or isinstance(negative_prompt, str) \
+            else list(negative_prompt)
+        if len(prompts) != nimg or len(negs) != nimg:
+            raise ValueError(f"{nimg} images need {nimg} prompts / negative prompts (got {len(prompts)} / {len(negs)})")
+        posterior_noise = kwargs.pop("posterior_noise", None)
+        timer = kwargs.pop("timer", None)
+        height = height or self.default_sample_size * self.vae_scale_factor
+        width = width or self.default_sample_size * self.vae_scale_factor
+        original_size = original_size or (height, width)
+        target_size = target_size or (height, width)
+        h, w = height // 8, width // 8
+        grid = TileGrid(h, w, (target_size[0] // 8, target_size[1] // 8), overlap)
+
+        def pick(x, i):
+            return None if x is None else x[i:i + 1] if torch.is_tensor(x) else x[i]
+        if grid.ntiles != 1 or self.process_group is not None:
+            outs = []
+            for i in range(nimg):
+                o = self(lr_img=imgs[i], prompt=prompts[i], height=height, width=width,
+                         num_inference_steps=num_inference_steps, start_point=start_point, timesteps=timesteps,
+                         denoising_end=denoising_end, overlap=overlap, guidance_scale=guidance_scale,
+                         negative_prompt=negs[i], generator=generator, latents=pick(latents, i),
+                         output_type=output_type, return_dict=True, guidance_rescale=guidance_rescale,
+                         original_size=original_size, target_size=target_size, add_sample=add_sample,
+                         posterior_noise=pick(posterior_noise, i))
+                outs.extend(o.images if isinstance(o.images, list) else [o.images])
+            return FaithDiffStableDiffusionXLPipelineOutput(images=outs) if return_dict else (outs,)
+        self.check_inputs(imgs[0], prompts[0], None, height, width, None)
+        self._guidance_scale, self._guidance_rescale = guidance_scale, guidance_rescale
+        self._clip_skip, self._cross_attention_kwargs, self._denoising_end = None, None, denoising_end
+        self._interrupt = False
+        dev = self.device
+        if dev.type != "cuda":
+            raise RuntimeError("FaithDiff on MI355X: call pipe.to('cuda') (there is no CPU execution path)")
+        unet = self.unet.hip()
+        cfg = 2 if self.do_classifier_free_guidance else 1
+        # prompts: one encoder pass over every image's prompt and negative prompt (each prompt its own row group)
+        pe, npe, ppe, nppe = self.encode_prompt(prompts, do_classifier_free_guidance=True,
+                                                negative_prompt=negs if any(n is not None for n in negs) else None)
+        if cfg == 2:
+            ctx = torch.stack([npe.float(), pe.float()], 1).reshape(2 * nimg, *pe.shape[1:])
+            text = torch.stack([nppe.float(), ppe.float()], 1).reshape(2 * nimg, -1)
+        else:
+            ctx, text = pe.float(), ppe.float()
+        ts, num_inference_steps = retrieve_timesteps(self.scheduler, num_inference_steps, dev, timesteps)
+        if denoising_end is not None and isinstance(denoising_end, float) and 0 < denoising_end < 1:
+            cutoff = int(round(self.scheduler.config.num_train_timesteps
+                               - denoising_end * self.scheduler.config.num_train_timesteps))
+            num_inference_steps = len([t for t in ts if t >= cutoff])
+        sig = self.scheduler.sigmas
+        self._num_timesteps = num_inference_steps
+        kh, kw = grid.kh, grid.kw
+        rows_t = torch.tensor(grid.rows, dtype=torch.int32, device=dev)
+        cols_t = torch.tensor(grid.cols, dtype=torch.int32, device=dev)
+        cond_dt = unet.dtype
+        cond_tiles = torch.empty((nimg * cfg, kh * kw, 512), dtype=cond_dt, device=dev)
+        canvas = torch.empty((nimg, 4, h, w), dtype=torch.float32, device=dev)
+        init_sigma = float(self.scheduler.init_noise_sigma)
+        a, b = self.DDPM_scheduler.add_noise_coefficients(999)
+        if timer is not None:
+            timer("images_start", 0)
+        for i in range(nimg):  # per image, exactly as __call__: preprocess, denoise encoder, grids, start latents
+            x_img = self._preprocess(imgs[i], height, width)
+            img_lat = self.denoise_encoder.encode_nhwc(x_img, height, width)  # the graph's buffer: used right away
+            img_lat_c = torch.empty_like(img_lat, dtype=cond_dt)
+            ops.unary(img_lat, img_lat_c)
+            ops.tlc_grids_nhwc(img_lat_c, rows_t, cols_t, h, w, 512, kh, kw, 0, 1, cfg, cond_tiles[i * cfg:])
+            noise = self.prepare_latents(1, 4, height, width, torch.float32, dev, generator, pick(latents, i))
+            if start_point == "lr":
+                moments = self.vae.encode_moments_nhwc(x_img, height, width)
+                pn = pick(posterior_noise, i)
+                eps_post = (pn.to(dev, torch.float32) if pn is not None
+                            else torch.randn((1, 4, h, w), device=dev, dtype=torch.float32))
+                ops.vae_sample_add_noise(moments, eps_post.contiguous(), noise.contiguous(), canvas[i], h * w,
+                                         self.vae.config.scaling_factor, init_sigma, a, b, True)
+            else:
+                ops.vae_sample_add_noise(None, None, noise.contiguous(), canvas[i], h * w, 1.0, init_sigma, 0.0, 1.0,
+                                         False)
+        unet.set_context(ctx.to(dev), ncfg=cfg)
+        tb = max(1, min(self.tile_batch, nimg))
+        cond_emb = False
+        if unet.has_extras:  # the condition embedding of every image's tile, once per call (HipUNet.cond_embed)
+            ie = torch.empty((nimg * cfg, kh * kw, 320), dtype=cond_dt, device=dev)
+            for c0 in range(0, nimg, tb):
+                r0, r1 = c0 * cfg, min(c0 + tb, nimg) * cfg
+                unet.cond_embed(cond_tiles[r0:r1].reshape(-1, 512), r1 - r0, kh, kw, out=ie[r0:r1].reshape(-1, 320))
+            cond_tiles, cond_emb = ie, True
+        text_rows = text.to(dev).contiguous()  # [nimg*cfg, 1280]
+        tids = torch.tensor([[original_size[0], original_size[1], *grid.origin(0), target_size[0], target_size[1]]],
+                            dtype=torch.float32).repeat(tb * cfg, 1).to(dev)
+        t_rows = torch.tensor(np.repeat(ts[:num_inference_steps], tb * cfg), dtype=torch.float32,
+                              device=dev).view(-1, tb * cfg)
+        weights = torch.tensor(grid.weights(), dtype=torch.float64, device=dev)
+        xin = torch.empty((tb * cfg * kh * kw, 4), dtype=cond_dt, device=dev)
+        tiles = torch.empty((nimg, 1, 4, kh, kw), dtype=torch.float32, device=dev)
+        nxt = torch.empty_like(canvas)
+        if timer is not None:
+            timer("loop_start", 0)
+        for st in range(num_inference_steps):
+            s_, sn = float(sig[st]), float(sig[st + 1])
+            for c0 in range(0, nimg, tb):
+                n = min(tb, nimg - c0)
+                rows, per = n * cfg, cfg * kh * kw
+                for j in range(n):
+                    ops.tlc_scale_input(canvas[c0 + j], rows_t, cols_t, h, w, kh, kw, 0, 1, cfg, s_,
+                                        xin[j * per:(j + 1) * per])
+                cond = cond_tiles[c0 * cfg:(c0 + n) * cfg].reshape(rows * kh * kw, cond_tiles.shape[-1])
+                eps = unet.run(xin[:rows * kh * kw], t_rows[st, :rows], tids[:rows], text_rows[c0 * cfg:(c0 + n) * cfg],
+                               cond, rows, kh, kw, add_sample=add_sample, cond_embedded=cond_emb, kv_pair0=c0)
+                for j in range(n):
+                    ops.tlc_cfg_euler_step(eps[j * per:(j + 1) * per], canvas[c0 + j], rows_t, cols_t, h, w, kh, kw,
+                                           0, 1, cfg, guidance_scale, guidance_rescale, s_, sn, tiles[c0 + j])
+            for i in range(nimg):
+                ops.tlc_blend(tiles[i], weights, rows_t, cols_t, 4, h, w, kh, kw, nxt[i])
+            canvas, nxt = nxt, canvas
+            if timer is not None:
+                timer("step", st)
+            if callback_on_step_end is not None:
+                out = callback_on_step_end(self, st, ts[st], {"latents": canvas})
+                if out is not None and out.get("latents") is not None:
+                    canvas.copy_(out["latents"].reshape(nimg, 4, h, w))
+        if output_type == "latent":
+            images = canvas.clone()
+        else:
+            if timer is not None:
+                timer("decode_start", 0)
+            images = []
+            for i in range(nimg):
+                z = torch.empty((h * w, 4), dtype=self.vae.dtype, device=dev)
+                ops.nchw_to_nhwc(canvas[i], z, 1, 4, h * w, 1.0 / self.vae.config.scaling_factor)
+                y = self.vae.decode_nhwc(z, h, w)
+                im = self._postprocess(y, height, width, output_type)
+                images.extend(im if isinstance(im, list) else [im])
+            if timer is not None:
+                timer("decode", 0)
+        if not return_dict:
+            return (images,)
+        return FaithDiffStableDiffusionXLPipelineOutput(images=images)
 
     def _postprocess(self, y, H, W, output_type):
         """VaeImageProcessor.postprocess (:1451)."""

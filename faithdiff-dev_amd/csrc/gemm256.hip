@@ -4,16 +4,14 @@
 // Why: the 256 x 128 eight-wave kernel (gemm8.hip) is bound by the per-CU operand stream into LDS, not by the
 // MFMA pipe (scripts/diag_probe.sh: its load-only build takes 70-90 % of the full time, its compute-only build
 // ~50 %).  A 256 x 256 tile needs 32 KB of operands per 4.2 MFLOP (131 flop/B) instead of 48 KB (85 flop/B).
-// The ring holds K slots of 32 (256 + 256 rows x 64 B = 32 KB per slot), five slots = all 160 KiB of LDS, so up to
-// four slots (128 KB) are in flight while one is read -- more bytes in flight than gemm8's two 48 KB stages.
 //
-// Structure: 512 threads = 8 waves (4 x 2), each a 64 x 128 sub-tile of v_mfma_f32_16x16x32 (32 accumulators);
-// per slot one counted s_waitcnt vmcnt (the next slot has landed) + one raw s_barrier, then the next
-// slot's LDS-DMA refill and the next slot's fragment reads under this slot's 32 MFMAs (register double-buffered
-// fragments).  64-B LDS rows with a source-side XOR swizzle (16-B chunk ^ ((row >> 2) & 3)): the 16-row
-// ds_read_b128 fragments are conflict-free.  K is summed in 32-deep slots in order, the same order as gemm8's
-// two 32-deep halves per 64-deep step, so both kernels give the same bits.  Conv: im2col gather from NHWC with
-// out-of-image taps on a zero page, exact-x2 / diffusers upsample and two-source channel concat folded in.
+// Structure: 512 threads = 8 waves (4 x 2), each a 64 x 128 sub-tile of v_mfma_f32_16x16x32 (32 accumulators),
+// in two groups of four that ping-pong (group 1 one barrier behind group 0, so on every SIMD one wave computes while
+// its partner reads fragments / issues LDS-DMA).  Two 64 KB K tiles of 64 in LDS as 128-B rows with a source-side
+// XOR swizzle (16-B chunk ^ ((row >> 1) & 7)): the 16-row ds_read_b128 fragments are conflict-free.  K is summed in
+// 32-deep halves in order, the same order as gemm8's two 32-deep halves per 64-deep step, so both kernels give the
+// same bits.  Conv: im2col gather from NHWC with out-of-image taps on a zero page, exact-x2 / diffusers upsample and
+// two-source channel concat folded in.
 // Epilogue: the 256 x 256 fp32 tile in two 128-row passes through the drained ring (phase 1 accumulators -> LDS,
 // phase 2 eight columns per thread: bias / row bias / activation / residual with 16-B loads, one 16-B store).
 #include <stdlib.h>
@@ -30,30 +28,25 @@ __device__ __attribute__((aligned(256))) unsigned char g_zero_page256[256];
 
 namespace {
 
-template <int N>
-__device__ __forceinline__ void vm_wait256() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 template <typename T, typename TO, bool CONV, int NW>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, NW == 4 ? 1 : 2)))
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 2)))
 gemm256_kernel(const fd_gemm_params p, const int group_m) {
-  // NW = 8: 4 x 2 waves of 64 x 128, two waves per SIMD; NW = 4: 2 x 2 waves of 128 x 128, one wave per SIMD
-  // (a third fewer fragment bytes read from LDS per slot; 512-VGPR waves)
+  // 8 waves (4 x 2) of 64 x 128: group 0 = waves 0-3 = tile rows [0, 128), group 1 = waves 4-7 = rows [128, 256);
+  // wave w and w + 4 share a SIMD
+  static_assert(NW == 8, "ping-pong needs two groups of four waves");
   typedef typename VecT<T>::v8 V8;
   constexpr int BM = 256, BN = 256, NTHR = 64 * NW, WAVES_N = 2, WAVES_M = NW / WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N, MT = WM / 16, NT = WN / 16;
-  constexpr int AI = 16 / NW;            // 16-row DMA blocks of A (and of B) per wave per slot
-  constexpr int NSL = 5;                 // ring slots
-  constexpr int SLOT = (BM + BN) * 64;   // 32 KB: 512 rows of 32 k
-  constexpr int A_BYTES = BM * 64;
-  constexpr int PER = 2 * AI;            // LDS-DMA instructions per wave per slot (A + B, 16 rows each)
+  constexpr int NBUF = 2;                // K tiles of 64 in LDS
+  constexpr int STAGE = (BM + BN) * 128;  // 64 KB: 512 rows of 64 k (128 B)
+  constexpr int A_BYTES = BM * 128;
+  constexpr int AI = BM / (8 * NW);      // 8-row DMA pieces of A (and of B) per wave per K tile
   constexpr int LDE = BN + 4;
   constexpr int EROWS = 128;
-  static_assert(EROWS * LDE * 4 <= NSL * SLOT, "epilogue staging");
   constexpr int RED_OFF = ((EROWS * LDE * 4 + 15) / 16) * 16;  // GroupNorm statistics scratch (gn_part)
-  static_assert(RED_OFF + 16 * NTHR <= NSL * SLOT, "GroupNorm reduction scratch");
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[NSL * SLOT];
+  constexpr int SMEM = 163840;
+  static_assert(NBUF * STAGE <= SMEM && RED_OFF + 16 * NTHR <= SMEM, "LDS");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -74,48 +67,49 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
     tn = in_g / gsz;
   }
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nsl = K / 32;
+  const int nk = K / 64;
 
   const T* __restrict__ A = (const T*)p.A;
   const T* __restrict__ Bw = (const T*)p.B;
   const T* __restrict__ A2 = (const T*)p.A2;
-  // this lane's 16 B of a DMA instruction: row (lane >> 2) of a 16-row block, LDS chunk (lane & 3) holding the
-  // source chunk (lane & 3) ^ ((row >> 2) & 3) = (lane & 3) ^ (lane >> 4)
-  const int lrow = lane >> 2, chunk = (lane & 3) ^ (lane >> 4);
+  // this lane's 16 B of a DMA piece: row (lane >> 3) of an 8-row piece, LDS chunk (lane & 7) holding the source
+  // chunk (lane & 7) ^ ((row >> 1) & 7).  Piece w + 8 i starts at row 8 (w + 8 i), so the tile row's bits 0-2 are
+  // lane >> 3 and its bit 3 is w & 1, the same for all of this lane's pieces.
+  const int lrow = lane >> 3, chunk = (lane & 7) ^ (((lrow >> 1) | ((w & 1) << 2)) & 7);
 
   // A rows of this lane's DMA pieces: plain GEMM -> row pointers; conv -> the output pixel (decoded per tap)
   const T* a_row[AI];
   int a_m[AI];  // conv: output row, -1 past M
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
-    const int m = m0 + (w + NW * i) * 16 + lrow;
+    const int m = m0 + (w + NW * i) * 8 + lrow;
     const int mm = m < M ? m : M - 1;
     a_m[i] = m < M ? m : -1;
     a_row[i] = CONV ? nullptr : A + (long long)mm * p.lda + chunk * 8;
   }
   int b_off[AI];  // element offsets of this lane's B rows (32-bit: fd_gemm256_try checks N * ldb < 2^31)
 #pragma unroll
-  for (int i = 0; i < AI; ++i) b_off[i] = (n0 + (w + NW * i) * 16 + lrow) * p.ldb + chunk * 8;
+  for (int i = 0; i < AI; ++i) b_off[i] = (n0 + (w + NW * i) * 8 + lrow) * p.ldb + chunk * 8;
   const int Hl = p.upsample ? p.Hout : p.Hin, Wl = p.upsample ? p.Wout : p.Win;
   const bool up2 = p.upsample && Hl == 2 * p.Hin && Wl == 2 * p.Win;
   const int C1 = p.C1 > 0 ? p.C1 : p.Cin;
 
   constexpr int mode = FD_G256_DIAG;
-  int g_key = -1;         // conv: (tap, source) of the gather offsets below; stage() runs in slot order
+  int g_key = -1;         // conv: (tap, source) of the gather offsets below; stage() runs in K order
   constexpr int ZP = -0x7fffffff - 1;  // g_off sentinel: the zero page (a real offset can be negative: A2 - C1)
   int g_off[AI];          // per DMA row: source pixel's channel-0 element offset for this tap, ZP = zero page
 #pragma unroll
   for (int i = 0; i < AI; ++i) g_off[i] = ZP;
-  auto stage = [&](int s, int buf) {  // slot s = k [32 s, 32 s + 32)
+  auto stage = [&](int t) {  // K tile t = k [64 t, 64 t + 64) into buffer t % 2
     if (mode & 1) return;
-    const int k0 = s * 32;
-    unsigned char* sa = smem + buf * SLOT;
+    const int k0 = t * 64;
+    unsigned char* sa = smem + (t & 1) * STAGE;
     if (CONV) {
       const int tap = k0 / p.Cin;
       const int c0 = k0 - tap * p.Cin;
       const bool second = (A2 != nullptr) && (c0 >= C1);
       const int key = tap * 2 + (int)second;
-      if (key != g_key) {  // the im2col source rows change only with the tap (every Cin / 32 slots): uniform
+      if (key != g_key) {  // the im2col source rows change only with the tap (every Cin / 64 tiles): uniform
         g_key = key;
         const int ky = tap / 3, kx = tap - (tap / 3) * 3;
 #pragma unroll
@@ -160,25 +154,23 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
       __builtin_amdgcn_global_load_lds((const void*)(Bw + (b_off[i] + k0)), LDS_PTR(sb + (w + NW * i) * 1024), 16, 0,
                                        0);
   };
-  // all but this wave's youngest `ahead` slots have landed (ahead <= NSL - 1)
-  auto wait_ahead = [&](int ahead) {
-    if (ahead >= 4) vm_wait256<4 * PER>();
-    else if (ahead == 3) vm_wait256<3 * PER>();
-    else if (ahead == 2) vm_wait256<2 * PER>();
-    else if (ahead == 1) vm_wait256<PER>();
-    else vm_wait256<0>();
-  };
 
   const int fr = lane & 15, fg = lane >> 4;
-  const int rd_off = fr * 64 + ((fg ^ (fr >> 2)) << 4);  // row fr of a 16-row block, logical chunk fg
-  auto read_frags = [&](int buf, V8 (&af)[MT], V8 (&bf)[NT]) {
+  auto read_frags = [&](int t, int h, V8 (&af)[MT], V8 (&bf)[NT]) {
     if (mode & 2) return;
-    const unsigned char* sa = smem + buf * SLOT + rd_off;
+    const unsigned char* sa = smem + (t & 1) * STAGE;
     const unsigned char* sb = sa + A_BYTES;
+    const int ch = h * 4 + fg;
 #pragma unroll
-    for (int mi = 0; mi < MT; ++mi) af[mi] = *(const V8*)(sa + (wm * WM + mi * 16) * 64);
+    for (int mi = 0; mi < MT; ++mi) {
+      const int r = wm * WM + mi * 16 + fr;
+      af[mi] = *(const V8*)(sa + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+    }
 #pragma unroll
-    for (int ni = 0; ni < NT; ++ni) bf[ni] = *(const V8*)(sb + (wn * WN + ni * 16) * 64);
+    for (int ni = 0; ni < NT; ++ni) {
+      const int r = wn * WN + ni * 16 + fr;
+      bf[ni] = *(const V8*)(sb + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+    }
   };
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -193,41 +185,36 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
       for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = mfma16x16x32(af[mi], bf[ni], acc[mi][ni]);
   };
 
-  // prologue: slots 0..NSL-1 in flight, slot 0 landed and visible, its fragments read
-#pragma unroll
-  for (int s0 = 0; s0 < NSL; ++s0)
-    if (s0 < nsl) stage(s0, s0);
-  wait_ahead(min(nsl - 1, NSL - 1));
+  // ---- ping-pong main loop (probes/gemm_pp.hip, 256 x 256 BK 64: 1453 TF at 4096^3 vs 1061 for the five-slot
+  // single-group loop).  Every wave runs, per 32-deep K half, a LOAD segment (its fragment ds_reads; in the first
+  // half its share of K tile t + 1 into the buffer tile t - 1 used; in the second half the wait for tile t + 1) and
+  // a COMPUTE segment (lgkmcnt(0) + 32 MFMAs), each closed by a raw s_barrier; group 1 starts one barrier late, so
+  // on every SIMD one wave's MFMAs run beside its partner's loads.  Buffer hazards: tile t - 1's buffer is last read
+  // by group 1 in the load segment closed by the barrier that opens group 0's first load segment of tile t; tile
+  // t + 1 has landed for every wave before the barrier closing group 1's second load segment of tile t, which
+  // precedes group 0's first read of it.  K is summed in 32-deep halves in order, as before (and as gemm8): the
+  // same bits.
+  if (nk > 0) stage(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  V8 a0[MT], b0[NT], a1[MT], b1[NT];
-  read_frags(0, a0, b0);
-  // slot s (its fragments already in registers): wait for slot s+1 (this wave's DMA; slots s+2..s+4 may fly) and
-  // for this wave's reads of slot s; barrier (slot s+1 visible, every wave done reading slot s); refill slot s's
-  // buffer with slot s+NSL (four slots in flight); slot s+1's fragment reads under slot s's MFMAs.
-  auto step = [&](int s, V8 (&ac)[MT], V8 (&bc)[NT], V8 (&an)[MT], V8 (&bn)[NT]) {
-    if (s + 1 < nsl) {
-      wait_ahead(min(NSL - 2, nsl - 2 - s));
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of slot s retired
-      __builtin_amdgcn_s_barrier();
-      if (s + NSL < nsl) stage(s + NSL, s % NSL);
-      read_frags((s + 1) % NSL, an, bn);
-    } else {
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-    }
-    mma(ac, bc);
+  const int grp = w >> 2;
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
+  V8 af[MT], bfr[NT];
+  for (int t = 0; t < nk; ++t) {
 #pragma unroll
-    for (int i = 0; i < MT + NT; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    for (int h = 0; h < 2; ++h) {
+      read_frags(t, h, af, bfr);
+      if (h == 0 && t + 1 < nk) stage(t + 1);
+      if (h == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 1 landed (this wave's part)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this half's fragments
+      mma(af, bfr);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, MT * NT - (MT + NT), 0);
-  };
-  int s = 0;
-  for (; s + 1 < nsl; s += 2) {
-    step(s, a0, b0, a1, b1);
-    step(s + 1, a1, b1, a0, b0);
   }
-  if (s < nsl) step(s, a0, b0, a1, b1);
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
 
   // ---- epilogue: two 128-row passes through the drained ring
   if (mode & 4) {
@@ -390,6 +377,7 @@ extern "C" int fd_gemm256_try(fd_gemm_params* p0, void* stream) {
   if (p->conv && (p->Cin % 32 || (p->C1 > 0 && p->C1 % 32))) return 0;
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if ((long long)((m_ref + 255) / 256) * (p->N / 256) < min_tiles) return 0;
+  if (p->K % 64 || (p->conv && (p->Cin % 64 || (p->C1 > 0 && p->C1 % 64)))) return 0;  // 64-deep K tiles
   // 32-bit element offsets inside the kernel (B rows; conv source pixels)
   if ((long long)p->N * p->ldb >= (1LL << 31)) return 0;
   if (p->conv && (long long)p->nimg * p->Hin * p->Win * (p->lda > p->Cin ? p->lda : p->Cin) >= (1LL << 31)) return 0;

@@ -124,7 +124,8 @@ __global__ void __launch_bounds__(64) gn_finalize_kernel(const float2* __restric
     s += v[u].x;
     q += v[u].y;
   }
-  for (int c = j + 64 * U; c < nchunks; c += 64) {  // nchunks > 1024 (not produced by gn_rows_per_chunk)
+  for (int c = j + 64 * U; c < nchunks; c += 64) {  // nchunks > 1024: the producer-epilogue partials of images
+    // with more than 1024 256-row blocks (fd_group_norm_partials at 512^2 / 1024^2: HW / 256 up to 4096), serial
     const float2 w = p[(long long)c * groups];
     s += w.x;
     q += w.y;
@@ -202,6 +203,97 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
   (void)NV;
 }
 
+// gn_apply2: the same y = x * scale[c] + shift[c] (+ SiLU), with each thread pinned to one 8-channel chunk
+// (t % VPR, the block's first (256 / VPR) * VPR threads): its 8 scales and shifts live in registers, built straight
+// from the group statistics -- no LDS tables, no barrier, no per-vector 64-bit modulo -- and U rows' vectors are
+// in flight per thread.  Same arithmetic per element as gn_apply_kernel (bitwise equal output).
+template <typename T, int U>
+__global__ void __launch_bounds__(256) gn_apply2_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                        const float2* __restrict__ stats, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, int HW, int C, int groups,
+                                                        int rows_per_block, int silu) {
+  typedef typename VecT<T>::v8 V8;
+  const int img = blockIdx.y, t = threadIdx.x;
+  const int VPR = C / 8, RPP = 256 / VPR;  // chunks per row, rows per pass
+  if (t >= RPP * VPR) return;
+  const int v = t % VPR, r0 = t / VPR;
+  const int cpg = C / groups;
+  const int rb = blockIdx.x * rows_per_block, re = min(rb + rows_per_block, HW);
+  const T* xb = x + (long long)img * HW * C + v * 8;
+  T* yb = y + (long long)img * HW * C + v * 8;
+  // the first U rows' vectors are requested before the statistics round trip
+  V8 val[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int r = rb + r0 + u * RPP;
+    if (r < re) val[u] = *(const V8*)(xb + (long long)r * C);
+  }
+  float sc[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = v * 8 + i, g = c / cpg;
+    const float2 st = stats[img * groups + g];
+    const float a = st.y * (gamma ? gamma[c] : 1.f);
+    sc[i] = a;
+    sh[i] = (beta ? beta[c] : 0.f) - st.x * a;
+  }
+  for (int r = rb + r0; r < re; r += RPP * U) {
+    V8 nxt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rn = r + (U + u) * RPP;
+      if (rn < re) nxt[u] = *(const V8*)(xb + (long long)rn * C);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rr = r + u * RPP;
+      if (rr >= re) break;
+      V8 out;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float f = (float)val[u][i] * sc[i] + sh[i];
+        if (silu) f = silu_f(f);
+        out[i] = (T)f;
+      }
+      *(V8*)(yb + (long long)rr * C) = out;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) val[u] = nxt[u];
+  }
+}
+
+static int gn_apply_version() {
+  static const int v = env_gn("FD_GN_APPLY_V", 2);  // 1 = the LDS-table kernel (A/B)
+  return v;
+}
+
+// the apply launch shared by fd_group_norm and fd_group_norm_partials (grid: ~1024 blocks of whole rows)
+static int gn_apply_launch(const void* x, void* y, const float2* stats, const float* gamma, const float* beta, int nimg,
+                           int HW, int C, int groups, int silu, int dtype, hipStream_t s) {
+  static const int apply_blocks = env_gn("FD_GN_APPLY_BLOCKS", 1024);
+  static const int apply_u = env_gn("FD_GN_APPLY_U", 4);  // vectors in flight per thread (A/B knob: 4 or 8)
+  int rpb = 1;
+  while ((long long)nimg * ((HW + rpb - 1) / rpb) > apply_blocks) rpb *= 2;
+  const int nblk = (HW + rpb - 1) / rpb;
+  if (gn_apply_version() == 2 && C / 8 <= 256) {
+    if (apply_u == 8) {
+      FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply2_kernel<T, 8>), dim3(nblk, nimg), dim3(256), 0, s,
+                                              (const T*)x, (T*)y, stats, gamma, beta, HW, C, groups, rpb, silu));
+    } else {
+      FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply2_kernel<T, 4>), dim3(nblk, nimg), dim3(256), 0, s,
+                                              (const T*)x, (T*)y, stats, gamma, beta, HW, C, groups, rpb, silu));
+    }
+  } else if (apply_u == 8) {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1, 8>), dim3(nblk, nimg), dim3(256), 0, s,
+                                            (const T*)x, (T*)y, stats, gamma, beta, HW, C, groups, rpb, silu));
+  } else {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
+                                            (T*)y, stats, gamma, beta, HW, C, groups, rpb, silu));
+  }
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
 extern "C" long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups) {
   const int rpc = gn_rows_per_chunk(nimg, HW);
   const int nch = (HW + rpc - 1) / rpc;
@@ -219,11 +311,6 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
   hipStream_t s = (hipStream_t)stream;
   const int NV = (C / 8 > 256) ? 2 : 1;
   if (NV == 2 && (C % 16)) return FD_ERR_SHAPE;
-  // apply: ~1024 blocks in total, each a run of whole rows
-  static const int apply_blocks = env_gn("FD_GN_APPLY_BLOCKS", 1024);
-  int rpb = 1;
-  while ((long long)nimg * ((HW + rpb - 1) / rpb) > apply_blocks) rpb *= 2;
-  const int nblk = (HW + rpb - 1) / rpb;
   if (NV == 1) {
     FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_partial_kernel<T, 1>), dim3(nch, nimg), dim3(256), 0, s, (const T*)x,
                                             (float2*)ws, HW, C, groups, rpc));
@@ -236,17 +323,7 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)ws, stats, HW, C, groups,
                      nch, eps);
   FD_LAUNCH_CHECK();
-  static const int apply_u = env_gn("FD_GN_APPLY_U", 4);  // vectors in flight per thread (A/B knob: 4 or 8)
-  if (apply_u == 8) {
-    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1, 8>), dim3(nblk, nimg), dim3(256), 0, s,
-                                            (const T*)x, (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb,
-                                            silu));
-  } else {
-    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
-                                            (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb, silu));
-  }
-  FD_LAUNCH_CHECK();
-  return FD_OK;
+  return gn_apply_launch(x, y, stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s);
 }
 
 // GroupNorm whose statistics the producing GEMM / conv epilogue already wrote (fd_gemm_params.gn_part, gn_done):
@@ -263,21 +340,7 @@ extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)part, (float2*)stats, HW,
                      C, groups, HW / 256, eps);
   FD_LAUNCH_CHECK();
-  static const int apply_blocks = env_gn("FD_GN_APPLY_BLOCKS", 1024);
-  int rpb = 1;
-  while ((long long)nimg * ((HW + rpb - 1) / rpb) > apply_blocks) rpb *= 2;
-  const int nblk = (HW + rpb - 1) / rpb;
-  static const int apply_u = env_gn("FD_GN_APPLY_U", 4);  // vectors in flight per thread (A/B knob: 4 or 8)
-  if (apply_u == 8) {
-    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1, 8>), dim3(nblk, nimg), dim3(256), 0, s,
-                                            (const T*)x, (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb,
-                                            silu));
-  } else {
-    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply_kernel<T, 1>), dim3(nblk, nimg), dim3(256), 0, s, (const T*)x,
-                                            (T*)y, (const float2*)stats, gamma, beta, HW, C, groups, rpb, silu));
-  }
-  FD_LAUNCH_CHECK();
-  return FD_OK;
+  return gn_apply_launch(x, y, (const float2*)stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -188,6 +188,7 @@ class HipUNet:
         self.kv_total = off
         self.ctx = None
         self.ncfg = None
+        self.npairs = 1
         self._kv = None
         self.graphs = GraphCache()
 
@@ -199,22 +200,30 @@ class HipUNet:
         for blk in self.up:
             yield from blk["attns"]
 
-    def set_context(self, ctx):
-        """ctx: [ncfg, 77, 2048] prompt embeddings ([neg, pos] under CFG).  Projects them through all 70 attn2
-        to_k/to_v at once into ``self._kv`` [ncfg*77, sum 2C] -- once per prompt, not per forward: the
-        reference recomputes attn2's K/V of the same prompt in every UNet call of the loop (pipeline:1350, 20
-        steps x every tile); the product is identical, the GEMM (105 GFLOP, ~0.23 ms) runs once.
-        The device buffers keep their addresses across calls with the same shape (a new prompt is copied in),
+    def set_context(self, ctx, ncfg=None):
+        """ctx: [npairs * ncfg, 77, 2048] prompt embeddings ([neg, pos] under CFG; ncfg defaults to all rows, one
+        prompt pair).  Projects them through all 70 attn2 to_k/to_v at once into ``self._kv`` [rows*77, sum 2C] --
+        once per prompt, not per forward: the reference recomputes attn2's K/V of the same prompt in every UNet call
+        of the loop (pipeline:1350, 20 steps x every tile); the product is identical, the GEMM (105 GFLOP per pair,
+        ~0.23 ms) runs once.
+        One pair (npairs = 1): every CFG pair of a forward (the TLC tiles of one image) attends to it (kv_mod =
+        ncfg).  Several pairs (images batched, one tile each): CFG pair j of a forward attends to prompt pair
+        kv_pair0 + j (see forward), i.e. K/V block = row block (kv_mod = 0).
+        The device buffers keep their addresses across calls with the same shape (new prompts are copied in),
         so the hipGraphs captured by run() stay valid; a new shape drops them."""
         c = ctx.to(device=self.device, dtype=self.dtype).reshape(-1, ctx.shape[-1])
-        if self.ctx is not None and self.ctx.shape == c.shape and self.ncfg == ctx.shape[0]:
+        ncfg = ctx.shape[0] if ncfg is None else int(ncfg)
+        if ctx.shape[0] % ncfg:
+            raise ValueError(f"set_context: {ctx.shape[0]} prompt rows are not whole CFG groups of {ncfg}")
+        if self.ctx is not None and self.ctx.shape == c.shape and self.ncfg == ncfg:
             self.ctx.copy_(c)
         else:
             self.ctx = c.contiguous().clone()
             self._kv = torch.empty((c.shape[0], self.kv_total), dtype=self.dtype, device=self.device)
             self.graphs.clear()
-        self.ncfg, self.Lk = ctx.shape[0], ctx.shape[1]
-        ops.gemm(self.ctx, self.kv_w, out=self._kv)  # [ncfg*77, sum 2C]: every attn2 K/V
+        self.ncfg, self.Lk = ncfg, ctx.shape[1]
+        self.npairs = ctx.shape[0] // ncfg
+        ops.gemm(self.ctx, self.kv_w, out=self._kv)  # [rows*77, sum 2C]: every attn2 K/V
 
     # ------------------------------------------------------------------------------------------ blocks
     def _resnet(self, r, x, B, H, Wd, temb, x2=None, C1=None):
@@ -260,10 +269,10 @@ class HipUNet:
                            HW * 3 * C, HW * 3 * C, HW * 3 * C, HW * C, kv_mod=0, scale=0.125)
             lin(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
             ln_lin(b["n2"], b["q2"], out=qkv[:, :C])  # row stride 3C (the view's)
-            kv = self._kv[:, b["kv_off"]:]  # [ncfg*77, ...] view; K at +0, V at +C, row stride kv_total
+            kv = self._kv[self._kv_row0:, b["kv_off"]:]  # [ncfg*77, ...] view; K at +0, V at +C, row stride kv_total
             Lk, ldkv = self.Lk, self.kv_total
             ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, ldkv, ldkv, C,
-                           HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self.ncfg, scale=0.125)
+                           HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self._kv_mod, scale=0.125)
             lin(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
             ff = ln_lin(b["n3"], b["ff1"][0], bias=b["ff1"][1], act="geglu")
             lin(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
@@ -294,10 +303,10 @@ class HipUNet:
             ops.gemm(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h, ln_out=st)
             w, c, d = b["q2_f"]
             ops.gemm(h, w, bias=d, out=qkv[:, :C], ldc=3 * C, ln_in=st, ln_c=c)
-            kv = self._kv[:, b["kv_off"]:]
+            kv = self._kv[self._kv_row0:, b["kv_off"]:]
             Lk, ldkv = self.Lk, self.kv_total
             ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, ldkv, ldkv, C,
-                           HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self.ncfg, scale=0.125)
+                           HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self._kv_mod, scale=0.125)
             ops.gemm(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h, ln_out=st)
             w, c, d = b["ff1_f"]
             ff = ops.gemm(h, w, bias=d, act="geglu", ln_in=st, ln_c=c)
@@ -359,21 +368,31 @@ class HipUNet:
             self._side = torch.cuda.Stream(self.device)
         return self._side
 
-    def run(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True, cond_embedded=False):
+    def run(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True, cond_embedded=False, kv_pair0=0):
         """forward() through the graph cache (fdhip/graphs.py): eager on the first call of a shape, captured on
         the second, one hipGraph replay after that.  The result is the graph's static output buffer (valid
         until the next run() of the same shape).  This is what the pipeline's denoise loop and bench.py call."""
-        key = ("unet", B, H, Wd, bool(add_sample), cond is None, bool(cond_embedded), x.dtype)
+        key = ("unet", B, H, Wd, bool(add_sample), cond is None, bool(cond_embedded), x.dtype, self.npairs > 1,
+               kv_pair0)
         return self.graphs.run(key, lambda *a: self.forward(*a, B, H, Wd, add_sample=add_sample,
-                                                            cond_embedded=cond_embedded),
+                                                            cond_embedded=cond_embedded, kv_pair0=kv_pair0),
                                [x, t, time_ids, text_embeds, cond])
 
-    def forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True, cond_embedded=False):
+    def forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True, cond_embedded=False, kv_pair0=0):
         """x: NHWC [B*H*W, 4] (dtype); t: fp32 [B]; time_ids fp32 [B, 6]; text_embeds fp32 [B, 1280];
         cond: NHWC [B*H*W, 512] image latents (dtype) or None -- or, with cond_embedded=True, their
-        condition embedding from cond_embed() [B*H*W, 320].  Returns eps NHWC [B*H*W, 4] (dtype)."""
+        condition embedding from cond_embed() [B*H*W, 320].  Returns eps NHWC [B*H*W, 4] (dtype).
+        With one prompt pair in the context every CFG pair of the forward uses it; with several (images batched,
+        set_context(ctx, ncfg)), CFG pair j uses prompt pair kv_pair0 + j."""
         assert self.ctx is not None, "call set_context(prompt_embeds) first"
         assert B % self.ncfg == 0
+        if self.npairs > 1:
+            if kv_pair0 + B // self.ncfg > self.npairs:
+                raise ValueError(f"forward: pairs {kv_pair0}..{kv_pair0 + B // self.ncfg} past the "
+                                 f"{self.npairs} prompt pairs of the context")
+            self._kv_mod, self._kv_row0 = 0, kv_pair0 * self.ncfg * self.Lk
+        else:
+            self._kv_mod, self._kv_row0 = self.ncfg, 0
         with ops.tile_groups(B // self.ncfg):
             return self._forward(x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample, cond_embedded)
 

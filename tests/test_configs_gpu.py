@@ -96,3 +96,29 @@ def test_c5_back_to_back_images_bitwise_fresh_pipeline():
     # and the first image again on the fresh pipeline (its caches now hold image b): bitwise the first run
     lat_a2, img_a2, _ = _run(fresh, imgs[0], prompts[0], noise[0], post[0], S, (1024, 1024), **kw)
     assert torch.equal(lat_a, lat_a2) and (img_a == img_a2).all()
+
+
+def test_c5_images_batched_bitwise_single_calls():
+    """pipe(lr_img=[3 images], prompt=[3 prompts]) -- the images' CFG pairs share each UNet forward (B = 6 rows, each
+    pair attending to its own prompt's K/V) -- gives every image bitwise what its own pipe() call gives: the latents
+    after every step and the decoded pixels."""
+    S = 1024
+    pipe = _build(seed=3)
+    imgs = [synthetic_degraded(S, S, 31 + i) for i in range(3)]
+    prompts = ["a harbour at dusk", "a handwritten letter", "a cat on a red sofa, restored"]
+    noise = torch.cat([det_tensor((1, 4, S // 8, S // 8), 80 + i) for i in range(3)])
+    post = torch.cat([det_tensor((1, 4, S // 8, S // 8), 90 + i) for i in range(3)])
+    kw = dict(negative_prompt="", guidance_scale=5.0, start_point="lr", height=S, width=S, overlap=0.5,
+              target_size=(1024, 1024), num_inference_steps=50, denoising_end=0.08)
+    steps = []
+    out = pipe(lr_img=imgs, prompt=prompts, latents=noise, posterior_noise=post,
+               callback_on_step_end=lambda p, i, t, k: steps.append(k["latents"].detach().cpu().clone()) or {},
+               **kw).images
+    assert len(out) == 3 and len(steps) == 4 and steps[-1].shape == (3, 4, S // 8, S // 8)
+    assert pipe.unet.hip().npairs == 3
+    for i in range(3):
+        lat, img, n = _run(pipe, imgs[i], prompts[i], noise[i:i + 1], post[i:i + 1], S, (1024, 1024),
+                           num_inference_steps=50, denoising_end=0.08)
+        assert n == 4
+        assert torch.equal(steps[-1][i:i + 1], lat), f"image {i}: batched latents differ from its own call"
+        assert (np.asarray(out[i]) == img).all(), f"image {i}: batched pixels differ from its own call"
