@@ -48,6 +48,12 @@ __device__ __forceinline__ float xor_max_16_32(float x) {
 #ifndef FD_FLASH_SFMA
 #define FD_FLASH_SFMA 1
 #endif
+// QPRE: Q pre-multiplied by scale * log2(e) (rounded to the 16-bit type once per query) and every score
+// accumulator started at -m (the running max, log2 domain): the MFMA leaves exp2's argument ready, so a tile whose
+// maxima did not grow needs one v_exp_f32 per score and nothing else (experimental; costs the rounding of Q * c)
+#ifndef FD_FLASH_QPRE
+#define FD_FLASH_QPRE 0
+#endif
 #ifndef FD_FLASH_TR_EARLY
 #define FD_FLASH_TR_EARLY 1
 #endif
@@ -107,6 +113,15 @@ flash_attn_d64_kernel(
     q = q < Lq ? q : Lq - 1;
 #pragma unroll
     for (int ds = 0; ds < 2; ++ds) qf[qb][ds] = *(const V8*)(Qb + (long long)q * ldq + ds * 32 + fg * 8);
+  }
+  constexpr bool QPRE = FD_FLASH_QPRE;
+  if constexpr (QPRE) {
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qf[qb][ds][i] = (T)((float)qf[qb][ds][i] * scale_log2);
   }
 
   const int lrow = lane >> 3, slot = lane & 7;
@@ -173,7 +188,10 @@ flash_attn_d64_kernel(
     for (int j = 0; j < NQB; ++j) o[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float mrow[NQB];
 #pragma unroll
-  for (int j = 0; j < NQB; ++j) mrow[j] = -INFINITY;
+  for (int j = 0; j < NQB; ++j) mrow[j] = QPRE ? 0.f : -INFINITY;
+  f32x4 minit[NQB];  // QPRE: {-m} x 4, the score accumulators' starting value
+#pragma unroll
+  for (int j = 0; j < NQB; ++j) minit[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   // softmax denominators on the MFMA pipe: lsum[qb] += ones(16 x 32) . P^T -- every row of the 16 x 16
   // block is the running sum for query column fr, of the same bf16 P the numerator uses (32 VALU adds
   // per tile traded for 4 MFMAs)
@@ -192,7 +210,7 @@ flash_attn_d64_kernel(
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
 #pragma unroll
-      for (int qb = 0; qb < NQB; ++qb) sd[kb][qb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int qb = 0; qb < NQB; ++qb) sd[kb][qb] = QPRE ? minit[qb] : (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ds = 0; ds < 2; ++ds) {
         const V8 kf = *(const V8*)(sk + kro[ds] + kb * 2048);
@@ -261,6 +279,41 @@ flash_attn_d64_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[kb][qb][i]);
       mx = xor_max_16_32(mx);
+      if constexpr (QPRE) {
+        // scores are already s * c - m: a query whose tile max is above its running max (or the first tile)
+        // shifts by d; the others (d = 0) keep exp2(s') -- the same bits whether or not the branch runs
+        float pv[4][4];
+        const bool up = (t == 0) || (mx > 0.f);
+        if (__any(up)) {
+          const float d = (t == 0) ? mx : fmaxf(mx, 0.f);
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pv[kb][i] = __builtin_amdgcn_exp2f(sc[kb][qb][i] - d);
+          const float alpha = __builtin_amdgcn_exp2f(-d);
+          lsum[qb] *= alpha;
+#pragma unroll
+          for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
+          mrow[qb] += d;
+          minit[qb] = (f32x4){-mrow[qb], -mrow[qb], -mrow[qb], -mrow[qb]};
+        } else {
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pv[kb][i] = __builtin_amdgcn_exp2f(sc[kb][qb][i]);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          V8 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[i] = (T)pv[2 * s2][i];
+            v[4 + i] = (T)pv[2 * s2 + 1][i];
+          }
+          pf[qb][s2] = v;
+        }
+        continue;
+      }
       const float mnew = fmaxf(mrow[qb], mx * scale_log2);
       float pv[4][4];
       // raw v_exp_f32 (no denormal range fix-up: results below 2^-126 flush to 0, irrelevant to a softmax

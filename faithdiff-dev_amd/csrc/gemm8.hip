@@ -73,6 +73,10 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   // epilogue staging
   constexpr int RED_OFF = ((EPB + 15) / 16) * 16;
   constexpr bool GN_OK = !GEGLU && !LNF && BM == 256 && (NTHR % (BNO / 8)) == 0 && RED_OFF + 16 * NTHR <= SMEM;
+  // the 160-column tiles (the UNet's 10 / 20 / 40-channel groups divide 160, not 128): a thread's chunk changes
+  // from row pass to row pass (NTHR % 20 != 0), so every chunk's two group sums go to an LDS slot per staged
+  // half, then 32 threads per group fold them in a fixed order (fd_gemm_params.gn_part, same layout)
+  constexpr bool GN160 = !GEGLU && !LNF && BM == 256 && BN == 160 && RED_OFF + EROWS * (BNO / 8) * 16 <= SMEM;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   float2* const ln_tab = (float2*)(smem + LNC_OFF);
   float* const ln_cs = (float*)(smem + LNC_OFF + BM * 8);
@@ -483,9 +487,12 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   // GroupNorm statistics: this thread's chunk (tid % VPR) is the same in every row pass (NTHR % VPR == 0);
   // gsplit = its columns in the chunk's first group (the host only asks for interior, group-aligned tiles)
   const bool gn = GN_OK && p.gn_part != nullptr;
-  const int gcpg = gn ? p.N / p.gn_groups : 8;
+  const int gcpg = (gn || (GN160 && p.gn_part != nullptr)) ? p.N / p.gn_groups : 8;
   const int gsplit = (((tid % VPR) * 8) / gcpg + 1) * gcpg - (tid % VPR) * 8;
   GnTile gna;
+  const bool gn160 = GN160 && p.gn_part != nullptr;
+  f32x4* const gslot = (f32x4*)(smem + RED_OFF);
+  float g16s = 0.f, g16q = 0.f;  // this thread's group (tid / 32) sums over its rows, both halves
   // LN-fold producer (fd_gemm_params.ln_out) on the 160-column tiles: per-row (sum, sumsq) of the values as stored,
   // over the tile's 160 columns -- the partial layout of the 4-wave 64 x 160 producer (gemm.hip), which the
   // consumers read -- summed 8-column chunk by chunk in column order.  Chunk slots after the epilogue staging.
@@ -601,6 +608,22 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
         *(TO8*)(C + (long long)m * p.ldc + n) = o;
         if (gn) gna.add(o, gsplit);
+        if (GN160 && gn160) {
+          const int gs = ((cv * 8) / gcpg + 1) * gcpg - cv * 8;
+          float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float f = (float)o[i];
+            if (i < gs) {
+              s0 += f;
+              q0 += f * f;
+            } else {
+              s1 += f;
+              q1 += f * f;
+            }
+          }
+          gslot[e] = (f32x4){s0, q0, s1, q1};
+        }
         if (LNO_OK && lno) {
           float ls = 0.f, lq = 0.f;
 #pragma unroll
@@ -642,6 +665,20 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         if (LNO_OK && lno) lnslot[e] = make_float2(ls, lq);
       }
     }
+    if (GN160 && gn160) {  // this half's chunk slots: thread (g, j) folds rows j, j + 32, ... of group g
+      __syncthreads();
+      const int g = tid >> 5, j = tid & 31;
+      if (g < BNO / gcpg) {
+        const int c0 = (g * gcpg) / 8, c1 = ((g + 1) * gcpg - 1) / 8;
+        for (int r = j; r < EROWS; r += 32)
+          for (int c = c0; c <= c1; ++c) {
+            const f32x4 v4 = gslot[r * VPR + c];
+            const bool first = (c * 8) / gcpg == g;
+            g16s += first ? v4[0] : v4[2];
+            g16q += first ? v4[1] : v4[3];
+          }
+      }
+    }
     if (LNO_OK && lno) {  // this half's rows: 20 chunk slots each, summed in column order
       __syncthreads();
       const int mr = m0 + half * EROWS + tid;
@@ -659,6 +696,20 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   }
   if constexpr (GN_OK) {
     if (gn) gn_tile_write(gna, (float2*)(smem + RED_OFF), tid, NTHR, VPR, gcpg, BNO, n0o, m0, p);
+  }
+  if constexpr (GN160) {
+    if (gn160) {  // 32-lane butterfly (fixed order), lane 0 of each group writes the tile's (sum, sumsq)
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) {
+        g16s += __shfl_xor(g16s, o, 64);
+        g16q += __shfl_xor(g16q, o, 64);
+      }
+      const int g = tid >> 5;
+      if ((tid & 31) == 0 && g < BNO / gcpg) {
+        const long long blk = (long long)(m0 / p.gn_hw) * (p.gn_hw / 256) + (m0 % p.gn_hw) / 256;
+        ((float2*)p.gn_part)[blk * p.gn_groups + n0o / gcpg + g] = make_float2(g16s, g16q);
+      }
+    }
   }
 }
 
@@ -856,10 +907,15 @@ extern "C" long long fd_gemm_ws_bytes(const fd_gemm_params* p) {
 // GroupNorm output statistics (fd_gemm_params.gn_part) from the 256 x 128 instance's vector epilogue: every
 // tile interior, inside one image and a whole number of groups wide.
 static bool gn_ok8(const fd_gemm_params* p, const Plan8& pl) {
-  if (!p->gn_part || pl.bm != 256 || pl.bn != 128 || p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out) return false;
+  if (!p->gn_part || pl.bm != 256 || (pl.bn != 128 && pl.bn != 160) || p->act == FD_ACT_GEGLU || p->ln_in ||
+      p->ln_out)
+    return false;
   if (p->gn_groups <= 0 || p->gn_hw <= 0 || p->N % p->gn_groups) return false;
   const int cpg = p->N / p->gn_groups;
-  if (cpg < 4 || 128 % cpg || p->N % 128 || p->M % 256 || p->gn_hw % 256 || p->M % p->gn_hw) return false;
+  // 128-column tiles: one chunk per thread, cpg >= 4; 160-column tiles: <= 16 groups per tile (32 folding
+  // threads each), so cpg >= 10
+  if (pl.bn == 128 ? (cpg < 4 || 128 % cpg) : (cpg < 10 || 160 % cpg)) return false;
+  if (p->N % pl.bn || p->M % 256 || p->gn_hw % 256 || p->M % p->gn_hw) return false;
   const unsigned long long al = (unsigned long long)p->C | (p->residual ? (unsigned long long)p->residual : 0) |
                                 (p->bias ? (unsigned long long)p->bias : 0) | (p->rowbias ? (unsigned long long)p->rowbias : 0);
   return (al & 15) == 0 && p->ldc % 8 == 0 && (!p->residual || p->ldr % 8 == 0) &&

@@ -8,8 +8,10 @@ Dense blocks without concatenation copies: each ResidualDenseBlock_5C works in o
 ranges are x (0:64), x1 (64:96), x2 (96:128), x3 (128:160), x4 (160:192).  conv_k writes its output straight into
 its range (a strided output view) and reads the buffer's first Cin_k columns (a strided input: the conv's pixel
 stride is 192), so torch.cat((x, x1, ..)) is never formed.  The implicit GEMM needs Cin % 64 == 0, so conv2
-(96 inputs) and conv4 (160) read 128 / 192 columns with zero weights on the 32 extra ones (which hold finite
-values: x2 / x4 of this or an earlier block, or the buffer's initial zeros).  LeakyReLU(0.2), the 0.2 residual
+(96 inputs) and conv4 (160) read 128 / 192 columns with zero weights on the 32 extra ones -- their own output
+range, zeroed before the conv, so a stale value of an earlier block (an fp16 inf would make 0 * inf = NaN) is never
+read.  forward() raises FloatingPointError on a non-finite output (fp16 trunk; the reference runs fp32).
+LeakyReLU(0.2), the 0.2 residual
 scale (alpha = 0.2 with a pre-scaled bias) and the residual add are in the conv epilogue; the RRDB's own
 out * 0.2 + x is one fd_axpby.  Nearest x2 upsampling is folded into upconv1 / upconv2's gather.
 """
@@ -64,6 +66,8 @@ class HipRRDBNet:
         ld = buf.stride(0)
         for k, (wp, b, cp) in enumerate(convs[:4]):
             c0 = NF + k * GC
+            if cp > c0:  # conv2 / conv4: the padded input columns are this conv's own output range
+                buf[:, c0:cp].zero_()
             ops.conv3x3(buf[:, :cp], wp, b, 1, H, W, out=buf[:, c0:c0 + GC], act="lrelu", lda=ld)
         wp, b, cp = convs[4]
         ops.conv3x3(buf[:, :cp], wp, b, 1, H, W, out=out, residual=buf[:, :NF], alpha=0.2, lda=ld)
@@ -104,6 +108,8 @@ class HipRRDBNet:
         y = ops.conv3x3(h, wp, bb, 1, 4 * Hp, 4 * Wp)  # [16 HW, 3]
         out = torch.empty((1, 3, 4 * Hp, 4 * Wp), device=dev, dtype=torch.float32)
         ops.nhwc_to_nchw(y, out, 1, 3, 16 * HW)
+        if not bool(torch.isfinite(out).all()):
+            raise FloatingPointError("BSRNet: non-finite output (fp16 trunk overflow)")
         return out[:, :, :4 * H, :4 * W]
 
     @torch.no_grad()

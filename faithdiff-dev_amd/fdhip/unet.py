@@ -77,6 +77,9 @@ class HipUNet:
             return r
 
         self.ln_fold = os.environ.get("FD_LN_FOLD", "1") != "0" and not self.fp8_mfma
+        # GroupNorm statistics from the producing conv / GEMM epilogue (256-row tiles; FD_UNET_GN_EPI=0: off)
+        self.gn_epi = os.environ.get("FD_UNET_GN_EPI", "1") != "0"
+        self._gn_src = None
         # transformer Linear weights: e4m3 bytes for the fp8 MFMA, else the compute dtype
         LW = (lambda t: ops.pack_e4m3(t.to(self.device))) if self.fp8_mfma else \
             (lambda t: _dev(t, self.device, dtype))  # noqa: E731
@@ -233,17 +236,31 @@ class HipUNet:
             cat = torch.empty((B * HW, r["cin"]), dtype=self.dtype, device=self.device)
             ops.concat_channels(x, C1, x2, r["cin"] - C1, cat, B * HW)
             x = cat
-        h = ops.group_norm(x, *r["n1"], B, HW, r["cin"], 32, 1e-5, silu=True)
+        h = ops.group_norm(x, *r["n1"], B, HW, r["cin"], 32, 1e-5, silu=True, stats=self._gn_stats_of(x))
+        s1 = self._gn_new(B, HW)
         h = ops.conv3x3(h, r["c1"][0], r["c1"][1], B, H, Wd,
-                        rowbias=temb[:, r["toff"]:r["toff"] + r["cout"]])
-        h2 = ops.group_norm(h, *r["n2"], B, HW, r["cout"], 32, 1e-5, silu=True, out=h)
+                        rowbias=temb[:, r["toff"]:r["toff"] + r["cout"]], gn=s1)
+        h2 = ops.group_norm(h, *r["n2"], B, HW, r["cout"], 32, 1e-5, silu=True, out=h, stats=s1)
         sc = ops.gemm(x, r["sc"][0], bias=r["sc"][1]) if "sc" in r else x
-        return ops.conv3x3(h2, r["c2"][0], r["c2"][1], B, H, Wd, residual=sc)
+        s2 = self._gn_new(B, HW)
+        out = ops.conv3x3(h2, r["c2"][0], r["c2"][1], B, H, Wd, residual=sc, gn=s2)
+        self._gn_src = (out, s2) if s2 is not None else None
+        return out
+
+    def _gn_new(self, B, HW):
+        """GroupNorm statistics asked of the next conv / GEMM's epilogue (ops.GnStats; None when FD_UNET_GN_EPI=0)."""
+        return ops.GnStats(B, HW, 32, self.device) if self.gn_epi else None
+
+    def _gn_stats_of(self, x):
+        """The statistics the producer of x wrote in its epilogue (resnet conv2 / transformer proj_out), if x is
+        that output; consumed once."""
+        src, self._gn_src = self._gn_src, None
+        return src[1] if src is not None and src[0] is x else None
 
     def _t2d(self, t, x, B, H, Wd):
         C, heads, HW = t["c"], t["heads"], H * Wd
         M = B * HW
-        h = ops.group_norm(x, *t["norm"], B, HW, C, 32, 1e-6, silu=False)
+        h = ops.group_norm(x, *t["norm"], B, HW, C, 32, 1e-6, silu=False, stats=self._gn_stats_of(x))
         if self.ln_fold:
             return self._t2d_folded(t, x, h, B, H, Wd)
         lin = self._lin
@@ -276,7 +293,16 @@ class HipUNet:
             lin(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
             ff = ln_lin(b["n3"], b["ff1"][0], bias=b["ff1"][1], act="geglu")
             lin(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
-        return lin(h, t["pout"][0], bias=t["pout"][1], residual=x)
+        return self._proj_out(t, h, x, B, HW)
+
+    def _proj_out(self, t, h, x, B, HW):
+        """proj_out + residual; its epilogue also writes the next GroupNorm's statistics (16-bit GEMM)."""
+        if self.fp8_mfma:
+            return ops.linear_e4m3(h, t["pout"][0], bias=t["pout"][1], residual=x)
+        s = self._gn_new(B, HW)
+        out = ops.gemm(h, t["pout"][0], bias=t["pout"][1], residual=x, gn=s)
+        self._gn_src = (out, s) if s is not None else None
+        return out
 
     def _lin(self, x, w, bias=None, residual=None, out=None, act="none"):
         """A transformer Linear: fd_gemm (16-bit MFMA) or, for the fp8 model, fd_quant_rows_e4m3 + fd_gemm_e4m3."""
@@ -311,7 +337,7 @@ class HipUNet:
             w, c, d = b["ff1_f"]
             ff = ops.gemm(h, w, bias=d, act="geglu", ln_in=st, ln_c=c)
             ops.gemm(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h, ln_out=st if i + 1 < nb else None)
-        return ops.gemm(h, t["pout"][0], bias=t["pout"][1], residual=x)
+        return self._proj_out(t, h, x, B, HW)
 
     def _cond_embed(self, cond, B, H, Wd, out=None):
         """condition_embedding (ext:528-534, the CNE: GroupNorm -> conv 512->512 + SiLU -> conv 512->320) of the
@@ -401,6 +427,7 @@ class HipUNet:
         # on a second stream beside conv_in and the FaithDiff extras (a fork / join inside the captured graph;
         # no split-K, so the streams never share the GEMM workspace).  Opt-in (FD_SIDE_STREAM=1): measured
         # 0.39 ms/step SLOWER at C2 when it also carried the prompt K/V GEMM (now in set_context).
+        self._gn_src = None
         cur = torch.cuda.current_stream(self.device)
         side = self._side_stream()
         if side is not None:
@@ -445,5 +472,5 @@ class HipUNet:
                 th, tw = skips[-1][2], skips[-1][3]
                 h = ops.conv3x3(h, *blk["us"], B, hh, ww, upsample=True, upsample_size=(th, tw))
                 hh, ww = th, tw
-        h = ops.group_norm(h, *self.norm_out, B, hh * ww, 320, 32, 1e-5, silu=True)
+        h = ops.group_norm(h, *self.norm_out, B, hh * ww, 320, 32, 1e-5, silu=True, stats=self._gn_stats_of(h))
         return ops.conv3x3(h, *self.conv_out, B, hh, ww)

@@ -400,23 +400,46 @@ def test_flash_attn_d512(dtype, n, T):
     (1, 128, 128, 128, 256, True, True),    # gemm256 upsample conv (256^2 out), cpg 8
     (2, 128, 128, 128, 256, False, True),   # gemm256, two images
     (1, 256, 256, 128, 128, False, True),   # gemm8 256x128, cpg 4 (chunks straddle groups)
-    (2, 16, 16, 320, 320, False, False),    # cpg 10: statistics left to the GroupNorm
+    (2, 128, 128, 320, 320, False, True),   # gemm8 256x160 (the UNet's 128^2 level), cpg 10
+    (2, 64, 64, 640, 640, False, None),     # the 64^2 level, cpg 20 (256x160 when the planner takes it)
+    (2, 16, 16, 320, 320, False, None),     # small M: whichever tile the planner picks
     (1, 24, 20, 128, 128, False, False)])   # H*W % 256 != 0
 def test_conv_groupnorm_statistics_from_epilogue(nimg, H, W, Cin, Cout, up, expect):
     """A conv asked for its output's GroupNorm statistics (ops.GnStats -> fd_gemm_params.gn_part) + group_norm
-    from them (fd_group_norm_partials) == group_norm computing its own statistics, up to the summation order."""
+    from them (fd_group_norm_partials) == group_norm computing its own statistics, up to the summation order.
+    expect None: either way (the planner's tile choice), the result must match."""
     from fdhip import ops
-    x = rnd(nimg * H * W, Cin, dtype=torch.float16)
-    w = (torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)).to(torch.float16)
+    dt = torch.bfloat16 if Cout % 320 == 0 else torch.float16  # the UNet's (bf16) and the VAE's (fp16) convs
+    x = rnd(nimg * H * W, Cin, dtype=dt)
+    w = (torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)).to(dt)
     b = torch.randn(Cout, device=DEV) * 0.3
-    res = rnd(nimg * H * W * (4 if up else 1), Cout, dtype=torch.float16)
+    res = rnd(nimg * H * W * (4 if up else 1), Cout, dtype=dt)
     Ho, Wo = (2 * H, 2 * W) if up else (H, W)
     st = ops.GnStats(nimg, Ho * Wo, 32, DEV)
     y = ops.conv3x3(x, ops.pack_conv3x3(w), b, nimg, H, W, upsample=up, residual=res, gn=st)
-    assert st.done == expect
+    if expect is not None:
+        assert st.done == expect
     g, be = torch.randn(Cout, device=DEV), torch.randn(Cout, device=DEV)
     got = ops.group_norm(y, g, be, nimg, Ho * Wo, Cout, 32, 1e-6, silu=True, stats=st)
     want = ops.group_norm(y, g, be, nimg, Ho * Wo, Cout, 32, 1e-6, silu=True)
     ref = F.silu(F.group_norm(y.float().view(nimg, Ho * Wo, Cout).permute(0, 2, 1), 32, g, be, 1e-6)).permute(0, 2, 1)
     assert rel_l2(got, want) < 2e-3
     assert rel_l2(got, ref.reshape(-1, Cout)) < 6e-3
+
+
+@pytest.mark.parametrize("B,HW,C", [(2, 16384, 320), (2, 4096, 640), (4, 1024, 1280)])
+def test_gemm_groupnorm_statistics_from_epilogue(B, HW, C):
+    """The UNet's transformer proj_out (GEMM + residual) asked for its output's GroupNorm statistics: group_norm from
+    them == group_norm computing its own (summation order aside), == torch GroupNorm."""
+    from fdhip import ops
+    x, res = rnd(B * HW, C), rnd(B * HW, C)
+    w = (torch.randn(C, C, device=DEV) / math.sqrt(C)).to(torch.bfloat16)
+    b = torch.randn(C, device=DEV) * 0.3
+    st = ops.GnStats(B, HW, 32, DEV)
+    y = ops.gemm(x, w, bias=b, residual=res, gn=st)
+    g, be = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    got = ops.group_norm(y, g, be, B, HW, C, 32, 1e-6, stats=st)
+    want = ops.group_norm(y, g, be, B, HW, C, 32, 1e-6)
+    ref = F.group_norm(y.float().view(B, HW, C).permute(0, 2, 1), 32, g, be, 1e-6).permute(0, 2, 1)
+    assert rel_l2(got, want) < 2e-3
+    assert rel_l2(got, ref.reshape(-1, C)) < 6e-3
