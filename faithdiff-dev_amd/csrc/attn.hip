@@ -54,6 +54,11 @@ __device__ __forceinline__ float xor_max_16_32(float x) {
 #ifndef FD_FLASH_QPRE
 #define FD_FLASH_QPRE 0
 #endif
+// KPRE: the next tile's K fragments are read right after a mid-tile barrier, under this tile's P.V MFMAs, and
+// held in 32 VGPRs across the loop edge (the ring refill moves to that barrier as well)
+#ifndef FD_FLASH_KPRE
+#define FD_FLASH_KPRE 0
+#endif
 #ifndef FD_FLASH_TR_EARLY
 #define FD_FLASH_TR_EARLY 1
 #endif
@@ -239,12 +244,39 @@ flash_attn_d64_kernel(
       }
     }
   };
+  constexpr bool KPRE = FD_FLASH_KPRE;
+  V8 kfr[KPRE ? 4 : 1][2];  // KPRE: K fragments of the next tile
+  auto read_k = [&](auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    const unsigned char* sk = smem + BUF * 16384;
+#pragma unroll
+    for (int kb = 0; kb < (KPRE ? 4 : 1); ++kb)
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds) kfr[kb][ds] = *(const V8*)(sk + kro[ds] + kb * 2048);
+  };
+  auto qk_regs = [&](Sc& sd) {
+#pragma unroll
+    for (int kb = 0; kb < (KPRE ? 4 : 1); ++kb) {
+#pragma unroll
+      for (int qb = 0; qb < NQB; ++qb) sd[kb][qb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < 2; ++ds)
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) sd[kb][qb] = mfma16x16x32(kfr[kb][ds], qf[qb][ds], sd[kb][qb]);
+    }
+  };
   const int nfull = Lk / 64;  // tiles with no key past Lk
 #pragma unroll
-  for (int i = 0; i < NBUF - 1; ++i)
+  for (int i = 0; i < (KPRE ? NBUF : NBUF - 1); ++i)
     if (i < nt) stage(i, i);
-  wait_vm_tiles<PER, NBUF - 2>(min(NBUF - 1, nt) - 1);  // tile 0 landed
-  __builtin_amdgcn_s_barrier();
+  if constexpr (KPRE) {
+    wait_vm_tiles<PER, NBUF - 1>(min(NBUF, nt) - 1);  // tile 0 landed
+    __builtin_amdgcn_s_barrier();
+    read_k(std::integral_constant<int, 0>());
+  } else {
+    wait_vm_tiles<PER, NBUF - 2>(min(NBUF - 1, nt) - 1);  // tile 0 landed
+    __builtin_amdgcn_s_barrier();
+  }
 
   // one 64-key tile in ring buffer BUF (compile-time, so every LDS address is base + immediate);
   // MASK: the ragged last tile (keys >= Lk scored -inf)
@@ -252,9 +284,10 @@ flash_attn_d64_kernel(
     constexpr int BUF = decltype(bufc)::value;
     constexpr bool MASK = decltype(maskc)::value;
     // buffer (BUF+NBUF-1)%NBUF was last read in the previous tile, which every wave finished before the barrier
-    if (t + NBUF - 1 < nt) stage(t + NBUF - 1, (BUF + NBUF - 1) % NBUF);
+    if (!KPRE && t + NBUF - 1 < nt) stage(t + NBUF - 1, (BUF + NBUF - 1) % NBUF);
     Sc sc;
-    qk(bufc, sc);
+    if constexpr (KPRE) qk_regs(sc);
+    else qk(bufc, sc);
     s16x4 vtr[4][2][2];
     if (TR_EARLY) read_vtr(bufc, vtr);  // V^T reads in flight under the softmax VALU
     if (MASK) {
@@ -361,6 +394,18 @@ flash_attn_d64_kernel(
     if (!TR_EARLY) read_vtr(bufc, vtr);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KPRE) {
+      // every wave is done with this tile's K (read one tile ago) and V^T (just waited): refill its buffer, and
+      // read the next tile's K under the P.V MFMAs
+      if (t + 1 < nt) {
+        if (t + NBUF - 1 < nt) wait_vm<PER * (NBUF - 2)>();
+        else wait_vm_tiles<PER, NBUF - 2>(nt - 2 - t);
+        __builtin_amdgcn_s_barrier();
+        if (t + NBUF < nt) stage(t + NBUF, BUF);
+        read_k(std::integral_constant<int, (BUF + 1) % NBUF>());
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
 #pragma unroll
@@ -378,7 +423,7 @@ flash_attn_d64_kernel(
 #pragma unroll
       for (int qb = 0; qb < NQB; ++qb) lsum[qb] = mfma16x16x32(ones, pf[qb][s2], lsum[qb]);
     }
-    if (t + 1 < nt) {
+    if (!KPRE && t + 1 < nt) {
       // tile t+1 landed (tiles t+2 .. t+NBUF-1, where issued, may still fly); every wave done reading tile t
       if (t + NBUF - 1 < nt) wait_vm<PER * (NBUF - 2)>();
       else wait_vm_tiles<PER, NBUF - 2>(nt - 2 - t);
