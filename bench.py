@@ -55,7 +55,9 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_FP8_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02f_gemm_traffic.json")
+# committed rocprofv3 PMC traffic passes, newest first (scripts/r02_prof.sh + scripts/traffic_from_pmc.py)
+TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in
+                 ("r03_gemm_traffic.json", "r03_gemm_traffic_fp8.json", "r02f_gemm_traffic.json")]
 
 
 def parse(argv=None):
@@ -303,12 +305,17 @@ def family_times(fn, kinds, reps=20):
 
 
 def load_traffic(workload):
-    try:
-        with open(TRAFFIC_FILE) as f:
-            tr = json.load(f)
-    except (OSError, ValueError):
-        return None
-    return tr if tr.get("workload") == workload else None
+    """The newest committed traffic file measured on this workload (its key), or None."""
+    for path in TRAFFIC_FILES:
+        try:
+            with open(path) as f:
+                tr = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if tr.get("workload") == workload:
+            tr["file"] = os.path.basename(path)
+            return tr
+    return None
 
 
 # ------------------------------------------------------------------------------------------------ legs
@@ -429,18 +436,19 @@ def roofline_leg(loop, fp8):
     n_g, fl_g, _, ms_g = fam["gemm"]
     gemm_tf = fl_g / (ms_g / 1e3) / 1e12
     res = {}
-    tr = None if fp8 else load_traffic(f"C2 {loop.h * 8}")
+    tr = load_traffic(f"C2 {loop.h * 8}" + (" (use_fp8, e4m3 MFMA Linears)" if fp8 else ""))
+    tr16 = None if fp8 else tr  # the fp8 file's bytes are the e4m3 family's (roofline_fp8), not this one's
     res["roofline"] = {
         "bound": "mfma", "achieved": round(gemm_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
         "frac": round(gemm_tf / PEAK_BF16_TFLOPS, 4),
-        "traffic": None if tr is None else tr["hbm_bytes_per_forward"],
+        "traffic": None if tr16 is None else tr16["hbm_bytes_per_forward"],
         "kernel": "gemm8_kernel + gemm256_kernel + gemm_kernel (all MFMA GEMM + implicit-GEMM conv launches of one UNet forward)",
         "launches": n_g, "algorithmic_flops": fl_g, "kernel_ms_per_forward": round(ms_g, 3),
         "avg_launch_us": round(ms_g / n_g * 1e3, 2),
         "method": "the forward's GEMM launches captured on their own into one hipGraph, replayed 20x between HIP "
                   "events on the capture stream",
-        "traffic_note": "HBM bytes per forward of these launches (rocprofv3 PMC pass, " + os.path.basename(TRAFFIC_FILE)
-                        + ")" if tr else "no PMC pass committed for this workload"}
+        "traffic_note": "HBM bytes per forward of these launches (rocprofv3 PMC pass, " + tr16["file"] + ")"
+                        if tr16 else "no PMC pass committed for this workload"}
     if "flash_attn" in fam:
         n_a, fl_a, _, ms_a = fam["flash_attn"]
         a_tf = fl_a / (ms_a / 1e3) / 1e12
@@ -452,6 +460,10 @@ def roofline_leg(loop, fp8):
         f8_tf = fl_f / (ms_f / 1e3) / 1e12
         res["roofline_fp8"] = {"bound": "mfma", "achieved": round(f8_tf, 1), "peak": PEAK_FP8_TFLOPS,
                                "unit": "TFLOP/s", "frac": round(f8_tf / PEAK_FP8_TFLOPS, 4),
+                               "traffic": None if tr is None or not fp8 else tr["hbm_bytes_per_forward"],
+                               "traffic_note": ("HBM bytes per forward of the e4m3 launches (rocprofv3 PMC pass, "
+                                                + tr["file"] + ")") if tr is not None and fp8 else
+                               "no PMC pass committed for this workload",
                                "kernel": "gemm_e4m3_dma_kernel (transformer Linears, e4m3 x e4m3)",
                                "launches": n_f, "algorithmic_flops": fl_f, "kernel_ms_per_forward": round(ms_f, 3)}
     flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False, cond_embed=False)

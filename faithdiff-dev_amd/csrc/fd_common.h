@@ -84,7 +84,7 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// GroupNorm statistics of a 256-row GEMM / conv output tile (fd_gemm_params.gn_part): in the vector epilogue
+// GroupNorm statistics of a 256-row (or 128-row) GEMM / conv output tile (fd_gemm_params.gn_part): in the vector epilogue
 // each thread owns one 8-column chunk (NTHR % VPR == 0), whose columns fall in at most two groups (cpg >= 4 and
 // the tile's first column a multiple of cpg); sums of the STORED values, then one fixed-order reduction per group.
 struct GnTile {
@@ -106,7 +106,7 @@ struct GnTile {
 };
 // red: 2 * nthr float2 of LDS no other thread still reads; every thread of the workgroup calls this
 __device__ __forceinline__ void gn_tile_write(const GnTile& a, float2* red, int tid, int nthr, int vpr, int cpg,
-                                              int ncols, int n0, int m0, const fd_gemm_params& p) {
+                                              int ncols, int n0, int m0, const fd_gemm_params& p, int rows = 256) {
   red[2 * tid] = make_float2(a.s0, a.q0);
   red[2 * tid + 1] = make_float2(a.s1, a.q1);
   __syncthreads();
@@ -120,7 +120,7 @@ __device__ __forceinline__ void gn_tile_write(const GnTile& a, float2* red, int 
         q += v.y;
       }
     }
-    const long long blk = (long long)(m0 / p.gn_hw) * (p.gn_hw / 256) + (m0 % p.gn_hw) / 256;
+    const long long blk = (long long)(m0 / p.gn_hw) * (p.gn_hw / rows) + (m0 % p.gn_hw) / rows;
     ((float2*)p.gn_part)[blk * p.gn_groups + n0 / cpg + tid] = make_float2(s, q);
   }
 }

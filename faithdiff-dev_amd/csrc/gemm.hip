@@ -75,7 +75,10 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   // (after the ring AND the staging areas: ln_cs is written while other waves may still read the ring)
   constexpr int LNC_OFF = (NS * STAGE > LNS_OFF + LNS) ? NS * STAGE : LNS_OFF + LNS;
   constexpr int LNC = LNF ? BM * 8 + BN * 4 : 0;
-  constexpr int SMEM = LNC_OFF + LNC;
+  // GroupNorm output statistics (fd_gemm_params.gn_part, 128-row blocks) from the 128 x 128 tiles: every thread
+  // keeps one 8-column chunk in every row pass (NTHR % 16 == 0); reduction scratch after everything else
+  constexpr bool GN4 = !GEGLU && !LNF && BM == 128 && BN == 128;
+  constexpr int SMEM = LNC_OFF + LNC + (GN4 ? 16 * 256 * KS : 0);
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   float2* const ln_tab = (float2*)(smem + LNC_OFF);
   float* const ln_cs = (float*)(smem + LNC_OFF + BM * 8);
@@ -383,6 +386,10 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   typedef __attribute__((ext_vector_type(8))) TO TO8;
   const bool lno = LNP && p.ln_out != nullptr;
   float2* lnslot = (float2*)(smem + LNS_OFF);
+  const bool gn = GN4 && p.gn_part != nullptr;  // the host asks only for interior, group-aligned tiles
+  const int gcpg = gn ? N / p.gn_groups : 8;
+  const int gsplit = (((tid % VPR) * 8) / gcpg + 1) * gcpg - (tid % VPR) * 8;
+  GnTile gna;
   // vector epilogue for every tile with whole rows; a tile that runs past N (Nout % 8 == 0 under vec) skips its
   // 8-column chunks beyond N (the BSRNet dense convs: N = 32 on 64-column tiles)
   const bool full_n = n0o + BNO <= Nout;
@@ -454,6 +461,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
         *(TO8*)(C + (long long)m * p.ldc + n) = o;
+        if (GN4 && gn) gna.add(o, gsplit);
         if (lno) {  // statistics of the values as stored (what the consumer GEMM multiplies)
           float s = 0.f, q = 0.f;
 #pragma unroll
@@ -505,6 +513,9 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
       }
       ((float2*)p.ln_out)[(long long)(m0 + tid) * (N / 160) + n0 / 160] = make_float2(s, q);
     }
+  }
+  if constexpr (GN4) {
+    if (gn) gn_tile_write(gna, (float2*)(smem + LNC_OFF + LNC), tid, NTHR, VPR, gcpg, BNO, n0o, m0, p, 128);
   }
 }
 
@@ -585,16 +596,33 @@ static int dispatch_ns(const fd_gemm_params* p, hipStream_t s, int ns, int ks, i
   }
 }
 
+// GroupNorm statistics from the 128 x 128 tiles (GN4): interior, image-aligned, group-aligned tiles only
+static bool gn_ok4(const fd_gemm_params* p, int cfg) {
+  if (!p->gn_part || cfg != CFG_128x128 || p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out || p->batch > 1)
+    return false;
+  if (p->gn_groups <= 0 || p->gn_hw <= 0 || p->N % p->gn_groups) return false;
+  const int cpg = p->N / p->gn_groups;
+  if (cpg < 4 || 128 % cpg || p->N % 128 || p->M % 128 || p->gn_hw % 128 || p->M % p->gn_hw) return false;
+  const unsigned long long al = (unsigned long long)p->C | (p->residual ? (unsigned long long)p->residual : 0) |
+                                (p->bias ? (unsigned long long)p->bias : 0) | (p->rowbias ? (unsigned long long)p->rowbias : 0);
+  return (al & 15) == 0 && p->ldc % 8 == 0 && (!p->residual || p->ldr % 8 == 0) &&
+         (!p->rowbias || p->rowbias_ld % 4 == 0);
+}
+
 template <typename T, typename TO>
-static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
+static int dispatch_tiles(fd_gemm_params* p0, hipStream_t s) {
   if (g_cfg == -2) {
     g_cfg = env_int("FD_GEMM_CFG", -1);
     g_ns = env_int("FD_GEMM_NS", 0);
     g_ks = env_int("FD_GEMM_KS", 0);
     g_swz = env_int("FD_GEMM_SWZ", 1) | (env_int("FD_GEMM_MODE", 0) << 4);
   }
-  int cfg = g_cfg >= 0 && g_cfg < CFG_COUNT ? g_cfg : pick_cfg(p);
-  if (p->ln_out) cfg = CFG_64x160;  // LN-fold producer: partials per 160 columns, whatever M (batch-invariant)
+  int cfg = g_cfg >= 0 && g_cfg < CFG_COUNT ? g_cfg : pick_cfg(p0);
+  if (p0->ln_out) cfg = CFG_64x160;  // LN-fold producer: partials per 160 columns, whatever M (batch-invariant)
+  if (p0->act == FD_ACT_GEGLU && cfg == CFG_64x160) cfg = CFG_128x128;
+  fd_gemm_params q = *p0;  // the kernel's copy: gn_part kept only where the 128 x 128 tiles write the statistics
+  if (!gn_ok4(p0, cfg)) q.gn_part = nullptr;
+  const fd_gemm_params* p = &q;
   // ring depth: 4 stages (1 WG/CU) pays only on long K when one wave of tiles covers the launch; 2 stages
   // (2-3 co-resident WGs/CU) otherwise (scripts/gemm_sweep.py + in-situ traces)
   const long long tiles = (long long)(p->batch > 0 ? p->batch : 1) * ((p->M + CFG_BM[cfg] - 1) / CFG_BM[cfg]) *
@@ -604,13 +632,15 @@ static int dispatch_tiles(const fd_gemm_params* p, hipStream_t s) {
   // covers the launch (one WG per CU either way).
   const int ns = g_ns ? g_ns : ((tiles <= 256 && p->K >= 512) ? 4 : 2);
   const int ks = g_ks ? g_ks : 2;
-  if (p->act == FD_ACT_GEGLU && cfg == CFG_64x160) cfg = CFG_128x128;
+  int rc;
   switch (cfg) {
-    case CFG_128x128: return dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, ks, g_swz);
-    case CFG_64x160: return dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, ks, g_swz);
-    case CFG_128x64: return dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, ks, g_swz);
-    default: return dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, ks, g_swz);
+    case CFG_128x128: rc = dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, ks, g_swz); break;
+    case CFG_64x160: rc = dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, ks, g_swz); break;
+    case CFG_128x64: rc = dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, ks, g_swz); break;
+    default: rc = dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, ks, g_swz);
   }
+  if (rc == FD_OK && q.gn_part) p0->gn_done = 128;
+  return rc;
 }
 
 // ------------------------------------------------------------------------------------------------ M <= 4
@@ -682,7 +712,7 @@ extern "C" int fd_gemm256_try(fd_gemm_params* p, void* stream);  // gemm256.hip
 
 extern "C" int fd_gemm(fd_gemm_params* p, void* stream) {
   if (!p || !p->A || !p->B || !p->C) return FD_ERR_ARG;
-  p->gn_done = 0;  // set by the 256-row kernels when they wrote the GroupNorm statistics (gn_part)
+  p->gn_done = 0;  // rows per partial block (256 / 128) when a kernel wrote the GroupNorm statistics (gn_part)
   if (p->M <= 0 || p->N <= 0 || p->K <= 0 || (p->K % 64) != 0) return FD_ERR_SHAPE;
   if (p->act == FD_ACT_GEGLU && (p->N % 32) != 0) return FD_ERR_SHAPE;
   if (p->rowbias && p->rows_per_group <= 0) return FD_ERR_ARG;

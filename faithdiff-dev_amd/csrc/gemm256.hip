@@ -410,6 +410,6 @@ extern "C" int fd_gemm256_try(fd_gemm_params* p0, void* stream) {
       hipLaunchKernelGGL((gemm256_kernel<T, TO, false, 8>), grid, block, 0, s, *p, gm);
   }));
   FD_LAUNCH_CHECK();
-  if (rc == FD_OK) p0->gn_done = q.gn_part != nullptr;
+  if (rc == FD_OK) p0->gn_done = q.gn_part != nullptr ? 256 : 0;
   return rc == FD_OK ? 1 : rc;
 }

@@ -800,6 +800,13 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
   }
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if (!enabled || p->batch > 1 || p->K < 128) return 0;
+  // 128-channel 3x3 convs on >= 512^2 images (the VAE decoder's last up block and the encoders' first level at
+  // 1024^2: 2048+ tiles, 8+ rounds) on the 4-wave kernel's 128 x 128 tiles, two workgroups per CU (one tile's
+  // prologue / epilogue under the other's main loop): 15 % faster than gemm8 256 x 128 without GroupNorm
+  // statistics (profiles/r03_vae_tile_ab.txt), but only 3 % with them, and the decode as a whole 0.1 ms slower
+  // (profiles/r03_n128_ab.txt).  Off by default; FD_GEMM8_N128=1 routes them (A/B).
+  static const int n128 = env_i("FD_GEMM8_N128", 0);
+  if (n128 && p->conv && p->N == 128 && m_ref >= 262144) return 0;
   Plan8 q;
   if (p->ln_out) {
     // LN-fold producer: only a 160-column tile writes the partial layout the consumers read.  Long K (the ff out
@@ -807,8 +814,18 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     // 0.64x the operand bytes per CU of the 4-wave 64 x 160 producer (probe with cold weights 47.1 -> 40.6 us,
     // profiles/r02e_m2048_split.jsonl); anything else stays on that producer (return 0).
     static const int lnp = env_i("FD_GEMM8_LNP", 1);
+    static const int lnp_s = env_i("FD_GEMM8_LNP_S", 4);  // A/B knob: splits of the 256 x 160 form (lnp = 2)
     if (!lnp || p->act == FD_ACT_GEGLU || p->conv || p->N % 160 || p->K < 4096 || m_ref < 128) return 0;
     if ((long long)((m_ref + 63) / 64) * (p->N / 160) > 256) return 0;
+    if (lnp == 2 && m_ref >= 256) {  // 256 x 160 tiles (0.76x the operand bytes per CU of 128 x 160), S-way K split
+      q.bm = 256;
+      q.bn = 160;
+      q.nw = 8;
+      q.waves_m = 8;
+      q.ns = 3;
+      q.S = lnp_s;
+      goto planned;
+    }
     q.bm = 128;
     q.bn = 160;
     q.nw = 4;
@@ -951,6 +968,6 @@ extern "C" int fd_gemm8_try(fd_gemm_params* p0, void* stream) {
     FD_G8(64, 160, 4, 2, 3);
   }
 #undef FD_G8
-  if (rc == FD_OK) p0->gn_done = q.gn_part != nullptr;
+  if (rc == FD_OK) p0->gn_done = q.gn_part != nullptr ? 256 : 0;
   return rc == FD_OK ? 1 : rc;
 }

@@ -124,11 +124,21 @@ __global__ void __launch_bounds__(64) gn_finalize_kernel(const float2* __restric
     s += v[u].x;
     q += v[u].y;
   }
-  for (int c = j + 64 * U; c < nchunks; c += 64) {  // nchunks > 1024: the producer-epilogue partials of images
-    // with more than 1024 256-row blocks (fd_group_norm_partials at 512^2 / 1024^2: HW / 256 up to 4096), serial
-    const float2 w = p[(long long)c * groups];
-    s += w.x;
-    q += w.y;
+  // nchunks > 1024: the producer-epilogue partials of large images (fd_group_norm_partials at 512^2 / 1024^2:
+  // HW / 256 up to 4096, HW / 128 up to 8192) -- U more loads in flight per round, each lane still summing its
+  // chunks j, j + 64, ... in ascending order (the same bits as one load at a time)
+  for (int c0 = j + 64 * U; c0 < nchunks; c0 += 64 * U) {
+    float2 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + 64 * u;
+      w[u] = c < nchunks ? p[(long long)c * groups] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s += w[u].x;
+      q += w[u].y;
+    }
   }
   for (int o = 32; o > 0; o >>= 1) {
     s += __shfl_xor(s, o, 64);
@@ -330,15 +340,16 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
 // part[(img * HW/256 + b) * groups + g] = (sum, sumsq) of the 256-row block b.  Finalize (fp64 fold, fixed order)
 // into stats (nimg * groups float2, caller's) + apply: the gn_partial pass (one full read of x) is gone.
 extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW,
-                                      int C, int groups, float eps, int silu, const void* part, void* stats,
-                                      int dtype, void* stream) {
+                                      int C, int groups, float eps, int silu, const void* part, int part_rows,
+                                      void* stats, int dtype, void* stream) {
   if (!x || !y || !part || !stats) return FD_ERR_ARG;
-  if (nimg <= 0 || HW <= 0 || HW % 256 || C <= 0 || groups <= 0 || groups > 64 || C % groups || C % 8 ||
+  if (part_rows != 128 && part_rows != 256) return FD_ERR_ARG;
+  if (nimg <= 0 || HW <= 0 || HW % part_rows || C <= 0 || groups <= 0 || groups > 64 || C % groups || C % 8 ||
       C > GN_MAXC)
     return FD_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)part, (float2*)stats, HW,
-                     C, groups, HW / 256, eps);
+                     C, groups, HW / part_rows, eps);
   FD_LAUNCH_CHECK();
   return gn_apply_launch(x, y, (const float2*)stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s);
 }

@@ -47,8 +47,8 @@ _SIGS = {
                                  c_int, c_int, c_vp]),
     "fd_group_norm_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),
     "fd_group_norm": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_int, c_int, c_vp, c_vp]),
-    "fd_group_norm_partials": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_int, c_vp, c_vp,
-                                       c_int, c_vp]),
+    "fd_group_norm_partials": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_int, c_vp, c_int,
+                                       c_vp, c_int, c_vp]),
     "fd_gemm_e4m3": (c_int, [c_vp, c_ll, c_vp, c_vp, c_ll, c_f, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_ll,
                              c_int, c_int, c_vp]),
     "fd_layer_norm_e4m3": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp]),

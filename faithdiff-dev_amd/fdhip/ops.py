@@ -159,22 +159,25 @@ def _launch_gemm(p, what):
 
 class GnStats:
     """GroupNorm statistics asked of the GEMM / conv that produces the GroupNorm's input (fd_gemm_params.gn_part):
-    pass it as ``gn=`` to gemm / conv3x3 and as ``stats=`` to group_norm.  ``done`` is set at launch when the
-    chosen kernel wrote them (256-row tiles, group-aligned, H*W % 256 == 0); otherwise group_norm computes its own.
+    pass it as ``gn=`` to gemm / conv3x3 and as ``stats=`` to group_norm.  ``done`` / ``rows`` are set at launch
+    when the chosen kernel wrote them (256-row tiles of gemm8 / gemm256 or the 4-wave kernel's 128 x 128 tiles,
+    group-aligned, H*W a multiple of the block rows); otherwise group_norm computes its own.
     The decision depends only on shapes, so it is the same in every replay of a captured graph."""
 
     def __init__(self, nimg, HW, groups, device):
         self.nimg, self.HW, self.groups = nimg, HW, groups
-        self.part = torch.empty((max(nimg * (HW // 256) * groups * 2, 2),), dtype=torch.float32, device=device)
-        self.done = False
+        # sized for 128-row blocks (the 4-wave kernel's 128 x 128 tiles); 256-row kernels use half of it
+        self.part = torch.empty((max(nimg * (HW // 128) * groups * 2, 2),), dtype=torch.float32, device=device)
+        self.done, self.rows = False, 0
 
     def attach(self, p):
-        self.done = False
-        if self.HW % 256 == 0 and p.M == self.nimg * self.HW:
+        self.done, self.rows = False, 0
+        if self.HW % 128 == 0 and p.M == self.nimg * self.HW:
             p.gn_part, p.gn_groups, p.gn_hw = self.part.data_ptr(), self.groups, self.HW
 
     def collect(self, p):
-        self.done = bool(p.gn_part) and bool(p.gn_done)
+        self.rows = int(p.gn_done) if p.gn_part else 0  # rows per partial block (256 / 128), 0 = not written
+        self.done = self.rows > 0
 
 
 def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=1, alpha=1.0, act="none",
@@ -366,7 +369,7 @@ def group_norm(x, gamma, beta, nimg, HW, C, groups=32, eps=1e-5, silu=False, out
         st = _gn_ws(nimg * groups * 8, x.device)
         _timed("group_norm", 0, 2.0 * nimg * HW * C * x.element_size(), lambda: L.check(
             L.load().fd_group_norm_partials(L.ptr(x), L.ptr(out), L.ptr(gamma), L.ptr(beta), nimg, HW, C, groups, eps,
-                                            int(silu), L.ptr(stats.part), L.ptr(st), L.dtype_code(x.dtype),
+                                            int(silu), L.ptr(stats.part), stats.rows, L.ptr(st), L.dtype_code(x.dtype),
                                             L.stream()), "fd_group_norm_partials"))
         return out
     nb = L.load().fd_group_norm_ws_bytes(nimg, HW, C, groups)

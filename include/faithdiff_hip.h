@@ -93,11 +93,12 @@ typedef struct fd_gemm_params {
   float ln_eps;
   /* GroupNorm statistics of the output for the GroupNorm that consumes it (VAE / UNet resnets: conv2 -> next
    * norm1, conv1 -> norm2; replaces the gn_partial pass of fd_group_norm).  Request: gn_part != NULL,
-   * gn_groups = G, gn_hw = rows per image.  When the chosen kernel can produce them (256-row tiles, every tile
-   * inside one image: gn_hw % 256 == 0, its columns a whole number of groups, the vector epilogue; no GEGLU /
-   * LayerNorm fold) fd_gemm writes, per image i, 256-row block b and group g, (sum, sum of squares) of the
-   * STORED outputs to gn_part[(i * gn_hw / 256 + b) * G + g] (float2) and sets gn_done = 1, else 0 (then the
-   * consumer runs the full fd_group_norm).  Consumer: fd_group_norm_partials. */
+   * gn_groups = G, gn_hw = rows per image.  When the chosen kernel can produce them (256-row tiles of gemm8 /
+   * gemm256, or the 128 x 128 tiles of the 4-wave kernel; every tile inside one image: gn_hw % R == 0, its
+   * columns a whole number of groups, the vector epilogue; no GEGLU / LayerNorm fold) fd_gemm writes, per image i,
+   * R-row block b and group g, (sum, sum of squares) of the STORED outputs to gn_part[(i * gn_hw / R + b) * G + g]
+   * (float2) and sets gn_done = R (256 or 128), else 0 (then the consumer runs the full fd_group_norm).  Size
+   * gn_part for R = 128.  Consumer: fd_group_norm_partials(..., part_rows = gn_done, ...). */
   float* gn_part;
   int gn_groups;
   int gn_hw;
@@ -125,12 +126,13 @@ int fd_conv2d_direct(const void* x, const float* w, const float* bias, void* y, 
 long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups);
 int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
                   int groups, float eps, int silu, int dtype, void* ws, void* stream);
-/* fd_group_norm when the producing fd_gemm wrote the statistics (fd_gemm_params.gn_part with gn_done = 1):
- * part [nimg][HW / 256][groups] float2 (sum, sumsq); stats: nimg * groups float2 of caller memory.  HW % 256 == 0.
- * Saves the statistics pass over x (one full read).  Same arithmetic as fd_group_norm except the summation
- * order of the statistics. */
+/* fd_group_norm when the producing fd_gemm wrote the statistics (fd_gemm_params.gn_part, gn_done = part_rows):
+ * part [nimg][HW / part_rows][groups] float2 (sum, sumsq), part_rows 256 or 128; stats: nimg * groups float2 of
+ * caller memory.  HW % part_rows == 0.  Saves the statistics pass over x (one full read).  Same arithmetic as
+ * fd_group_norm except the summation order of the statistics. */
 int fd_group_norm_partials(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
-                           int groups, float eps, int silu, const void* part, void* stats, int dtype, void* stream);
+                           int groups, float eps, int silu, const void* part, int part_rows, void* stats, int dtype,
+                           void* stream);
 
 /* LayerNorm fused with the per-row e4m3 quantization of fd_quant_rows_e4m3 (use_fp8 model): the row is
  * normalised, rounded to dtype, then q[m][:] = e4m3_RNE(y * 448 / amax_m), scale[m] = amax_m / 448 -- bitwise

@@ -5,6 +5,7 @@ once on store, so the relative L2 error vs an fp32 reference computed from the *
 is ~2^-9 (bf16) / 2^-12 (fp16) per stored value.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -400,6 +401,7 @@ def test_flash_attn_d512(dtype, n, T):
     (1, 128, 128, 128, 256, True, True),    # gemm256 upsample conv (256^2 out), cpg 8
     (2, 128, 128, 128, 256, False, True),   # gemm256, two images
     (1, 256, 256, 128, 128, False, True),   # gemm8 256x128, cpg 4 (chunks straddle groups)
+    (1, 512, 512, 128, 128, False, True),   # 128-channel conv on a 512^2 image (4-wave 128x128 under FD_GEMM8_N128=1)
     (2, 128, 128, 320, 320, False, True),   # gemm8 256x160 (the UNet's 128^2 level), cpg 10
     (2, 64, 64, 640, 640, False, None),     # the 64^2 level, cpg 20 (256x160 when the planner takes it)
     (2, 16, 16, 320, 320, False, None),     # small M: whichever tile the planner picks
@@ -419,6 +421,9 @@ def test_conv_groupnorm_statistics_from_epilogue(nimg, H, W, Cin, Cout, up, expe
     y = ops.conv3x3(x, ops.pack_conv3x3(w), b, nimg, H, W, upsample=up, residual=res, gn=st)
     if expect is not None:
         assert st.done == expect
+    if st.done:
+        routed = os.environ.get("FD_GEMM8_N128", "0") != "0" and Cout == 128 and nimg * Ho * Wo >= 262144
+        assert st.rows == (128 if routed else 256)
     g, be = torch.randn(Cout, device=DEV), torch.randn(Cout, device=DEV)
     got = ops.group_norm(y, g, be, nimg, Ho * Wo, Cout, 32, 1e-6, silu=True, stats=st)
     want = ops.group_norm(y, g, be, nimg, Ho * Wo, Cout, 32, 1e-6, silu=True)
