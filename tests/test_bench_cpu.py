@@ -49,3 +49,17 @@ def test_workloads_parse():
     assert bench.parse([]).workload == "c2"
     a = bench.parse(["--workload", "c3", "--c3-steps", "4"])
     assert a.workload == "c3" and a.c3_steps == 4
+
+
+def test_traffic_files_are_matched_by_workload(tmp_path, monkeypatch):
+    """bench.load_traffic takes the newest committed PMC traffic file whose workload key matches (bf16 and the
+    use_fp8 leg have their own keys), and returns None when no pass covers the workload."""
+    import json
+    import bench
+    a, b = tmp_path / "new.json", tmp_path / "old.json"
+    a.write_text(json.dumps({"workload": "C2 1024 (use_fp8, e4m3 MFMA Linears)", "hbm_bytes_per_forward": 2.0}))
+    b.write_text(json.dumps({"workload": "C2 1024", "hbm_bytes_per_forward": 1.0}))
+    monkeypatch.setattr(bench, "TRAFFIC_FILES", [str(tmp_path / "missing.json"), str(a), str(b)])
+    assert bench.load_traffic("C2 1024")["hbm_bytes_per_forward"] == 1.0
+    assert bench.load_traffic("C2 1024 (use_fp8, e4m3 MFMA Linears)")["file"] == "new.json"
+    assert bench.load_traffic("C2 512") is None
