@@ -23,6 +23,20 @@
 
 __device__ __attribute__((aligned(256))) unsigned char g_zero_page8[256];
 
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+// Operand fragment of one MFMA: 8 x 16-bit (16x16x32) or, for e4m3 operands (T = uint8_t), 32 bytes (16x16x128)
+template <typename T> struct Frag8 { typedef typename VecT<T>::v8 type; };
+template <> struct Frag8<uint8_t> { typedef i32x8 type; };
+
+__device__ __forceinline__ f32x4 mfma8(bf16x8 a, bf16x8 b, f32x4 c) { return mfma16x16x32(a, b, c); }
+__device__ __forceinline__ f32x4 mfma8(f16x8 a, f16x8 b, f32x4 c) { return mfma16x16x32(a, b, c); }
+// OCP e4m3 x e4m3 on the block-scaled MFMA with unit E8M0 scales (127 = 2^0); the per-row activation scale is
+// applied in the epilogue (as gemm_fp8.hip's kernels, so both give the same bits)
+__device__ __forceinline__ f32x4 mfma8(i32x8 a, i32x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -39,11 +53,21 @@ __device__ __forceinline__ void vm_wait() {
 // above) and 64 x 160 over 4 waves (one wave per SIMD, 32 x 80 each: the M = 2048 projections' 256-tile
 // launches, where the previous 4-wave kernel split each K step over two waves and exposed the LDS-read
 // latency in front of every MFMA group).
+//
+// T = uint8_t: OCP e4m3 operands (fd_gemm_e4m3, the use_fp8 model's transformer Linears).  A 128-byte K step then
+// holds 128 elements and takes ONE v_mfma_scale_f32_16x16x128_f8f6f4 per 16x16 block (the cycles of the two
+// 16x16x32 bf16 MFMAs it replaces, twice the FLOP); the two halves of a step split the wave's column blocks
+// (half 0: ni < NH, half 1: the rest) instead of K.  a_scale[m] * alpha (= w_scale) replaces alpha per row.
 template <typename T, int BM, int BN, int NW, int WAVES_M, int NS, bool CONV, bool GEGLU, typename TO,
           bool LNF = false>
 __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, const int S, const int gm_mode,
-                                                        float* __restrict__ slabs, unsigned* __restrict__ counters) {
-  typedef typename VecT<T>::v8 V8;
+                                                        float* __restrict__ slabs, unsigned* __restrict__ counters,
+                                                        const float* __restrict__ a_scale) {
+  typedef typename Frag8<T>::type V8;
+  constexpr bool F8 = sizeof(T) == 1;
+  static_assert(!F8 || (!CONV && !LNF), "e4m3: plain GEMM only");
+  constexpr int KS = F8 ? 128 : 64;  // elements per 128-byte K step
+  constexpr int CH = 16 / (int)sizeof(T);  // elements per 16-byte chunk
   constexpr bool SCHED = FD_GEMM8_SCHED;
   constexpr int NTHR = 64 * NW;
   static_assert(NS >= 3 && NS <= 5, "ring depth");
@@ -66,7 +90,9 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   // area, in the same LDS object (a second __shared__ array makes hipcc assume ds_reads may alias the
   // LDS-DMA targets and drain vmcnt(0) in front of them)
   constexpr int LNC_OFF = (NS * STAGE > EPB) ? NS * STAGE : EPB;
-  constexpr int SMEM = LNC_OFF + (LNF ? BM * 8 + BN * 4 : 0);
+  // e4m3: the tile's per-row scales a_scale[m] * alpha (fp32) after that
+  constexpr int SC_OFF = LNC_OFF + (LNF ? BM * 8 + BN * 4 : 0);
+  constexpr int SMEM = SC_OFF + (F8 ? BM * 4 : 0);
   static_assert(SMEM <= 163840, "LDS");
   static_assert(!GEGLU || (WN % 32 == 0), "GEGLU pairs must not straddle waves");
   // GroupNorm output statistics (fd_gemm_params.gn_part): one 8-column chunk per thread, reduction scratch after the
@@ -80,6 +106,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
   float2* const ln_tab = (float2*)(smem + LNC_OFF);
   float* const ln_cs = (float*)(smem + LNC_OFF + BM * 8);
+  float* const sc_tab = (float*)(smem + SC_OFF);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -122,7 +149,9 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     }
     if (tid < BN) lncv = p.ln_c[min(n0 + tid, p.N - 1)];
   }
-  const int nk = K / 64;
+  float scv = 0.f;  // e4m3: this thread's row scale, requested ahead of the operand stages like the LN partials
+  if (F8 && tid < BM) scv = a_scale[min(m0 + tid, M - 1)] * p.alpha;
+  const int nk = K / KS;
   const int kb = (int)((long long)split * nk / S), ke = (int)((long long)(split + 1) * nk / S);
   const int nkl = ke - kb;
 
@@ -143,14 +172,14 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     const int mm = m < M ? m : M - 1;
     a_m[i] = m < M ? m : -1;
     a_chunk[i] = slot ^ ((row >> 1) & 7);
-    a_row[i] = CONV ? nullptr : A + (long long)mm * p.lda + a_chunk[i] * 8;
+    a_row[i] = CONV ? nullptr : A + (long long)mm * p.lda + a_chunk[i] * CH;
   }
   const T* b_row[B_I];
 #pragma unroll
   for (int i = 0; i < B_I; ++i) {
     const int row = (w + NW * i) * 8 + lrow;  // < BN for the loads this wave issues
     const int n = n0 + (row < BN ? row : 0);
-    b_row[i] = Bw + (long long)(n < N ? n : N - 1) * p.ldb + (slot ^ ((row >> 1) & 7)) * 8;
+    b_row[i] = Bw + (long long)(n < N ? n : N - 1) * p.ldb + (slot ^ ((row >> 1) & 7)) * CH;
   }
   const int Hl = p.upsample ? p.Hout : p.Hin, Wl = p.upsample ? p.Wout : p.Win;
   const bool up2 = p.upsample && Hl == 2 * p.Hin && Wl == 2 * p.Win;
@@ -162,7 +191,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   for (int i = 0; i < A_I; ++i) g_base[i] = nullptr;
   auto stage = [&](int kt, int buf) {  // kt: global K step
     if (mode & 1) return;
-    const int k0 = kt * 64;
+    const int k0 = kt * KS;
     unsigned char* sa = smem + buf * STAGE;
     if (CONV) {
       const int tap = k0 / p.Cin;
@@ -260,7 +289,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = mfma16x16x32(af[mi], bf[ni], acc[mi][ni]);
+      for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = mfma8(af[mi], bf[ni], acc[mi][ni]);
   };
 
   // ---- main loop: ring of 3 stages; stage s lives in buffer s % 3.  The waits the compiler must see
@@ -271,6 +300,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   for (int s0 = 0; s0 < NS; ++s0)
     if (s0 < nkl) stage(kb + s0, s0);
   wait_ahead(min(nkl - 1, NS - 1));
+  if (F8 && tid < BM) sc_tab[tid] = scv;
   if (LNF && tid < BN) ln_cs[tid] = lncv;
   if (LNF && tid < BM) {  // (mean, rstd) per row, fp64 fold in a fixed order; written once stage 0 (issued after
     // the partials) has landed, so the 17 partial registers are not live across the K loop; read after its barriers
@@ -290,9 +320,10 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     ln_tab[tid] = make_float2((float)mu, rsqrtf((float)var + p.ln_eps));
   }
   __builtin_amdgcn_s_barrier();
+  int buf = 0;
+  if constexpr (!F8) {
   V8 a0[MT], b0[NT], a1[MT], b1[NT];
   read_frags(0, 0, a0, b0);
-  int buf = 0;
   // one K step: half-1 reads under the half-0 MFMAs, barrier, refill + next half-0 reads under the half-1
   // MFMAs.  The steady-state loop has no branches inside, so sched_group_barrier can interleave one read
   // (or LDS-DMA issue) between consecutive MFMAs within each of the two regions.
@@ -342,10 +373,93 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   int kt = 0;
   for (; kt < nkl - NS; ++kt) step(true, NS - 2, kt);
   for (; kt < nkl - 1; ++kt) step(false, min(NS - 2, nkl - 2 - kt), kt);
-  constexpr bool lnf = LNF;
   read_frags(buf, 1, a1, b1);
   mma(a0, b0);
   mma(a1, b1);
+  } else {
+    // e4m3: half 0 = every A fragment + B column blocks ni < NH, half 1 = the others (A reused from a register
+    // copy, since the next stage's half-0 reads overwrite a0 under the half-1 MFMAs)
+    static_assert(NT >= 2, "column blocks per wave");
+    constexpr int NH = NT / 2, NB1 = NT - NH;
+    auto frag = [&](const unsigned char* base, int r) {  // lane: row fr, bytes 32 fg .. 32 fg + 31
+      const int sw = (r >> 1) & 7;
+      const u32x4 lo = *(const u32x4*)(base + r * 128 + (((2 * fg) ^ sw) << 4));
+      const u32x4 hi = *(const u32x4*)(base + r * 128 + (((2 * fg + 1) ^ sw) << 4));
+      return V8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    };
+    auto rd0 = [&](int b, V8 (&af)[MT], V8 (&bf)[NH]) {
+      if (mode & 2) return;
+      const unsigned char* sa = smem + b * STAGE;
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) af[mi] = frag(sa, wm * WM + mi * 16 + fr);
+#pragma unroll
+      for (int ni = 0; ni < NH; ++ni) bf[ni] = frag(sa + A_BYTES, wn * WN + ni * 16 + fr);
+    };
+    auto rd1 = [&](int b, V8 (&bf)[NB1]) {
+      if (mode & 2) return;
+      const unsigned char* sb = smem + b * STAGE + A_BYTES;
+#pragma unroll
+      for (int ni = 0; ni < NB1; ++ni) bf[ni] = frag(sb, wn * WN + (NH + ni) * 16 + fr);
+    };
+    auto mm0 = [&](const V8 (&af)[MT], const V8 (&bf)[NH]) {
+      if (mode & 2) return;
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NH; ++ni) acc[mi][ni] = mfma8(af[mi], bf[ni], acc[mi][ni]);
+    };
+    auto mm1 = [&](const V8 (&af)[MT], const V8 (&bf)[NB1]) {
+      if (mode & 2) return;
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NB1; ++ni) acc[mi][NH + ni] = mfma8(af[mi], bf[ni], acc[mi][NH + ni]);
+    };
+    V8 a0[MT], a1[MT], b0[NH], b1[NB1];
+    rd0(0, a0, b0);
+    auto step8 = [&](const bool refill, const int ahead, const int kt) {
+      rd1(buf, b1);
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) a1[mi] = a0[mi];
+      mm0(a0, b0);
+      if (SCHED) {  // the 2 * NB1 half-1 reads between the MT * NH half-0 MFMAs
+        constexpr int R1 = 2 * NB1, M0 = MT * NH, RPM = (R1 + M0 - 1) / M0;
+#pragma unroll
+        for (int i = 0; i < M0; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+          for (int j = 0; j < RPM; ++j)
+            if (i * RPM + j < R1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      wait_ahead(ahead);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+      if (refill) stage(kb + kt + NS, buf);
+      buf = buf == NS - 1 ? 0 : buf + 1;
+      rd0(buf, a0, b0);
+      mm1(a1, b1);
+      if (SCHED) {  // refill DMA + the next stage's 2 * (MT + NH) half-0 reads between the MT * NB1 MFMAs
+        constexpr int R0 = 2 * (MT + NH), M1 = MT * NB1, RPM = (R0 + M1 - 1) / M1;
+#pragma unroll
+        for (int i = 0; i < M1; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          if (refill && i < PER_LO) __builtin_amdgcn_sched_group_barrier(0x010, 1, 1);
+#pragma unroll
+          for (int j = 0; j < RPM; ++j)
+            if (i * RPM + j < R0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+        }
+      }
+    };
+    int kt = 0;
+    for (; kt < nkl - NS; ++kt) step8(true, NS - 2, kt);
+    for (; kt < nkl - 1; ++kt) step8(false, min(NS - 2, nkl - 2 - kt), kt);
+    rd1(buf, b1);
+    mm0(a0, b0);
+    mm1(a0, b1);
+  }
+  constexpr bool lnf = LNF;
 
   // ---- split-K combine: each split stores its fp32 partial slab write-through (sc1) and drains it; one
   // lane then takes a ticket on the tile's counter (agent-scope atomic).  The last arriver reads all S
@@ -506,6 +620,9 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) {
         const int rl = wm * WM + mi * 16 + fg * 4 - half * EROWS;
+        float rsc[4];  // alpha, or for e4m3 the row's a_scale * alpha
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rsc[j] = F8 ? sc_tab[rl + j + half * EROWS] : alpha;
         if (GEGLU) {
           // LN-fold operands read into registers ahead of the staging stores (same LDS object: hipcc would
           // otherwise re-read them after every store)
@@ -522,7 +639,13 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
             const int col = (wn * WN) / 2 + (ni / 2) * 16 + fr;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              float hv = acc[mi][ni][j] * alpha, g = acc[mi][ni + 1][j] * alpha;
+              float hv = acc[mi][ni][j] * rsc[j], g = acc[mi][ni + 1][j] * rsc[j];
+              if (F8) {  // explicit fma (contraction would otherwise be the compiler's choice): gemm_fp8.hip's form
+                hv = __builtin_fmaf(acc[mi][ni][j], rsc[j], gbh[ni / 2]);
+                g = __builtin_fmaf(acc[mi][ni + 1][j], rsc[j], gbg[ni / 2]);
+                ep[(rl + j) * LDE + col] = hv * gelu_f(g);
+                continue;
+              }
               if (LNF) {
                 hv = st[j & (LNF ? 3 : 0)].y * (hv - st[j & (LNF ? 3 : 0)].x * lcn[ni % (LNF ? NT : 1)]);
                 g = st[j & (LNF ? 3 : 0)].y * (g - st[j & (LNF ? 3 : 0)].x * lcn[(ni + 1) % (LNF ? NT : 1)]);
@@ -537,7 +660,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
           for (int ni = 0; ni < NT; ++ni) {
             const int col = wn * WN + ni * 16 + fr;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) ep[(rl + j) * LDE + col] = acc[mi][ni][j] * alpha;
+            for (int j = 0; j < 4; ++j) ep[(rl + j) * LDE + col] = acc[mi][ni][j] * rsc[j];
           }
         }
       }
@@ -749,30 +872,30 @@ int choose_split(int m_ref, int N, int K, int bn) {
 }
 
 template <typename T, typename TO, int BM, int BN, int NW, int WAVES_M, int NS>
-int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
+int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s, const float* a_scale = nullptr) {
   dim3 grid(pl.tiles * pl.S), block(64 * NW);
   float* slabs = (float*)((char*)p->ws + 65536 * sizeof(unsigned));
   unsigned* cnt = (unsigned*)p->ws;
   if (p->conv) {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, true, false, TO>), grid, block, 0, s, *p, pl.S,
-                       pl.group_m, slabs, cnt);
+                       pl.group_m, slabs, cnt, a_scale);
   } else if (p->act == FD_ACT_GEGLU) {
     if constexpr ((BN / (NW / WAVES_M)) % 32 == 0) {
       if (p->ln_in)
         hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, true, TO, true>), grid, block, 0, s, *p,
-                           pl.S, pl.group_m, slabs, cnt);
+                           pl.S, pl.group_m, slabs, cnt, a_scale);
       else
         hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, true, TO>), grid, block, 0, s, *p, pl.S,
-                           pl.group_m, slabs, cnt);
+                           pl.group_m, slabs, cnt, a_scale);
     } else {
       return FD_ERR_ARG;
     }
   } else if (p->ln_in) {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO, true>), grid, block, 0, s, *p, pl.S,
-                       pl.group_m, slabs, cnt);
+                       pl.group_m, slabs, cnt, a_scale);
   } else {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO>), grid, block, 0, s, *p, pl.S,
-                       pl.group_m, slabs, cnt);
+                       pl.group_m, slabs, cnt, a_scale);
   }
   FD_LAUNCH_CHECK();
   return FD_OK;
@@ -969,5 +1092,91 @@ extern "C" int fd_gemm8_try(fd_gemm_params* p0, void* stream) {
   }
 #undef FD_G8
   if (rc == FD_OK) p0->gn_done = q.gn_part != nullptr ? 256 : 0;
+  return rc == FD_OK ? 1 : rc;
+}
+
+// ------------------------------------------------------------------------------------ e4m3 (fd_gemm_e4m3)
+namespace {
+template <typename TO, int BM, int BN, int NW, int WAVES_M>
+int launch8_e4m3(const fd_gemm_params* p, const Plan8& pl, const float* a_scale, hipStream_t s) {
+  dim3 grid(pl.tiles), block(64 * NW);
+  if (p->act == FD_ACT_GEGLU) {
+    if constexpr ((BN / (NW / WAVES_M)) % 32 == 0)
+      hipLaunchKernelGGL((gemm8_kernel<uint8_t, BM, BN, NW, WAVES_M, 3, false, true, TO>), grid, block, 0, s, *p, 1,
+                         pl.group_m, nullptr, nullptr, a_scale);
+    else
+      return FD_ERR_ARG;
+  } else {
+    hipLaunchKernelGGL((gemm8_kernel<uint8_t, BM, BN, NW, WAVES_M, 3, false, false, TO>), grid, block, 0, s, *p, 1,
+                       pl.group_m, nullptr, nullptr, a_scale);
+  }
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+}  // namespace
+
+// The e4m3 GEMM of fd_gemm_e4m3 on the eight-wave kernel family (p->A / p->B e4m3 bytes, p->alpha = w_scale,
+// a_scale[M] per-row activation scales).  No split-K: every output is one accumulator over K in order, so the
+// tile shape -- chosen here from (M, N, K) -- never changes a bit (batched TLC tiles stay bitwise).  Tile choice:
+// least rounds x per-tile time on 256 CUs, the per-tile time a + b * K / 1280 us fitted per shape to the graph-timed
+// launches of profiles/r03_f8_tiles.jsonl (K = 640 .. 5120; the fixed part -- prologue, epilogue, launch ramp --
+// is 40-60 % of a K = 1280 tile); FD_F8_TILE = 256160 / 256128 / 128160 / 64160 forces one (A/B, tests).
+// Returns 1 when launched, 0 when not applicable (ragged K, batch, alignment), < 0 on error.
+extern "C" int fd_gemm8_e4m3_try(fd_gemm_params* p, const float* a_scale, void* stream) {
+  if (p->batch > 1 || p->conv || p->ln_in || p->ln_out || p->rowbias || p->K % 128) return 0;
+  if (((unsigned long long)p->A | (unsigned long long)p->B) & 15 || p->lda % 16 || p->ldb % 16) return 0;
+  const int force = env_i("FD_F8_TILE", 0);  // read per call: tests compare the shapes in one process
+  struct Cand { int bm, bn, nw, wm; double a, b; };
+  static const Cand cands[4] = {{256, 160, 8, 8, 10.6, 10.2}, {256, 128, 8, 4, 7.5, 7.9},
+                                {128, 160, 4, 2, 7.4, 6.0}, {64, 160, 4, 2, 5.65, 4.42}};
+  const bool geglu = p->act == FD_ACT_GEGLU;
+  int best = -1;
+  double bt = 1e30;
+  for (int c = 0; c < 4; ++c) {
+    const Cand& q = cands[c];
+    if (geglu && (q.bn / (q.nw / q.wm)) % 32) continue;
+    if (force && force != q.bm * 1000 + q.bn) continue;
+    const long long tiles = (long long)((p->M + q.bm - 1) / q.bm) * ((p->N + q.bn - 1) / q.bn);
+    // the 256 x 160 GEGLU tile stores 80 columns: its fixed part is relatively smaller (fit: 0.9x)
+    const double t = (double)((tiles + 255) / 256) * (q.a + q.b * p->K / 1280.0) * (geglu && c == 0 ? 0.9 : 1.0);
+    if (t < bt * 0.999) { bt = t; best = c; }
+  }
+  if (best < 0) return 0;
+  Plan8 pl;
+  pl.bm = cands[best].bm;
+  pl.bn = cands[best].bn;
+  pl.nw = cands[best].nw;
+  pl.waves_m = cands[best].wm;
+  pl.ns = 3;
+  pl.S = 1;
+  const int tiles_m = (p->M + pl.bm - 1) / pl.bm, tiles_n = (p->N + pl.bn - 1) / pl.bn;
+  pl.tiles = tiles_m * tiles_n;
+  {  // group_m as plan8
+    const long long per_xcd = ((long long)pl.tiles + 7) / 8;
+    double bestc = 1e30;
+    int gm = 1;
+    for (int g = 1; g <= tiles_m; g *= 2) {
+      const long long cols = per_xcd < g ? 1 : (per_xcd + g - 1) / g;
+      const long long rows = per_xcd < g ? per_xcd : g;
+      const double c = rows * (double)pl.bm + (cols < tiles_n ? cols : tiles_n) * (double)pl.bn;
+      if (c < bestc - 1e-9) { bestc = c; gm = g; }
+    }
+    pl.group_m = gm;
+  }
+  fd_gemm_params q = *p;
+  q.gn_part = nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  int rc = FD_ERR_DTYPE;
+#define FD_G8F(BM_, BN_, NW_, WM_) FD_DISPATCH_O(q.out_dtype, rc = (launch8_e4m3<TO, BM_, BN_, NW_, WM_>(&q, pl, a_scale, s)))
+  if (pl.bm == 256 && pl.bn == 160) {
+    FD_G8F(256, 160, 8, 8);
+  } else if (pl.bm == 256) {
+    FD_G8F(256, 128, 8, 4);
+  } else if (pl.bm == 128) {
+    FD_G8F(128, 160, 4, 2);
+  } else {
+    FD_G8F(64, 160, 4, 2);
+  }
+#undef FD_G8F
   return rc == FD_OK ? 1 : rc;
 }

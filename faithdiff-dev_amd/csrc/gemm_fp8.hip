@@ -81,10 +81,11 @@ __device__ __forceinline__ void f8_epilogue(const f32x4 (&acc)[MI][4], int m0, i
         for (int g = 0; g < 2; ++g) {
           const int nh = n0 + wn + g * 32 + (lane & 15);
           if (nh >= N) continue;
-          float hv = acc[i][2 * g][r] * s, gv = acc[i][2 * g + 1][r] * s;
-          if (bias) hv += bias[nh], gv += bias[nh + 16];
+          // explicit fma / product roundings (no compiler contraction): the eight-wave kernel's form, same bits
+          const float hv = __builtin_fmaf(acc[i][2 * g][r], s, bias ? bias[nh] : 0.f);
+          const float gv = __builtin_fmaf(acc[i][2 * g + 1][r], s, bias ? bias[nh + 16] : 0.f);
           const int o = ((n0 + wn) / 32 + g) * 16 + (lane & 15);
-          float v = hv * gelu_f(gv);
+          float v = __fmul_rn(hv, gelu_f(gv));
           if (R) v += (float)R[(long long)m * ldr + o];
           C[(long long)m * ldc + o] = (TO)v;
         }
@@ -94,7 +95,7 @@ __device__ __forceinline__ void f8_epilogue(const f32x4 (&acc)[MI][4], int m0, i
       for (int j = 0; j < 4; ++j) {
         const int n = n0 + wn + j * 16 + (lane & 15);
         if (n >= N) continue;
-        float v = acc[i][j][r] * s;
+        float v = __fmul_rn(acc[i][j][r], s);
         if (bias) v += bias[n];
         if (act != FD_ACT_NONE) v = act_f(v, act);
         if (R) v += (float)R[(long long)m * ldr + n];
@@ -223,15 +224,15 @@ __device__ __forceinline__ void f8_epilogue_vec(const f32x4 (&acc)[MI][4], float
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
           const int nh = min(n0 + wn + g * 32, N - 32) + (lane & 15);  // whole groups past N: clamped, unused
-          float hv = acc[i][2 * g][r] * s, gv = acc[i][2 * g + 1][r] * s;
-          if (bias) hv += bias[nh], gv += bias[nh + 16];
+          const float hv = __builtin_fmaf(acc[i][2 * g][r], s, bias ? bias[nh] : 0.f);
+          const float gv = __builtin_fmaf(acc[i][2 * g + 1][r], s, bias ? bias[nh + 16] : 0.f);
           ep[lr * W + (wn / 32 + g) * 16 + (lane & 15)] = hv * gelu_f(gv);
         }
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int lc = wn + j * 16 + (lane & 15);
-          float v = acc[i][j][r] * s;
+          float v = __fmul_rn(acc[i][j][r], s);
           if (bias) v += bias[min(n0 + lc, N - 1)];
           if (act != FD_ACT_NONE) v = act_f(v, act);
           ep[lr * W + lc] = v;
@@ -454,6 +455,8 @@ extern "C" int fd_quant_rows_e4m3(const void* x, long long ldx, void* q, long lo
   return FD_OK;
 }
 
+extern "C" int fd_gemm8_e4m3_try(fd_gemm_params* p, const float* a_scale, void* stream);  // gemm8.hip
+
 extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, const void* W, long long ldw,
                             float w_scale, void* C, long long ldc, int M, int N, int K, const float* bias,
                             const void* residual, long long ldr, int act, int out_dtype, void* stream) {
@@ -474,7 +477,31 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
   // K % 128 == 0: LDS-DMA ring kernel -- 64-row tiles with 3 stages (72 KB: two workgroups per CU), 128-row
   // tiles with 2 stages (64 KB; a 3-stage 96-KB ring leaves one workgroup per CU: 8192x640x640 23 -> 38 us).
   // Ragged K, or FD_F8_KERNEL=reg (A/B timing): the register-staged kernel.
-  static const char* kenv = getenv("FD_F8_KERNEL");
+  const char* kenv = getenv("FD_F8_KERNEL");  // per call (tests compare the kernels in one process)
+  // K % 128 == 0: the eight-wave kernel family (gemm8.hip, 256-row tiles) unless FD_F8_KERNEL selects one of these
+  if (!kenv) {
+    fd_gemm_params p{};
+    p.A = A;
+    p.B = W;
+    p.C = C;
+    p.lda = lda;
+    p.ldb = ldw;
+    p.ldc = ldc;
+    p.M = M;
+    p.N = N;
+    p.K = K;
+    p.batch = 1;
+    p.bias = bias;
+    p.residual = residual;
+    p.ldr = ldr;
+    p.alpha = w_scale;
+    p.act = act;
+    p.out_dtype = out_dtype;
+    p.m_ref = M;
+    const int r8 = fd_gemm8_e4m3_try(&p, a_scale, stream);
+    if (r8 < 0) return r8;
+    if (r8 == 1) return FD_OK;
+  }
   const bool dma = (K % F8_BK) == 0 && !(kenv && kenv[0] == 'r');
   // 16-B vector epilogue when every output row / residual row starts 16-B aligned (FD_F8_KERNEL=scalar: off)
   const int vec = (nout % 8) == 0 && (ldc % 8) == 0 && (((unsigned long long)C) & 15) == 0 &&

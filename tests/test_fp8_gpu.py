@@ -150,6 +150,62 @@ def test_gemm_e4m3_geglu(M, F, K):
     assert rel_l2(got, want) < 5e-5
 
 
+class _env:
+    """Temporarily set environment knobs the C ABI reads per call (FD_F8_KERNEL, FD_F8_TILE)."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        import os
+        self.old = {k: os.environ.get(k) for k in self.kw}
+        for k, v in self.kw.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
+
+    def __exit__(self, *a):
+        import os
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("tile", ["256160", "256128", "128160", "64160", None])
+@pytest.mark.parametrize("M,N,K,act,out", [(2048, 1280, 1280, "none", torch.bfloat16),
+                                           (2048, 2560, 1280, "geglu", torch.bfloat16),
+                                           (600, 480, 640, "none", torch.float32),
+                                           (333, 800, 256, "silu", torch.bfloat16),
+                                           (700, 320, 384, "geglu", torch.float32),
+                                           (8192, 640, 2560, "none", torch.bfloat16)])
+def test_gemm_e4m3_eight_wave_bitwise_vs_four_wave(tile, M, N, K, act, out):
+    """The eight-wave e4m3 kernel family (gemm8.hip, every tile shape incl. edge tiles past M / N) gives the same
+    bits as the 4-wave e4m3 kernels (FD_F8_KERNEL=dma): one fp32 accumulator per output over K in the same order
+    and the same epilogue arithmetic (row scale x w_scale, bias, activation / GEGLU, residual)."""
+    from fdhip import ops
+    if act == "geglu" and tile in ("128160", "64160"):
+        pytest.skip("GEGLU pairs need 32-column wave blocks (not the 80-column ones of these tiles)")
+    g = torch.Generator().manual_seed(M + N + K)
+    x = (torch.randn(M, K, generator=g) * 2).to(torch.bfloat16).to(DEV)
+    w = torch.randn(N, K, generator=g) * K ** -0.5
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    nout = N // 2 if act == "geglu" else N
+    res = None if out == torch.float32 else (torch.randn(M, nout, generator=g)).to(out).to(DEV)
+    q, s = ops.quant_rows_e4m3(x)
+    w8 = ops.pack_e4m3(w.to(DEV))
+    kw = dict(bias=b, residual=res, w_scale=0.75, act=act, out_dtype=out)
+    with _env(FD_F8_KERNEL="dma"):
+        want = ops.gemm_e4m3(q, s, w8, **kw)
+    with _env(FD_F8_KERNEL=None, FD_F8_TILE=tile):
+        got = ops.gemm_e4m3(q, s, w8, **kw)
+    torch.cuda.synchronize()
+    assert torch.isfinite(got.float()).all()
+    assert torch.equal(got, want)
+
+
 _FP8 = {}
 
 
