@@ -82,12 +82,16 @@ __device__ __forceinline__ void wait_vm_tiles(int n) {
   }
 }
 
-template <typename T, int NWV, int NQB, int NBUF>
+// MXO: O is written as MX e4m3 (the use_fp8 model's out-projection operand): the fp32 normalised output of each
+// (query, head) is two 32-column blocks, each spread over the 4 lanes of the query (xor 16 / 32 shuffles for its
+// amax); bytes at O + b * obs + q * ldo + h * 64, E8M0 scales at osb[b * osbs + q * ldos + 2 h + {0, 1}].
+template <typename T, int NWV, int NQB, int NBUF, bool MXO = false>
 __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(NQB == 1 ? 4 : 1, NQB == 1 ? 4 : 2)))
 flash_attn_d64_kernel(
     const T* __restrict__ Q, long long ldq, long long qbs, const T* __restrict__ K, long long ldk, long long kbs,
     const T* __restrict__ V, long long ldv, long long vbs, T* __restrict__ O, long long ldo, long long obs,
-    int Lq, int Lk, int kv_mod, int causal, float scale_log2, int heads, int swz) {
+    int Lq, int Lk, int kv_mod, int causal, float scale_log2, int heads, int swz, uint8_t* __restrict__ osb = nullptr,
+    long long ldos = 0, long long osbs = 0) {
   typedef typename VecT<T>::v8 V8;
   constexpr bool TR_EARLY = FD_FLASH_TR_EARLY;
   // NBUF-deep K/V ring: tile t+NBUF-1 is issued while tile t is consumed (counted vmcnt, raw s_barrier), so
@@ -453,6 +457,31 @@ flash_attn_d64_kernel(
   for (int qb = 0; qb < NQB; ++qb) {
     const float inv = 1.0f / lsum[qb][0];
     const int q = q0 + qb * 16 + fr;
+    if constexpr (MXO) {
+      float am[2] = {0.f, 0.f};
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) am[db >> 1] = fmaxf(am[db >> 1], fabsf(o[db][qb][j] * inv));
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        am[c] = fmaxf(am[c], __shfl_xor(am[c], 16, 64));
+        am[c] = fmaxf(am[c], __shfl_xor(am[c], 32, 64));
+      }
+      if (q >= Lq) continue;
+      const int E0 = mx_exp(am[0]), E1 = mx_exp(am[1]);
+      uint8_t* o8 = (uint8_t*)O + (long long)b * obs + (long long)q * ldo + h * 64;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+        *(unsigned*)(o8 + db * 16 + fg * 4) = mx_pack4(o[db][qb][0] * inv, o[db][qb][1] * inv, o[db][qb][2] * inv,
+                                                       o[db][qb][3] * inv, db < 2 ? E0 : E1);
+      if (fg == 0) {
+        uint8_t* sr = osb + (long long)b * osbs + (long long)q * ldos + h * 2;
+        sr[0] = (uint8_t)(E0 + 127);
+        sr[1] = (uint8_t)(E1 + 127);
+      }
+      continue;
+    }
     if (q >= Lq) continue;
     T* orow = O + (long long)b * obs + (long long)q * ldo + h * 64;
 #pragma unroll
@@ -466,10 +495,10 @@ flash_attn_d64_kernel(
   }
 }
 
-extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const void* k, long long ldk,
-                                   long long kbs, const void* v, long long ldv, long long vbs, void* o, long long ldo,
-                                   long long obs, int batch, int heads, int Lq, int Lk, int kv_mod, int causal,
-                                   float scale, int dtype, void* stream) {
+static int flash_d64(const void* q, long long ldq, long long qbs, const void* k, long long ldk, long long kbs,
+                     const void* v, long long ldv, long long vbs, void* o, long long ldo, long long obs, int batch,
+                     int heads, int Lq, int Lk, int kv_mod, int causal, float scale, int dtype, uint8_t* osb,
+                     long long ldos, long long osbs, void* stream) {
   if (!q || !k || !v || !o) return FD_ERR_ARG;
   if (batch <= 0 || heads <= 0 || Lq <= 0 || Lk <= 0 || kv_mod < 0) return FD_ERR_SHAPE;
   if ((ldq | ldk | ldv | ldo) & 7) return FD_ERR_SHAPE;
@@ -498,6 +527,12 @@ extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const 
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
 #define FD_FLASH(NW_, NQ_)                                                                                      \
+  if (osb) {                                                                                                     \
+    if (dtype != FD_BF16) return FD_ERR_DTYPE;                                                                  \
+    hipLaunchKernelGGL((flash_attn_d64_kernel<bf16, NW_, NQ_, FLASH_NBUF, true>), grid, block, 0, s, (const bf16*)q, \
+                       ldq, qbs, (const bf16*)k, ldk, kbs, (const bf16*)v, ldv, vbs, (bf16*)o, ldo, obs, Lq, Lk,   \
+                       kv_mod, causal, sl2, heads, swz, osb, ldos, osbs);                                        \
+  } else                                                                                                         \
   FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d64_kernel<T, NW_, NQ_, FLASH_NBUF>), grid, block, 0, s, (const T*)q, ldq, \
                                           qbs, (const T*)k, ldk, kbs, (const T*)v, ldv, vbs, (T*)o, ldo, obs, Lq, Lk, \
                                           kv_mod, causal, sl2, heads, swz))
@@ -515,6 +550,24 @@ extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const 
 #undef FD_FLASH
   FD_LAUNCH_CHECK();
   return FD_OK;
+}
+
+extern "C" int fd_flash_attn(const void* q, long long ldq, long long qbs, const void* k, long long ldk,
+                             long long kbs, const void* v, long long ldv, long long vbs, void* o, long long ldo,
+                             long long obs, int batch, int heads, int Lq, int Lk, int kv_mod, int causal,
+                             float scale, int dtype, void* stream) {
+  return flash_d64(q, ldq, qbs, k, ldk, kbs, v, ldv, vbs, o, ldo, obs, batch, heads, Lq, Lk, kv_mod, causal, scale,
+                   dtype, nullptr, 0, 0, stream);
+}
+
+extern "C" int fd_flash_attn_mx(const void* q, long long ldq, long long qbs, const void* k, long long ldk,
+                                long long kbs, const void* v, long long ldv, long long vbs, void* o8, long long ldo,
+                                long long obs, void* osb, long long ldos, long long osbs, int batch, int heads, int Lq,
+                                int Lk, int kv_mod, int causal, float scale, int dtype, void* stream) {
+  if (!osb) return FD_ERR_ARG;
+  if ((((unsigned long long)o8) & 3) || (ldo & 3) || (obs & 3) || ldos < 2 * heads) return FD_ERR_SHAPE;
+  return flash_d64(q, ldq, qbs, k, ldk, kbs, v, ldv, vbs, o8, ldo, obs, batch, heads, Lq, Lk, kv_mod, causal, scale,
+                   dtype, (uint8_t*)osb, ldos, osbs, stream);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -125,6 +125,23 @@ __device__ __forceinline__ void gn_tile_write(const GnTile& a, float2* red, int 
   }
 }
 
+// OCP MX e4m3 (32-element blocks, one E8M0 scale byte each): the block's scale exponent E is the least one with
+// amax <= 448 * 2^E (448 = 1.75 * 2^8, so no element saturates), q = RNE_e4m3(v * 2^-E) (the scaling is exact),
+// byte = E + 127.  All-zero (or NaN) blocks: E = 0.  Shared by every MX producer so they write the same bytes.
+__device__ __forceinline__ int mx_exp(float amax) {
+  if (!(amax > 0.f)) return 0;
+  const unsigned b = __float_as_uint(amax);
+  const int e = (int)((b >> 23) & 255u) - 127;
+  const int E = (b & 0x7fffffu) <= 0x600000u ? e - 8 : e - 7;
+  return E < -127 ? -127 : (E > 127 ? 127 : E);
+}
+// 4 floats * 2^-E -> 4 e4m3 bytes (RNE) in one dword, element 0 in the low byte
+__device__ __forceinline__ unsigned mx_pack4(float a, float b, float c, float d, int E) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_ldexpf(a, -E), __builtin_amdgcn_ldexpf(b, -E), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_ldexpf(c, -E), __builtin_amdgcn_ldexpf(d, -E), w, true);
+  return (unsigned)w;
+}
+
 #define FD_LAUNCH_CHECK()                                  \
   do {                                                     \
     if (hipGetLastError() != hipSuccess) return FD_ERR_HIP; \

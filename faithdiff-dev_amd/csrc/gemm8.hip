@@ -26,8 +26,21 @@ __device__ __attribute__((aligned(256))) unsigned char g_zero_page8[256];
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 
 // Operand fragment of one MFMA: 8 x 16-bit (16x16x32) or, for e4m3 operands (T = uint8_t), 32 bytes (16x16x128)
+// e4m3 operand tags: uint8_t = per-row scaled (fd_gemm_e4m3), mx8_t = OCP MX block-scaled (fd_gemm_mxe4m3)
+struct mx8_t {
+  uint8_t v;
+};
 template <typename T> struct Frag8 { typedef typename VecT<T>::v8 type; };
 template <> struct Frag8<uint8_t> { typedef i32x8 type; };
+template <> struct Frag8<mx8_t> { typedef i32x8 type; };
+// e4m3 side arguments: per-row A scales (uint8_t operands), A block scales (mx8_t), output block scales (TO = uint8_t)
+struct f8_args {
+  const float* a_scale;
+  const uint8_t* a_bs;
+  long long a_bs_ld;
+  uint8_t* o_bs;
+  long long o_bs_ld;
+};
 
 __device__ __forceinline__ f32x4 mfma8(bf16x8 a, bf16x8 b, f32x4 c) { return mfma16x16x32(a, b, c); }
 __device__ __forceinline__ f32x4 mfma8(f16x8 a, f16x8 b, f32x4 c) { return mfma16x16x32(a, b, c); }
@@ -35,6 +48,10 @@ __device__ __forceinline__ f32x4 mfma8(f16x8 a, f16x8 b, f32x4 c) { return mfma1
 // applied in the epilogue (as gemm_fp8.hip's kernels, so both give the same bits)
 __device__ __forceinline__ f32x4 mfma8(i32x8 a, i32x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+// MX A operand: this lane's E8M0 byte (its row, its 32-element block) as the A scale; W unscaled (127)
+__device__ __forceinline__ f32x4 mfma8s(i32x8 a, i32x8 b, f32x4 c, int sa) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, sa, 0, 127);
 }
 
 template <int N>
@@ -58,13 +75,19 @@ __device__ __forceinline__ void vm_wait() {
 // holds 128 elements and takes ONE v_mfma_scale_f32_16x16x128_f8f6f4 per 16x16 block (the cycles of the two
 // 16x16x32 bf16 MFMAs it replaces, twice the FLOP); the two halves of a step split the wave's column blocks
 // (half 0: ni < NH, half 1: the rest) instead of K.  a_scale[m] * alpha (= w_scale) replaces alpha per row.
+// T = mx8_t: A carries E8M0 block scales ([M][K / 32] bytes): each stage also DMAs the tile's BM x 4 scale bytes
+// (one dword per row) into LDS, and every MFMA takes its lane's byte as the A scale.  TO = uint8_t: the output is
+// written as MX e4m3 (+ block scales f8.o_bs), each 32-column block's amax reduced over its 4 epilogue threads.
 template <typename T, int BM, int BN, int NW, int WAVES_M, int NS, bool CONV, bool GEGLU, typename TO,
           bool LNF = false>
 __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, const int S, const int gm_mode,
                                                         float* __restrict__ slabs, unsigned* __restrict__ counters,
-                                                        const float* __restrict__ a_scale) {
+                                                        const f8_args f8) {
   typedef typename Frag8<T>::type V8;
   constexpr bool F8 = sizeof(T) == 1;
+  constexpr bool MXI = __is_same(T, mx8_t);
+  constexpr bool MXO = __is_same(TO, uint8_t);
+  static_assert(!MXO || (F8 && !LNF && !CONV), "MX output from the e4m3 kernels only");
   static_assert(!F8 || (!CONV && !LNF), "e4m3: plain GEMM only");
   constexpr int KS = F8 ? 128 : 64;  // elements per 128-byte K step
   constexpr int CH = 16 / (int)sizeof(T);  // elements per 16-byte chunk
@@ -80,7 +103,12 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   constexpr int B_I = (B_TOT + NW - 1) / NW;  // ... at most this many per wave
   constexpr int B_LO = B_TOT / NW;         // waves >= B_TOT % NW issue only this many
   static_assert(A_I * 8 * NW == BM, "A rows per stage");
-  constexpr int PER_HI = A_I + B_I, PER_LO = A_I + B_LO;
+  // MX: every wave DMAs one dword (the 4 block scales of a K step) for each of 64 consecutive rows starting at its
+  // RPW-row slice, all lanes active (an exec-masked LDS-DMA makes hipcc branch around it inside the main loop); the
+  // slices of neighbouring waves overlap and write identical bytes.  Region per stage: (NW - 1) * RPW + 64 rows.
+  constexpr int RPW = BM / NW;
+  constexpr int SCR = ((NW - 1) * RPW + 64) * 4;
+  constexpr int PER_HI = A_I + B_I + (MXI ? 1 : 0), PER_LO = A_I + B_LO + (MXI ? 1 : 0);
   constexpr int BNO = GEGLU ? BN / 2 : BN;
   constexpr int LDE = BNO + 4;
   // epilogue staged fp32 [EROWS][BNO+4] in the ring's LDS: the whole tile when it fits, else 128-row halves
@@ -92,7 +120,9 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   constexpr int LNC_OFF = (NS * STAGE > EPB) ? NS * STAGE : EPB;
   // e4m3: the tile's per-row scales a_scale[m] * alpha (fp32) after that
   constexpr int SC_OFF = LNC_OFF + (LNF ? BM * 8 + BN * 4 : 0);
-  constexpr int SMEM = SC_OFF + (F8 ? BM * 4 : 0);
+  constexpr int SCL_OFF = SC_OFF + (F8 && !MXI ? BM * 4 : 0);
+  // MX: the ring's block-scale dwords (NS stages x BM rows) after that
+  constexpr int SMEM = SCL_OFF + (MXI ? NS * SCR : 0);
   static_assert(SMEM <= 163840, "LDS");
   static_assert(!GEGLU || (WN % 32 == 0), "GEGLU pairs must not straddle waves");
   // GroupNorm output statistics (fd_gemm_params.gn_part): one 8-column chunk per thread, reduction scratch after the
@@ -150,7 +180,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     if (tid < BN) lncv = p.ln_c[min(n0 + tid, p.N - 1)];
   }
   float scv = 0.f;  // e4m3: this thread's row scale, requested ahead of the operand stages like the LN partials
-  if (F8 && tid < BM) scv = a_scale[min(m0 + tid, M - 1)] * p.alpha;
+  if (F8 && !MXI && tid < BM) scv = f8.a_scale[min(m0 + tid, M - 1)] * p.alpha;
   const int nk = K / KS;
   const int kb = (int)((long long)split * nk / S), ke = (int)((long long)(split + 1) * nk / S);
   const int nkl = ke - kb;
@@ -181,6 +211,8 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     const int n = n0 + (row < BN ? row : 0);
     b_row[i] = Bw + (long long)(n < N ? n : N - 1) * p.ldb + (slot ^ ((row >> 1) & 7)) * CH;
   }
+  const uint8_t* s_src = nullptr;  // MX: this lane's row of A block scales (row w * RPW + lane, clamped)
+  if (MXI) s_src = f8.a_bs + (long long)min(m0 + w * RPW + lane, M - 1) * f8.a_bs_ld;
   const int Hl = p.upsample ? p.Hout : p.Hin, Wl = p.upsample ? p.Wout : p.Win;
   const bool up2 = p.upsample && Hl == 2 * p.Hin && Wl == 2 * p.Win;
   const int C1 = p.C1 > 0 ? p.C1 : p.Cin;
@@ -243,6 +275,9 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     for (int i = 0; i < B_I; ++i)
       if (i < B_LO || hi)
         __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (w + NW * i) * 1024), 16, 0, 0);
+    if constexpr (MXI)  // the 4 block scales of this K step (128 elements = 4 blocks) of rows w * RPW .. + 63
+      __builtin_amdgcn_global_load_lds((const void*)(s_src + kt * 4), LDS_PTR(smem + SCL_OFF + buf * SCR + w * RPW * 4),
+                                       4, 0, 0);
   };
   // all but the youngest `ahead` stages of this wave's loads have landed
   auto wait_ahead = [&](int ahead) {  // ahead <= NS - 1 (the prologue); NS - 2 in the steady loop
@@ -300,7 +335,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   for (int s0 = 0; s0 < NS; ++s0)
     if (s0 < nkl) stage(kb + s0, s0);
   wait_ahead(min(nkl - 1, NS - 1));
-  if (F8 && tid < BM) sc_tab[tid] = scv;
+  if (F8 && !MXI && tid < BM) sc_tab[tid] = scv;
   if (LNF && tid < BN) ln_cs[tid] = lncv;
   if (LNF && tid < BM) {  // (mean, rstd) per row, fp64 fold in a fixed order; written once stage 0 (issued after
     // the partials) has landed, so the 17 partial registers are not live across the K loop; read after its barriers
@@ -381,17 +416,27 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     // copy, since the next stage's half-0 reads overwrite a0 under the half-1 MFMAs)
     static_assert(NT >= 2, "column blocks per wave");
     constexpr int NH = NT / 2, NB1 = NT - NH;
-    auto frag = [&](const unsigned char* base, int r) {  // lane: row fr, bytes 32 fg .. 32 fg + 31
+    // The 8-bit 16x16x128 operand's K order (measured, probes/mx_diag2.py): a lane's 32 bytes are two 16-byte
+    // halves at hardware k = 16 fg .. and 64 + 16 fg .., and the A scale of hardware block kb (k 32 kb ..) is taken
+    // from lane row + 16 kb.  Per-row scaling only needs A and B to agree (chunks 2 fg, 2 fg + 1 of the 128-B
+    // row); MX needs memory block kb = hardware block kb, so the lane reads chunks fg and 4 + fg.
+    constexpr int C0 = MXI ? 1 : 2, C1 = MXI ? 4 : 1;
+    auto frag = [&](const unsigned char* base, int r) {  // lane: row fr, 32 bytes of the 128-B K step
       const int sw = (r >> 1) & 7;
-      const u32x4 lo = *(const u32x4*)(base + r * 128 + (((2 * fg) ^ sw) << 4));
-      const u32x4 hi = *(const u32x4*)(base + r * 128 + (((2 * fg + 1) ^ sw) << 4));
+      const u32x4 lo = *(const u32x4*)(base + r * 128 + (((C0 * fg) ^ sw) << 4));
+      const u32x4 hi = *(const u32x4*)(base + r * 128 + (((C0 * fg + C1) ^ sw) << 4));
       return V8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
     };
-    auto rd0 = [&](int b, V8 (&af)[MT], V8 (&bf)[NH]) {
+    auto rd0 = [&](int b, V8 (&af)[MT], V8 (&bf)[NH], int (&sc)[MT]) {
       if (mode & 2) return;
       const unsigned char* sa = smem + b * STAGE;
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) af[mi] = frag(sa, wm * WM + mi * 16 + fr);
+      if constexpr (MXI) {
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi)
+          sc[mi] = (int)((*(const unsigned*)(smem + SCL_OFF + b * SCR + (wm * WM + mi * 16 + fr) * 4) >> (8 * fg)) & 255u);
+      }
 #pragma unroll
       for (int ni = 0; ni < NH; ++ni) bf[ni] = frag(sa + A_BYTES, wn * WN + ni * 16 + fr);
     };
@@ -401,27 +446,36 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
 #pragma unroll
       for (int ni = 0; ni < NB1; ++ni) bf[ni] = frag(sb, wn * WN + (NH + ni) * 16 + fr);
     };
-    auto mm0 = [&](const V8 (&af)[MT], const V8 (&bf)[NH]) {
+    auto mm0 = [&](const V8 (&af)[MT], const V8 (&bf)[NH], const int (&sc)[MT]) {
       if (mode & 2) return;
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < NH; ++ni) acc[mi][ni] = mfma8(af[mi], bf[ni], acc[mi][ni]);
+        for (int ni = 0; ni < NH; ++ni)
+          acc[mi][ni] = MXI ? mfma8s(af[mi], bf[ni], acc[mi][ni], sc[mi]) : mfma8(af[mi], bf[ni], acc[mi][ni]);
     };
-    auto mm1 = [&](const V8 (&af)[MT], const V8 (&bf)[NB1]) {
+    auto mm1 = [&](const V8 (&af)[MT], const V8 (&bf)[NB1], const int (&sc)[MT]) {
       if (mode & 2) return;
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < NB1; ++ni) acc[mi][NH + ni] = mfma8(af[mi], bf[ni], acc[mi][NH + ni]);
+        for (int ni = 0; ni < NB1; ++ni)
+          acc[mi][NH + ni] = MXI ? mfma8s(af[mi], bf[ni], acc[mi][NH + ni], sc[mi])
+                                 : mfma8(af[mi], bf[ni], acc[mi][NH + ni]);
     };
     V8 a0[MT], a1[MT], b0[NH], b1[NB1];
-    rd0(0, a0, b0);
+    int s0[MT], s1[MT];
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) s0[mi] = s1[mi] = 127;
+    rd0(0, a0, b0, s0);
     auto step8 = [&](const bool refill, const int ahead, const int kt) {
       rd1(buf, b1);
 #pragma unroll
-      for (int mi = 0; mi < MT; ++mi) a1[mi] = a0[mi];
-      mm0(a0, b0);
+      for (int mi = 0; mi < MT; ++mi) {
+        a1[mi] = a0[mi];
+        s1[mi] = s0[mi];
+      }
+      mm0(a0, b0, s0);
       if (SCHED) {  // the 2 * NB1 half-1 reads between the MT * NH half-0 MFMAs
         constexpr int R1 = 2 * NB1, M0 = MT * NH, RPM = (R1 + M0 - 1) / M0;
 #pragma unroll
@@ -438,8 +492,8 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
       __builtin_amdgcn_s_barrier();
       if (refill) stage(kb + kt + NS, buf);
       buf = buf == NS - 1 ? 0 : buf + 1;
-      rd0(buf, a0, b0);
-      mm1(a1, b1);
+      rd0(buf, a0, b0, s0);
+      mm1(a1, b1, s1);
       if (SCHED) {  // refill DMA + the next stage's 2 * (MT + NH) half-0 reads between the MT * NB1 MFMAs
         constexpr int R0 = 2 * (MT + NH), M1 = MT * NB1, RPM = (R0 + M1 - 1) / M1;
 #pragma unroll
@@ -456,8 +510,8 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     for (; kt < nkl - NS; ++kt) step8(true, NS - 2, kt);
     for (; kt < nkl - 1; ++kt) step8(false, min(NS - 2, nkl - 2 - kt), kt);
     rd1(buf, b1);
-    mm0(a0, b0);
-    mm1(a0, b1);
+    mm0(a0, b0, s0);
+    mm1(a0, b1, s0);
   }
   constexpr bool lnf = LNF;
 
@@ -622,7 +676,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         const int rl = wm * WM + mi * 16 + fg * 4 - half * EROWS;
         float rsc[4];  // alpha, or for e4m3 the row's a_scale * alpha
 #pragma unroll
-        for (int j = 0; j < 4; ++j) rsc[j] = F8 ? sc_tab[rl + j + half * EROWS] : alpha;
+        for (int j = 0; j < 4; ++j) rsc[j] = (F8 && !MXI) ? sc_tab[rl + j + half * EROWS] : alpha;
         if (GEGLU) {
           // LN-fold operands read into registers ahead of the staging stores (same LDS object: hipcc would
           // otherwise re-read them after every store)
@@ -726,6 +780,18 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
 #pragma unroll
           for (int i = 0; i < 8; ++i) v[it][i] += (float)res[it][i];
         }
+        if constexpr (MXO) {  // 32-column block = 4 consecutive threads (VPR % 4 == 0, n0o % 32 == 0)
+          float am = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(v[it][i]));
+          am = fmaxf(am, __shfl_xor(am, 1, 64));
+          am = fmaxf(am, __shfl_xor(am, 2, 64));
+          const int E = mx_exp(am);
+          *(u32x2*)((uint8_t*)p.C + (long long)m * p.ldc + n) =
+              u32x2{mx_pack4(v[it][0], v[it][1], v[it][2], v[it][3], E), mx_pack4(v[it][4], v[it][5], v[it][6], v[it][7], E)};
+          if ((cv & 3) == 0) f8.o_bs[(long long)m * f8.o_bs_ld + n / 32] = (uint8_t)(E + 127);
+          continue;
+        }
         TO8 o;
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
@@ -759,7 +825,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         }
       }
     }
-    } else {  // edge tiles / unaligned operands: scalar, bounds-checked
+    } else if constexpr (!MXO) {  // edge tiles / unaligned operands: scalar, bounds-checked (MX: host-checked interior)
       for (int e = tid; e < EROWS * VPR; e += NTHR) {
         const int r = e / VPR, cv = e % VPR;
         const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
@@ -872,30 +938,30 @@ int choose_split(int m_ref, int N, int K, int bn) {
 }
 
 template <typename T, typename TO, int BM, int BN, int NW, int WAVES_M, int NS>
-int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s, const float* a_scale = nullptr) {
+int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
   dim3 grid(pl.tiles * pl.S), block(64 * NW);
   float* slabs = (float*)((char*)p->ws + 65536 * sizeof(unsigned));
   unsigned* cnt = (unsigned*)p->ws;
   if (p->conv) {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, true, false, TO>), grid, block, 0, s, *p, pl.S,
-                       pl.group_m, slabs, cnt, a_scale);
+                       pl.group_m, slabs, cnt, f8_args{});
   } else if (p->act == FD_ACT_GEGLU) {
     if constexpr ((BN / (NW / WAVES_M)) % 32 == 0) {
       if (p->ln_in)
         hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, true, TO, true>), grid, block, 0, s, *p,
-                           pl.S, pl.group_m, slabs, cnt, a_scale);
+                           pl.S, pl.group_m, slabs, cnt, f8_args{});
       else
         hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, true, TO>), grid, block, 0, s, *p, pl.S,
-                           pl.group_m, slabs, cnt, a_scale);
+                           pl.group_m, slabs, cnt, f8_args{});
     } else {
       return FD_ERR_ARG;
     }
   } else if (p->ln_in) {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO, true>), grid, block, 0, s, *p, pl.S,
-                       pl.group_m, slabs, cnt, a_scale);
+                       pl.group_m, slabs, cnt, f8_args{});
   } else {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO>), grid, block, 0, s, *p, pl.S,
-                       pl.group_m, slabs, cnt, a_scale);
+                       pl.group_m, slabs, cnt, f8_args{});
   }
   FD_LAUNCH_CHECK();
   return FD_OK;
@@ -1095,88 +1161,146 @@ extern "C" int fd_gemm8_try(fd_gemm_params* p0, void* stream) {
   return rc == FD_OK ? 1 : rc;
 }
 
-// ------------------------------------------------------------------------------------ e4m3 (fd_gemm_e4m3)
+// ------------------------------------------------------------------------------------ e4m3 (fd_gemm_e4m3 / _mxe4m3)
 namespace {
-template <typename TO, int BM, int BN, int NW, int WAVES_M>
-int launch8_e4m3(const fd_gemm_params* p, const Plan8& pl, const float* a_scale, hipStream_t s) {
+template <typename T, typename TO, int BM, int BN, int NW, int WAVES_M>
+int launch8_e4m3(const fd_gemm_params* p, const Plan8& pl, const f8_args& f8, hipStream_t s) {
   dim3 grid(pl.tiles), block(64 * NW);
   if (p->act == FD_ACT_GEGLU) {
     if constexpr ((BN / (NW / WAVES_M)) % 32 == 0)
-      hipLaunchKernelGGL((gemm8_kernel<uint8_t, BM, BN, NW, WAVES_M, 3, false, true, TO>), grid, block, 0, s, *p, 1,
-                         pl.group_m, nullptr, nullptr, a_scale);
+      hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, 3, false, true, TO>), grid, block, 0, s, *p, 1,
+                         pl.group_m, nullptr, nullptr, f8);
     else
       return FD_ERR_ARG;
   } else {
-    hipLaunchKernelGGL((gemm8_kernel<uint8_t, BM, BN, NW, WAVES_M, 3, false, false, TO>), grid, block, 0, s, *p, 1,
-                       pl.group_m, nullptr, nullptr, a_scale);
+    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, 3, false, false, TO>), grid, block, 0, s, *p, 1,
+                       pl.group_m, nullptr, nullptr, f8);
   }
   FD_LAUNCH_CHECK();
   return FD_OK;
 }
-}  // namespace
 
-// The e4m3 GEMM of fd_gemm_e4m3 on the eight-wave kernel family (p->A / p->B e4m3 bytes, p->alpha = w_scale,
-// a_scale[M] per-row activation scales).  No split-K: every output is one accumulator over K in order, so the
-// tile shape -- chosen here from (M, N, K) -- never changes a bit (batched TLC tiles stay bitwise).  Tile choice:
-// least rounds x per-tile time on 256 CUs, the per-tile time a + b * K / 1280 us fitted per shape to the graph-timed
-// launches of profiles/r03_f8_tiles.jsonl (K = 640 .. 5120; the fixed part -- prologue, epilogue, launch ramp --
-// is 40-60 % of a K = 1280 tile); FD_F8_TILE = 256160 / 256128 / 128160 / 64160 forces one (A/B, tests).
-// Returns 1 when launched, 0 when not applicable (ragged K, batch, alignment), < 0 on error.
-extern "C" int fd_gemm8_e4m3_try(fd_gemm_params* p, const float* a_scale, void* stream) {
-  if (p->batch > 1 || p->conv || p->ln_in || p->ln_out || p->rowbias || p->K % 128) return 0;
-  if (((unsigned long long)p->A | (unsigned long long)p->B) & 15 || p->lda % 16 || p->ldb % 16) return 0;
+// Tile plan for the e4m3 kernels.  No split-K: every output is one accumulator over K in order, so the tile shape --
+// chosen from (M, N, K) -- never changes a bit (batched TLC tiles stay bitwise).  Least rounds x per-tile time on
+// 256 CUs, the per-tile time a + b * K / 1280 us fitted per shape to the graph-timed launches of
+// profiles/r03_f8_tiles.jsonl (K = 640 .. 5120; the fixed part -- prologue, epilogue, launch ramp -- is 40-60 % of a
+// K = 1280 tile); FD_F8_TILE = 256160 / 256128 / 128160 / 64160 forces one (A/B, tests).  mx_out: only tiles whose
+// output columns are whole 32-column blocks and lie inside M / N_out (the MX epilogue has no edge path).
+int plan_e4m3(const fd_gemm_params* p, bool mx_out, Plan8* pl) {
   const int force = env_i("FD_F8_TILE", 0);  // read per call: tests compare the shapes in one process
   struct Cand { int bm, bn, nw, wm; double a, b; };
   static const Cand cands[4] = {{256, 160, 8, 8, 10.6, 10.2}, {256, 128, 8, 4, 7.5, 7.9},
                                 {128, 160, 4, 2, 7.4, 6.0}, {64, 160, 4, 2, 5.65, 4.42}};
   const bool geglu = p->act == FD_ACT_GEGLU;
+  const int nout = geglu ? p->N / 2 : p->N;
   int best = -1;
   double bt = 1e30;
   for (int c = 0; c < 4; ++c) {
     const Cand& q = cands[c];
     if (geglu && (q.bn / (q.nw / q.wm)) % 32) continue;
     if (force && force != q.bm * 1000 + q.bn) continue;
+    const int bno = geglu ? q.bn / 2 : q.bn;
+    if (mx_out && (bno % 32 || nout % bno || p->M % q.bm)) continue;
     const long long tiles = (long long)((p->M + q.bm - 1) / q.bm) * ((p->N + q.bn - 1) / q.bn);
     // the 256 x 160 GEGLU tile stores 80 columns: its fixed part is relatively smaller (fit: 0.9x)
     const double t = (double)((tiles + 255) / 256) * (q.a + q.b * p->K / 1280.0) * (geglu && c == 0 ? 0.9 : 1.0);
     if (t < bt * 0.999) { bt = t; best = c; }
   }
   if (best < 0) return 0;
-  Plan8 pl;
-  pl.bm = cands[best].bm;
-  pl.bn = cands[best].bn;
-  pl.nw = cands[best].nw;
-  pl.waves_m = cands[best].wm;
-  pl.ns = 3;
-  pl.S = 1;
-  const int tiles_m = (p->M + pl.bm - 1) / pl.bm, tiles_n = (p->N + pl.bn - 1) / pl.bn;
-  pl.tiles = tiles_m * tiles_n;
-  {  // group_m as plan8
-    const long long per_xcd = ((long long)pl.tiles + 7) / 8;
-    double bestc = 1e30;
-    int gm = 1;
-    for (int g = 1; g <= tiles_m; g *= 2) {
-      const long long cols = per_xcd < g ? 1 : (per_xcd + g - 1) / g;
-      const long long rows = per_xcd < g ? per_xcd : g;
-      const double c = rows * (double)pl.bm + (cols < tiles_n ? cols : tiles_n) * (double)pl.bn;
-      if (c < bestc - 1e-9) { bestc = c; gm = g; }
-    }
-    pl.group_m = gm;
+  pl->bm = cands[best].bm;
+  pl->bn = cands[best].bn;
+  pl->nw = cands[best].nw;
+  pl->waves_m = cands[best].wm;
+  pl->ns = 3;
+  pl->S = 1;
+  const int tiles_m = (p->M + pl->bm - 1) / pl->bm, tiles_n = (p->N + pl->bn - 1) / pl->bn;
+  pl->tiles = tiles_m * tiles_n;
+  const long long per_xcd = ((long long)pl->tiles + 7) / 8;  // group_m as plan8
+  double bestc = 1e30;
+  int gm = 1;
+  for (int g = 1; g <= tiles_m; g *= 2) {
+    const long long cols = per_xcd < g ? 1 : (per_xcd + g - 1) / g;
+    const long long rows = per_xcd < g ? per_xcd : g;
+    const double c = rows * (double)pl->bm + (cols < tiles_n ? cols : tiles_n) * (double)pl->bn;
+    if (c < bestc - 1e-9) { bestc = c; gm = g; }
   }
-  fd_gemm_params q = *p;
-  q.gn_part = nullptr;
-  hipStream_t s = (hipStream_t)stream;
+  pl->group_m = gm;
+  return 1;
+}
+
+template <typename T>
+int launch_e4m3(const fd_gemm_params* p, const Plan8& pl, const f8_args& f8, int out_dtype, hipStream_t s) {
   int rc = FD_ERR_DTYPE;
-#define FD_G8F(BM_, BN_, NW_, WM_) FD_DISPATCH_O(q.out_dtype, rc = (launch8_e4m3<TO, BM_, BN_, NW_, WM_>(&q, pl, a_scale, s)))
-  if (pl.bm == 256 && pl.bn == 160) {
-    FD_G8F(256, 160, 8, 8);
-  } else if (pl.bm == 256) {
-    FD_G8F(256, 128, 8, 4);
-  } else if (pl.bm == 128) {
-    FD_G8F(128, 160, 4, 2);
-  } else {
-    FD_G8F(64, 160, 4, 2);
+#define FD_G8F(TO_)                                                                            \
+  if (pl.bm == 256 && pl.bn == 160) rc = launch8_e4m3<T, TO_, 256, 160, 8, 8>(p, pl, f8, s);   \
+  else if (pl.bm == 256) rc = launch8_e4m3<T, TO_, 256, 128, 8, 4>(p, pl, f8, s);              \
+  else if (pl.bm == 128) rc = launch8_e4m3<T, TO_, 128, 160, 4, 2>(p, pl, f8, s);              \
+  else rc = launch8_e4m3<T, TO_, 64, 160, 4, 2>(p, pl, f8, s);
+  if (out_dtype == FD_BF16) {
+    FD_G8F(bf16)
+  } else if (out_dtype == FD_F16) {
+    FD_G8F(f16)
+  } else if (out_dtype == FD_F32) {
+    FD_G8F(float)
+  } else if (out_dtype == FD_MXE4M3) {
+    FD_G8F(uint8_t)
   }
 #undef FD_G8F
+  return rc;
+}
+}  // namespace
+
+// The e4m3 GEMM of fd_gemm_e4m3 on the eight-wave kernel family (p->A / p->B e4m3 bytes, p->alpha = w_scale,
+// a_scale[M] per-row activation scales).  Returns 1 when launched, 0 when not applicable (ragged K, batch,
+// alignment), < 0 on error.
+extern "C" int fd_gemm8_e4m3_try(fd_gemm_params* p, const float* a_scale, void* stream) {
+  if (p->batch > 1 || p->conv || p->ln_in || p->ln_out || p->rowbias || p->K % 128) return 0;
+  if (((unsigned long long)p->A | (unsigned long long)p->B) & 15 || p->lda % 16 || p->ldb % 16) return 0;
+  Plan8 pl;
+  if (!plan_e4m3(p, false, &pl)) return 0;
+  fd_gemm_params q = *p;
+  q.gn_part = nullptr;
+  f8_args f8{a_scale, nullptr, 0, nullptr, 0};
+  const int rc = launch_e4m3<uint8_t>(&q, pl, f8, q.out_dtype, (hipStream_t)stream);
   return rc == FD_OK ? 1 : rc;
+}
+
+extern "C" int fd_gemm_mxe4m3(const void* A8, long long lda, const void* a_bs, long long ldas, const void* W8,
+                              long long ldw, float w_scale, void* C, long long ldc, void* c_bs, long long ldcs, int M,
+                              int N, int K, const float* bias, const void* residual, long long ldr, int act,
+                              int out_dtype, void* stream) {
+  if (!A8 || !a_bs || !W8 || !C) return FD_ERR_ARG;
+  if (act < FD_ACT_NONE || act > FD_ACT_GEGLU) return FD_ERR_ARG;
+  const int nout = act == FD_ACT_GEGLU ? N / 2 : N;
+  if (M <= 0 || N <= 0 || K <= 0 || K % 128 || lda % 16 || ldw % 16 || lda < K || ldw < K || ldc < nout)
+    return FD_ERR_SHAPE;
+  if (act == FD_ACT_GEGLU && (N % 32)) return FD_ERR_SHAPE;
+  if (ldas % 4 || ldas < K / 32 || ((unsigned long long)a_bs & 3)) return FD_ERR_SHAPE;
+  if ((((unsigned long long)A8) | ((unsigned long long)W8)) & 15) return FD_ERR_ARG;
+  if (out_dtype != FD_BF16 && out_dtype != FD_F16 && out_dtype != FD_F32 && out_dtype != FD_MXE4M3) return FD_ERR_DTYPE;
+  const bool mx_out = out_dtype == FD_MXE4M3;
+  if (residual && (ldr < nout || out_dtype == FD_F32 || mx_out)) return FD_ERR_SHAPE;
+  if (mx_out && (!c_bs || ldcs < nout / 32 || ldc % 8 || ((unsigned long long)C & 7))) return FD_ERR_SHAPE;
+  fd_gemm_params p{};
+  p.A = A8;
+  p.B = W8;
+  p.C = C;
+  p.lda = lda;
+  p.ldb = ldw;
+  p.ldc = ldc;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.batch = 1;
+  p.bias = bias;
+  p.residual = residual;
+  p.ldr = ldr;
+  p.alpha = w_scale;
+  p.act = act;
+  p.out_dtype = out_dtype;
+  p.m_ref = M;
+  Plan8 pl;
+  if (!plan_e4m3(&p, mx_out, &pl)) return FD_ERR_SHAPE;
+  f8_args f8{nullptr, (const uint8_t*)a_bs, ldas, (uint8_t*)c_bs, ldcs};
+  return launch_e4m3<mx8_t>(&p, pl, f8, out_dtype, (hipStream_t)stream);
 }

@@ -435,7 +435,59 @@ __global__ __launch_bounds__(256) void quant_rows_e4m3_wave_kernel(const T* __re
     }
   }
 }
+// MX e4m3 quantization (fd_quant_rows_mx): one thread per 8 consecutive elements of a row, a 32-element block = 4
+// consecutive threads (K % 32 == 0), block amax by two xor shuffles, then mx_exp / mx_pack4 (fd_common.h).
+template <typename T>
+__global__ __launch_bounds__(256) void quant_rows_mx_kernel(const T* __restrict__ x, long long ldx,
+                                                            uint8_t* __restrict__ q, long long ldq,
+                                                            uint8_t* __restrict__ sb, long long lds, int M, int K) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int vpr = K / 8;
+  const long long row = t / vpr;
+  const int v = (int)(t - row * vpr);
+  const bool ok = row < M;  // groups of 4 threads share a row: all in or all out
+  float f[8];
+  if (ok) {
+    F8Vec<T>::ld(x + row * ldx + v * 8, f);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = 0.f;
+  }
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(f[i]));
+  am = fmaxf(am, __shfl_xor(am, 1, 64));
+  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  if (!ok) return;
+  const int E = mx_exp(am);
+  *(u32x2*)(q + row * ldq + v * 8) = u32x2{mx_pack4(f[0], f[1], f[2], f[3], E), mx_pack4(f[4], f[5], f[6], f[7], E)};
+  if ((v & 3) == 0) sb[row * lds + v / 4] = (uint8_t)(E + 127);
+}
 }  // namespace
+
+extern "C" int fd_quant_rows_mx(const void* x, long long ldx, void* q, long long ldq, void* s, long long lds, int M,
+                                int K, int dtype, void* stream) {
+  if (!x || !q || !s) return FD_ERR_ARG;
+  if (M <= 0 || K <= 0 || (K % 32) || ldx < K || ldq < K || lds < K / 32 || (ldq % 8)) return FD_ERR_SHAPE;
+  const int esz = dtype == FD_F32 ? 4 : 2;
+  if ((((unsigned long long)x) & 15) || ((ldx * esz) % 16) || (((unsigned long long)q) & 7)) return FD_ERR_ARG;
+  const long long threads = (long long)M * (K / 8);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == FD_BF16)
+    hipLaunchKernelGGL(quant_rows_mx_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ldx, (uint8_t*)q, ldq,
+                       (uint8_t*)s, lds, M, K);
+  else if (dtype == FD_F16)
+    hipLaunchKernelGGL(quant_rows_mx_kernel<f16>, grid, dim3(256), 0, st, (const f16*)x, ldx, (uint8_t*)q, ldq,
+                       (uint8_t*)s, lds, M, K);
+  else if (dtype == FD_F32)
+    hipLaunchKernelGGL(quant_rows_mx_kernel<float>, grid, dim3(256), 0, st, (const float*)x, ldx, (uint8_t*)q, ldq,
+                       (uint8_t*)s, lds, M, K);
+  else
+    return FD_ERR_DTYPE;
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
 
 extern "C" int fd_quant_rows_e4m3(const void* x, long long ldx, void* q, long long ldq, float* scale, int M, int K,
                                   int dtype, void* stream) {

@@ -355,15 +355,18 @@ extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma
 }
 
 // ------------------------------------------------------------------------------------------------
-// LayerNorm: one wave per row, 4 rows per 256-thread block; row kept in registers (C <= 2048).
-// Q8: instead of y, write the row quantized to e4m3 for fd_gemm_e4m3 (the use_fp8 model): the LayerNorm output is
+// LayerNorm: one wave per row, 4 rows per 256-thread block; row kept in registers (C <= 2048).  Every output path
+// computes fma((x - mean) * rstd, gamma, beta) explicitly, so the y / e4m3 / MX forms round identically.
+// Q8 = 1: instead of y, write the row quantized to e4m3 for fd_gemm_e4m3 (the use_fp8 model): the LayerNorm output is
 // rounded to T first and then quantized exactly as fd_quant_rows_e4m3 does, so LN + quant fused == LN; quant.
-template <typename T, bool Q8>
+// Q8 = 2: the same rounded output as MX e4m3 (fd_quant_rows_mx's bytes): a 32-element block = 4 consecutive lanes.
+template <typename T, int Q8>
 __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x, long long ldx, T* __restrict__ y,
                                                          long long ldy, const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, int M, int C, float eps,
                                                          uint8_t* __restrict__ q8, long long ldq,
-                                                         float* __restrict__ qscale) {
+                                                         float* __restrict__ qscale, uint8_t* __restrict__ qbs = nullptr,
+                                                         long long ldbs = 0) {
   typedef typename VecT<T>::v8 V8;
   constexpr int MAXV = 4;  // up to 4 vectors of 8 per lane => C <= 2048
   const int lane = threadIdx.x & 63;
@@ -412,7 +415,36 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
     }
   }
   const float rstd = rsqrtf(wave_sum(q) / C + eps);
-  if (Q8) {
+  if (Q8 == 2) {  // C % 32 == 0: a lane's vectors are whole quarters of blocks, groups of 4 lanes all in or out
+    V8 outs[MAXV];  // the rounded output first (as the y path stores it), then quantized from those values
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int v = lane + k * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        outs[k][i] = v < VPR ? (T)__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3], b4[k][i >> 2][i & 3])
+                             : (T)0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int v = lane + k * 64;
+      float am = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf((float)outs[k][i]));
+      am = fmaxf(am, __shfl_xor(am, 1, 64));
+      am = fmaxf(am, __shfl_xor(am, 2, 64));
+      if (v < VPR) {
+        const int E = mx_exp(am);
+        const V8 o = outs[k];
+        *(u32x2*)(q8 + row * ldq + v * 8) =
+            u32x2{mx_pack4((float)o[0], (float)o[1], (float)o[2], (float)o[3], E),
+                  mx_pack4((float)o[4], (float)o[5], (float)o[6], (float)o[7], E)};
+        if ((v & 3) == 0) qbs[row * ldbs + v / 4] = (uint8_t)(E + 127);
+      }
+    }
+    return;
+  }
+  if (Q8 == 1) {
     V8 outs[MAXV];
     float amax = 0.f;
 #pragma unroll
@@ -421,7 +453,7 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
       if (v < VPR) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          outs[k][i] = (T)((vals[k][i] - mean) * rstd * g4[k][i >> 2][i & 3] + b4[k][i >> 2][i & 3]);
+          outs[k][i] = (T)__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3], b4[k][i >> 2][i & 3]);
           amax = fmaxf(amax, fabsf((float)outs[k][i]));
         }
       }
@@ -451,7 +483,7 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
       V8 out;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        out[i] = (T)((vals[k][i] - mean) * rstd * g4[k][i >> 2][i & 3] + b4[k][i >> 2][i & 3]);
+        out[i] = (T)__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3], b4[k][i >> 2][i & 3]);
       *(V8*)(yr + v * 8) = out;
     }
   }
@@ -463,7 +495,7 @@ extern "C" int fd_layer_norm(const void* x, long long ldx, void* y, long long ld
   if ((((unsigned long long)gamma) | ((unsigned long long)beta)) & 15) return FD_ERR_ARG;  // 16-B vector loads
   if (M <= 0 || C <= 0 || C % 8 || C > 2048 || (ldx & 7) || (ldy & 7)) return FD_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((layer_norm_kernel<T, false>), dim3((M + 3) / 4), dim3(256), 0, s,
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((layer_norm_kernel<T, 0>), dim3((M + 3) / 4), dim3(256), 0, s,
                                           (const T*)x, ldx, (T*)y, ldy, gamma, beta, M, C, eps, nullptr, 0, nullptr));
   FD_LAUNCH_CHECK();
   return FD_OK;
@@ -476,9 +508,24 @@ extern "C" int fd_layer_norm_e4m3(const void* x, long long ldx, void* q, long lo
   if ((((unsigned long long)gamma) | ((unsigned long long)beta)) & 15) return FD_ERR_ARG;
   if (M <= 0 || C <= 0 || C % 8 || C > 2048 || (ldx & 7) || (ldq & 7) || ldq < C) return FD_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((layer_norm_kernel<T, true>), dim3((M + 3) / 4), dim3(256), 0, s,
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((layer_norm_kernel<T, 1>), dim3((M + 3) / 4), dim3(256), 0, s,
                                           (const T*)x, ldx, (T*)nullptr, 0, gamma, beta, M, C, eps, (uint8_t*)q, ldq,
-                                          scale));
+                                          scale, nullptr, 0));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+extern "C" int fd_layer_norm_mx(const void* x, long long ldx, void* q, long long ldq, void* sb, long long lds,
+                                const float* gamma, const float* beta, int M, int C, float eps, int dtype, void* stream) {
+  if (!x || !q || !sb || !gamma || !beta) return FD_ERR_ARG;
+  if ((((unsigned long long)gamma) | ((unsigned long long)beta)) & 15) return FD_ERR_ARG;
+  if (((unsigned long long)q) & 7) return FD_ERR_ARG;
+  if (M <= 0 || C <= 0 || C % 32 || C > 2048 || (ldx & 7) || (ldq & 7) || ldq < C || lds < C / 32)
+    return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((layer_norm_kernel<T, 2>), dim3((M + 3) / 4), dim3(256), 0, s,
+                                          (const T*)x, ldx, (T*)nullptr, 0, gamma, beta, M, C, eps, (uint8_t*)q, ldq,
+                                          nullptr, (uint8_t*)sb, lds));
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

@@ -53,6 +53,12 @@ _SIGS = {
                              c_int, c_int, c_vp]),
     "fd_layer_norm_e4m3": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp]),
     "fd_quant_rows_e4m3": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_int, c_int, c_int, c_vp]),
+    "fd_gemm_mxe4m3": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_f, c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_int,
+                               c_vp, c_vp, c_ll, c_int, c_int, c_vp]),
+    "fd_quant_rows_mx": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_int, c_vp]),
+    "fd_layer_norm_mx": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp]),
+    "fd_flash_attn_mx": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_vp, c_ll,
+                                 c_ll, c_int, c_int, c_int, c_int, c_int, c_int, c_f, c_int, c_vp]),
     "fd_layer_norm": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_vp, c_int, c_int, c_f, c_int, c_vp]),
     "fd_flash_attn": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_int, c_int,
                               c_int, c_int, c_int, c_int, c_f, c_int, c_vp]),

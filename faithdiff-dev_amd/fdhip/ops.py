@@ -282,6 +282,96 @@ def gemm_e4m3(a8, a_scale, w8, out=None, bias=None, residual=None, w_scale=1.0, 
     return out
 
 
+class MX:
+    """An OCP MX e4m3 activation: q uint8 [M, K] (e4m3 bytes) and s uint8 [M, K/32] (E8M0 block scales, byte =
+    exponent + 127), the format the use_fp8 model's producers (flash attention, GEGLU, LayerNorm) write for
+    fd_gemm_mxe4m3.  ``s`` rows are padded to a multiple of 4 bytes (the GEMM reads one dword per 128 elements)."""
+
+    def __init__(self, M, K, device, q=None, s=None):
+        if K % 32:
+            raise ValueError(f"MX: K={K} not a multiple of 32")
+        self.q = torch.empty((M, K), dtype=torch.uint8, device=device) if q is None else q
+        self.s = torch.empty((M, -(-K // 128) * 4), dtype=torch.uint8, device=device) if s is None else s
+
+    @property
+    def shape(self):
+        return tuple(self.q.shape)
+
+    def dequant(self):
+        """fp32 values (host-side checking only)."""
+        M, K = self.q.shape
+        e = self.s[:, :K // 32].to(torch.float32) - 127.0
+        return self.q.view(torch.float8_e4m3fn).float() * torch.exp2(e).repeat_interleave(32, dim=1)
+
+
+def _mx_out_tiles(M, nout, geglu):
+    """Whether fd_gemm_mxe4m3 has a tile shape for an MX output (its plan_e4m3 with mx_out): (rows, output columns)
+    dividing (M, nout) with the columns a multiple of 32."""
+    tiles = [(256, 64)] if geglu else [(256, 160), (256, 128), (128, 160), (64, 160)]
+    return any(M % bm == 0 and nout % bn == 0 for bm, bn in tiles)
+
+
+def quant_rows_mx(x, out=None):
+    """x [M, K] (bf16 / f16 / f32, K % 32 == 0) -> MX (fd_quant_rows_mx)."""
+    M, K = x.shape
+    out = MX(M, K, x.device) if out is None else out
+    L.check(L.load().fd_quant_rows_mx(L.ptr(x), x.stride(0), L.ptr(out.q), out.q.stride(0), L.ptr(out.s),
+                                      out.s.stride(0), M, K, L.dtype_code(x.dtype), L.stream()), "fd_quant_rows_mx")
+    return out
+
+
+def layer_norm_mx(x, gamma, beta, eps=1e-5, out=None):
+    """LayerNorm(x) rounded to x.dtype and written as MX (bitwise quant_rows_mx(layer_norm(x)))."""
+    M, C = x.shape
+    out = MX(M, C, x.device) if out is None else out
+    L.check(L.load().fd_layer_norm_mx(L.ptr(x), x.stride(0), L.ptr(out.q), out.q.stride(0), L.ptr(out.s),
+                                      out.s.stride(0), L.ptr(gamma), L.ptr(beta), M, C, eps, L.dtype_code(x.dtype),
+                                      L.stream()), "fd_layer_norm_mx")
+    return out
+
+
+def gemm_mx(a, w8, out=None, bias=None, residual=None, w_scale=1.0, act="none", out_dtype=torch.bfloat16):
+    """out = act(w_scale * (dequant(a) @ w8^T) + bias) + residual on the block-scaled e4m3 MFMA (fd_gemm_mxe4m3);
+    a: MX [M, K]; w8 e4m3 bytes [N, K] (geglu: packed by pack_geglu, N/2 output columns).  out_dtype "mx" (or an
+    MX ``out``): the output is written as MX e4m3 (GEGLU producer of the ff-out GEMM)."""
+    M, K = a.q.shape
+    N = w8.shape[0]
+    if w8.shape[1] != K:
+        raise ValueError(f"gemm_mx: K mismatch {a.q.shape} x {w8.shape}")
+    nout = N // 2 if act == "geglu" else N
+    mx_out = isinstance(out, MX) or out_dtype == "mx"
+    if out is None:
+        out = MX(M, nout, a.q.device) if mx_out else torch.empty((M, nout), dtype=out_dtype, device=a.q.device)
+    if mx_out and not _mx_out_tiles(M, nout, act == "geglu"):
+        # no tile shape covers this output with whole 32-column blocks (small test sizes): the fp32 output, then
+        # fd_quant_rows_mx -- the same bytes the fused epilogue writes (it quantizes the same fp32 values)
+        y = gemm_mx(a, w8, bias=bias, w_scale=w_scale, act=act, out_dtype=torch.float32)
+        return quant_rows_mx(y, out=out)
+    if mx_out:
+        cq, cs, ldcs, code = out.q, out.s, out.s.stride(0), 3
+    else:
+        cq, cs, ldcs, code = out, None, 0, L.dtype_code(out.dtype)
+        if residual is not None and residual.dtype != out.dtype:
+            raise ValueError(f"gemm_mx: residual dtype {residual.dtype} != output dtype {out.dtype}")
+    args = (L.ptr(a.q), a.q.stride(0), L.ptr(a.s), a.s.stride(0), L.ptr(w8), w8.stride(0), w_scale, L.ptr(cq),
+            cq.stride(0), L.ptr(cs), ldcs, M, N, K, L.ptr(bias), L.ptr(residual),
+            0 if residual is None else residual.stride(0), L.ACT[act], code, L.stream())
+    _timed("gemm_e4m3", 2.0 * M * N * K, 0.0, lambda: L.check(L.load().fd_gemm_mxe4m3(*args), "fd_gemm_mxe4m3"))
+    return out
+
+
+def flash_attn_mx(q, k, v, out, batch, heads, Lq, Lk, ldq, ldk, ldv, qbs, kbs, vbs, kv_mod=0, scale=0.125):
+    """flash_attn with the output written as MX (out: MX [batch * Lq, heads * 64]); the row of (b, q) is b * Lq + q."""
+    ldo = out.q.stride(0)
+    lds = out.s.stride(0)
+    _timed("flash_attn", 4.0 * batch * heads * Lq * Lk * 64, 0, label=f"flash b={batch} h={heads} Lq={Lq} Lk={Lk}",
+           launch=lambda: L.check(
+        L.load().fd_flash_attn_mx(L.ptr(q), ldq, qbs, L.ptr(k), ldk, kbs, L.ptr(v), ldv, vbs, L.ptr(out.q), ldo,
+                                  Lq * ldo, L.ptr(out.s), lds, Lq * lds, batch, heads, Lq, Lk, kv_mod, 0, scale,
+                                  L.dtype_code(q.dtype), L.stream()), "fd_flash_attn_mx"))
+    return out
+
+
 def linear_e4m3(x, w8, bias=None, residual=None, act="none", out=None):
     """nn.Linear of a quantize_8bit UNet on the fp8 MFMA: per-row e4m3 activations x e4m3 weight bytes."""
     q, s = quant_rows_e4m3(x)

@@ -44,6 +44,10 @@ class HipUNet:
         separate LayerNorm path is used (the fold needs W * gamma, which is not an e4m3 weight)."""
         L.require_device()
         self.fp8_mfma = bool(fp8_mfma)
+        # fp8 activations as OCP MX e4m3 (32-element blocks, E8M0 scales) written by their producers -- flash
+        # attention, the GEGLU epilogue, LayerNorm -- instead of per-row scales from separate quantization launches
+        # (FD_FP8_MX=0: the per-row form, A/B)
+        self.fp8_mx = self.fp8_mfma and os.environ.get("FD_FP8_MX", "1") != "0"
         self.device, self.dtype = torch.device(device), dtype
         f32 = torch.float32
         W = lambda k: _dev(sd[k], self.device, dtype)  # noqa: E731
@@ -263,6 +267,8 @@ class HipUNet:
         h = ops.group_norm(x, *t["norm"], B, HW, C, 32, 1e-6, silu=False, stats=self._gn_stats_of(x))
         if self.ln_fold:
             return self._t2d_folded(t, x, h, B, H, Wd)
+        if self.fp8_mx:
+            return self._t2d_mx(t, x, h, B, H, Wd)
         lin = self._lin
         h = lin(h, t["pin"][0], bias=t["pin"][1])
         qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
@@ -295,8 +301,35 @@ class HipUNet:
             lin(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
         return self._proj_out(t, h, x, B, HW)
 
+    def _t2d_mx(self, t, x, hn, B, H, Wd):
+        """_t2d of the fp8 model with MX e4m3 activations: every transformer Linear is fd_gemm_mxe4m3, its A operand
+        written as MX by the producer -- LayerNorm (norm1/2/3), flash attention (out-projections), the GEGLU epilogue
+        (ff out); only proj_in / proj_out inputs (GroupNorm output, residual stream) take a quantization launch."""
+        C, heads, HW = t["c"], t["heads"], H * Wd
+        M = B * HW
+        h = ops.gemm_mx(ops.quant_rows_mx(hn), t["pin"][0], bias=t["pin"][1], out_dtype=self.dtype)
+        qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
+        n8, att8, ff8 = ops.MX(M, C, self.device), ops.MX(M, C, self.device), ops.MX(M, 4 * C, self.device)
+        for b in t["blocks"]:
+            ops.gemm_mx(ops.layer_norm_mx(h, *b["n1"], 1e-5, out=n8), b["qkv"], out=qkv)
+            ops.flash_attn_mx(qkv, qkv[:, C:], qkv[:, 2 * C:], att8, B, heads, HW, HW, 3 * C, 3 * C, 3 * C,
+                              HW * 3 * C, HW * 3 * C, HW * 3 * C, kv_mod=0, scale=0.125)
+            ops.gemm_mx(att8, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
+            ops.gemm_mx(ops.layer_norm_mx(h, *b["n2"], 1e-5, out=n8), b["q2"], out=qkv[:, :C])
+            kv = self._kv[self._kv_row0:, b["kv_off"]:]
+            Lk, ldkv = self.Lk, self.kv_total
+            ops.flash_attn_mx(qkv, kv, kv[:, C:], att8, B, heads, HW, Lk, 3 * C, ldkv, ldkv,
+                              HW * 3 * C, Lk * ldkv, Lk * ldkv, kv_mod=self._kv_mod, scale=0.125)
+            ops.gemm_mx(att8, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
+            ops.gemm_mx(ops.layer_norm_mx(h, *b["n3"], 1e-5, out=n8), b["ff1"][0], bias=b["ff1"][1], act="geglu",
+                        out=ff8)
+            ops.gemm_mx(ff8, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
+        return self._proj_out(t, h, x, B, HW)
+
     def _proj_out(self, t, h, x, B, HW):
         """proj_out + residual; its epilogue also writes the next GroupNorm's statistics (16-bit GEMM)."""
+        if self.fp8_mx:
+            return ops.gemm_mx(ops.quant_rows_mx(h), t["pout"][0], bias=t["pout"][1], residual=x)
         if self.fp8_mfma:
             return ops.linear_e4m3(h, t["pout"][0], bias=t["pout"][1], residual=x)
         s = self._gn_new(B, HW)

@@ -154,6 +154,29 @@ int fd_gemm_e4m3(const void* A8, long long lda, const float* a_scale, const void
                  void* C, long long ldc, int M, int N, int K, const float* bias, const void* residual, long long ldr,
                  int act, int out_dtype, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * MX-fp8 (OCP MX e4m3: one E8M0 scale byte per 32 consecutive K elements of a row) -- the use_fp8 model's
+ * activation format when the producers write it directly (flash attention, GEGLU, LayerNorm; no separate
+ * quantization launch).  Scale rule (every producer): E = least exponent with amax_block <= 448 * 2^E,
+ * q = RNE_e4m3(v * 2^-E), byte = E + 127 (all-zero block: 127).
+ *
+ * GEMM: C = out( act(w_scale * sum_k (A8[m][k] * 2^(as[m][k/32] - 127)) * W8[n][k] + bias[n]) + residual[m][n] ),
+ * on v_mfma_scale_f32_16x16x128_f8f6f4 with the A block scales as the MFMA's per-lane scale operand.  A8 [M][lda]
+ * e4m3, as [M][ldas] bytes (ldas % 4 == 0, >= K / 32, 4-B aligned); W8 as fd_gemm_e4m3.  out_dtype FD_BF16 / FD_F32,
+ * or FD_MXE4M3: C gets e4m3 bytes [M][ldc] of the (GEGLU) output and c_bs [M][ldcs] its block scales (no residual;
+ * M % 256 == 0 and N_out % 64 == 0).  Requires K % 128 == 0.  Replaces: as fd_gemm_e4m3. */
+enum { FD_MXE4M3 = 3 };
+int fd_gemm_mxe4m3(const void* A8, long long lda, const void* a_bs, long long ldas, const void* W8, long long ldw,
+                   float w_scale, void* C, long long ldc, void* c_bs, long long ldcs, int M, int N, int K,
+                   const float* bias, const void* residual, long long ldr, int act, int out_dtype, void* stream);
+/* x[M][K] (bf16 / f16 / f32, row stride ldx) -> MX e4m3 q [M][ldq] + scales s [M][lds].  K % 32 == 0. */
+int fd_quant_rows_mx(const void* x, long long ldx, void* q, long long ldq, void* s, long long lds, int M, int K,
+                     int dtype, void* stream);
+/* LayerNorm (as fd_layer_norm, output rounded to dtype) written as MX e4m3 -- bitwise fd_layer_norm then
+ * fd_quant_rows_mx.  C % 32 == 0. */
+int fd_layer_norm_mx(const void* x, long long ldx, void* q, long long ldq, void* s, long long lds, const float* gamma,
+                     const float* beta, int M, int C, float eps, int dtype, void* stream);
+
 /* Per-row e4m3 quantization of x[M][K] (row stride ldx, bf16 / f16): scale[m] = amax_m / 448,
  * q[m][k] = e4m3_RNE(x[m][k] * 448 / amax_m) into q (row stride ldq bytes).  Requires K % 16 == 0,
  * ldx % 8 == 0, ldq % 16 == 0.  Activation side of fd_gemm_e4m3 (the reference has no counterpart: it
@@ -180,6 +203,14 @@ int fd_flash_attn(const void* q, long long ldq, long long q_bstride, const void*
                   long long k_bstride, const void* v, long long ldv, long long v_bstride, void* o, long long ldo,
                   long long o_bstride, int batch, int heads, int Lq, int Lk, int kv_mod, int causal, float scale,
                   int dtype, void* stream);
+/* fd_flash_attn (d = 64, bf16 in) with the output written as MX e4m3 for the use_fp8 model's out-projection
+ * (fd_gemm_mxe4m3): o8 e4m3 bytes at o8 + b * obs + q * ldo + h * 64 (ldo, obs in bytes, % 4 == 0), E8M0 scales of
+ * the (query, head)'s two 32-column blocks at osb[b * osbs + q * ldos + 2 h + {0, 1}], quantized from the fp32
+ * normalised output (fd_quant_rows_mx's rule). */
+int fd_flash_attn_mx(const void* q, long long ldq, long long q_bstride, const void* k, long long ldk,
+                     long long k_bstride, const void* v, long long ldv, long long v_bstride, void* o8, long long ldo,
+                     long long o_bstride, void* osb, long long ldos, long long os_bstride, int batch, int heads, int Lq,
+                     int Lk, int kv_mod, int causal, float scale, int dtype, void* stream);
 
 /* The information transformer's nn.MultiheadAttention(640, 8) with batch_first=False fed
  * (L=B, N=HW, E) (ext:242,251-254,576-577): for each pixel n, softmax attention over the L rows of

@@ -206,6 +206,128 @@ def test_gemm_e4m3_eight_wave_bitwise_vs_four_wave(tile, M, N, K, act, out):
     assert torch.equal(got, want)
 
 
+# ---------------------------------------------------------------------------------------------- MX e4m3 (OCP MX)
+def mx_ref(x, K=None):
+    """Restatement of the MX rule (fd_common.h mx_exp / mx_pack4) on the host: per 32-element block,
+    E = least exponent with amax <= 448 * 2^E (amax = ma * 2^ea, ma in [1, 2): E = ea - 8 if ma <= 1.75 else ea - 7;
+    all-zero block E = 0), q = RNE_e4m3(x * 2^-E), scale byte = E + 127."""
+    x = x.float().cpu()
+    M, K = x.shape
+    xb = x.reshape(M, K // 32, 32)
+    amax = xb.abs().amax(-1)
+    m, e = torch.frexp(amax)  # amax = m * 2^e, m in [0.5, 1)
+    E = torch.where(2 * m <= 1.75, e - 1 - 8, e - 1 - 7)
+    E = torch.where(amax > 0, E, torch.zeros_like(E)).clamp(-127, 127)
+    q = e4m3((xb * torch.exp2(-E.float())[..., None]).reshape(M, K))
+    return q, (E + 127).to(torch.uint8)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize("M,K", [(1, 32), (77, 2048), (2048, 1280), (513, 5120), (6, 2080)])
+def test_quant_rows_mx_bitexact(dtype, M, K):
+    from fdhip import ops
+    x = (torch.randn(M, K, device=DEV) * torch.logspace(-4, 3, M, device=DEV)[:, None]).to(dtype)
+    x[0, :32] = 0  # an all-zero block
+    if K >= 96:
+        x[0, 64:96] = 448.0 * 4  # amax exactly 448 * 2^2 (ma = 1.75: E = 2, no saturation)
+    got = ops.quant_rows_mx(x)
+    want_q, want_s = mx_ref(x)
+    assert torch.equal(got.s[:, :K // 32].cpu(), want_s)
+    assert torch.equal(got.q.cpu(), want_q)
+    # dequantized within e4m3's half ulp of each value (2^-4 relative; 2^-10 * 2^E in the subnormal range), nothing
+    # saturated
+    deq = got.dequant().cpu()
+    blk = torch.exp2(want_s.float() - 127).repeat_interleave(32, 1)
+    assert torch.all((deq - x.float().cpu()).abs() <= x.float().cpu().abs() * 2.0 ** -4 + blk * 2.0 ** -10)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,C", [(4096, 640), (1024, 1280), (7, 320), (130, 2048)])
+def test_layer_norm_mx_equals_layer_norm_then_quant(dtype, M, C):
+    from fdhip import ops
+    x = (torch.randn(M, C, device=DEV) * 3 + 1).to(dtype)
+    g = torch.randn(C, device=DEV)
+    b = torch.randn(C, device=DEV)
+    got = ops.layer_norm_mx(x, g, b, 1e-5)
+    ref = ops.quant_rows_mx(ops.layer_norm(x, g, b, 1e-5))
+    assert torch.equal(got.s[:, :C // 32], ref.s[:, :C // 32]) and torch.equal(got.q, ref.q)
+
+
+@pytest.mark.parametrize("tile", ["256160", "256128", "128160", "64160"])
+@pytest.mark.parametrize("M,N,K", [(2048, 1280, 1280), (300, 200, 640), (700, 320, 384)])
+def test_gemm_mx_exact(tile, M, N, K):
+    """Exact data through the block-scaled MFMA's per-lane A scales: small-integer e4m3 values with E8M0 block
+    scales 2^-3 .. 2^3 (every product and partial sum exact in fp32), every tile shape incl. edge tiles."""
+    from fdhip import ops
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randint(-6, 7, (M, K), generator=g).float()
+    sb = torch.randint(124, 131, (M, K // 32), generator=g).to(torch.uint8)
+    w = torch.randint(-4, 5, (N, K), generator=g).float() * 0.5
+    mx = ops.MX(M, K, DEV)
+    mx.q.copy_(e4m3(a).to(DEV))
+    mx.s.zero_()
+    mx.s[:, :K // 32].copy_(sb.to(DEV))
+    with _env(FD_F8_TILE=tile):
+        got = ops.gemm_mx(mx, e4m3(w).to(DEV), out_dtype=torch.float32).cpu()
+    deq = a.double() * torch.exp2(sb.double() - 127).repeat_interleave(32, 1)
+    assert torch.equal(got.double(), deq @ w.double().T)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(2048, 1280, 1280, "none"), (2048, 2560, 1280, "geglu"),
+                                       (8192, 640, 2560, "none"), (333, 128, 384, "geglu")])
+def test_gemm_mx_vs_dequantized_and_mx_output(M, N, K, act):
+    """Random operands: the bf16 / fp32 outputs against the fp64 product of the same dequantized operands, and
+    the MX output (GEGLU producer of the ff-out GEMM) bitwise equal to fd_quant_rows_mx of the fp32 output."""
+    from fdhip import ops
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV) * K ** -0.5
+    b = torch.randn(N, device=DEV) * 0.1
+    if act == "geglu":
+        w, b = ops.pack_geglu(w, b)
+    w8 = ops.pack_e4m3(w)
+    a = ops.quant_rows_mx(x)
+    y32 = ops.gemm_mx(a, w8, bias=b, act=act, out_dtype=torch.float32)
+    lin = a.dequant().double() @ widen(w8).double().T + b.double()
+    if act == "geglu":
+        Fh = N // 2
+        hh = lin.view(M, N // 32, 2, 16)
+        want = (hh[:, :, 0] * torch.nn.functional.gelu(hh[:, :, 1])).reshape(M, Fh)
+        assert rel_l2(y32, want) < 5e-5
+        got = ops.gemm_mx(a, w8, bias=b, act=act, out_dtype="mx")
+        ref = ops.quant_rows_mx(y32)
+        assert torch.equal(got.s[:, :Fh // 32], ref.s[:, :Fh // 32]) and torch.equal(got.q, ref.q)
+    else:
+        assert rel_l2(y32, lin) < 1e-5
+        res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+        yb = ops.gemm_mx(a, w8, bias=b, residual=res)
+        assert rel_l2(yb, lin + res.double()) < 4e-3
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk", [(2, 20, 1024, 1024), (2, 10, 4096, 77), (1, 5, 200, 77), (2, 2, 333, 128)])
+def test_flash_attn_mx_output(B, H, Lq, Lk):
+    """fd_flash_attn_mx: the same attention as fd_flash_attn, output as MX e4m3 quantized from the fp32 result:
+    its dequantized values within e4m3 rounding of the bf16 output, and its block scales those of the bf16
+    output's blocks up to one exponent step (the bf16 rounding of amax)."""
+    from fdhip import ops
+    C = H * 64
+    g = torch.Generator(device=DEV).manual_seed(Lq + Lk)
+    q = torch.randn(B * Lq, C, device=DEV, generator=g).to(torch.bfloat16)
+    kv = torch.randn(B * Lk, 2 * C, device=DEV, generator=g).to(torch.bfloat16)
+    ref = torch.empty(B * Lq, C, device=DEV, dtype=torch.bfloat16)
+    ops.flash_attn(q, kv, kv[:, C:], ref, B, H, Lq, Lk, C, 2 * C, 2 * C, C, Lq * C, Lk * 2 * C, Lk * 2 * C, Lq * C,
+                   scale=0.125)
+    out = ops.MX(B * Lq, C, DEV)
+    ops.flash_attn_mx(q, kv, kv[:, C:], out, B, H, Lq, Lk, C, 2 * C, 2 * C, Lq * C, Lk * 2 * C, Lk * 2 * C,
+                      scale=0.125)
+    deq, r = out.dequant(), ref.float()
+    blk = torch.exp2(out.s[:, :C // 32].float() - 127).repeat_interleave(32, 1)  # the block's scale 2^E
+    # e4m3 RNE: half an ulp = 2^-4 relative for normals, 2^-10 * 2^E below them; plus the bf16 rounding of ref
+    assert torch.all((deq - r).abs() <= r.abs() * (2.0 ** -4 + 2.0 ** -7) + blk * 2.0 ** -9)
+    _, s_ref = mx_ref(ref)
+    assert (out.s[:, :C // 32].cpu().int() - s_ref.int()).abs().max() <= 1
+    assert rel_l2(deq, r) < 3e-2
+
+
 _FP8 = {}
 
 
