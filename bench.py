@@ -57,7 +57,8 @@ PEAK_FP8_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 # committed rocprofv3 PMC traffic passes, newest first (scripts/r02_prof.sh + scripts/traffic_from_pmc.py)
 TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in
-                 ("r03_gemm_traffic.json", "r03_gemm_traffic_fp8.json", "r02f_gemm_traffic.json")]
+                 ("r03c_gemm_traffic.json", "r03c_gemm_traffic_fp8.json", "r03_gemm_traffic.json",
+                  "r03_gemm_traffic_fp8.json", "r02f_gemm_traffic.json")]
 
 
 def parse(argv=None):
@@ -464,7 +465,8 @@ def roofline_leg(loop, fp8):
                                "traffic_note": ("HBM bytes per forward of the e4m3 launches (rocprofv3 PMC pass, "
                                                 + tr["file"] + ")") if tr is not None and fp8 else
                                "no PMC pass committed for this workload",
-                               "kernel": "gemm_e4m3_dma_kernel (transformer Linears, e4m3 x e4m3)",
+                               "kernel": "gemm8_kernel on e4m3 operands (transformer Linears, e4m3 x e4m3 on "
+                                         "v_mfma_scale_f32_16x16x128_f8f6f4; MX block-scaled A unless FD_FP8_MX=0)",
                                "launches": n_f, "algorithmic_flops": fl_f, "kernel_ms_per_forward": round(ms_f, 3)}
     flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False, cond_embed=False)
     res["forward_graph_ms"] = round(fam["_all"][3], 3)

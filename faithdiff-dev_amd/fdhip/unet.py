@@ -48,6 +48,9 @@ class HipUNet:
         # attention, the GEGLU epilogue, LayerNorm -- instead of per-row scales from separate quantization launches
         # (FD_FP8_MX=0: the per-row form, A/B)
         self.fp8_mx = self.fp8_mfma and os.environ.get("FD_FP8_MX", "1") != "0"
+        # MX output straight from the GEGLU epilogue (forces 256 x 128 tiles; profiles/r03_f8_tiles_mx.jsonl: 48.1 vs
+        # 39.7 + a 2048 x 5120 quantization for the 256 x 160 bf16 form); FD_FP8_MX_GEGLU=1 turns it on (A/B)
+        self.fp8_mx_geglu = os.environ.get("FD_FP8_MX_GEGLU", "0") == "1"
         self.device, self.dtype = torch.device(device), dtype
         f32 = torch.float32
         W = lambda k: _dev(sd[k], self.device, dtype)  # noqa: E731
@@ -321,8 +324,13 @@ class HipUNet:
             ops.flash_attn_mx(qkv, kv, kv[:, C:], att8, B, heads, HW, Lk, 3 * C, ldkv, ldkv,
                               HW * 3 * C, Lk * ldkv, Lk * ldkv, kv_mod=self._kv_mod, scale=0.125)
             ops.gemm_mx(att8, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
-            ops.gemm_mx(ops.layer_norm_mx(h, *b["n3"], 1e-5, out=n8), b["ff1"][0], bias=b["ff1"][1], act="geglu",
-                        out=ff8)
+            if self.fp8_mx_geglu:  # GEGLU epilogue writes MX (256 x 128 tiles: 32-column output blocks)
+                ops.gemm_mx(ops.layer_norm_mx(h, *b["n3"], 1e-5, out=n8), b["ff1"][0], bias=b["ff1"][1],
+                            act="geglu", out=ff8)
+            else:  # GEGLU on its faster 256 x 160 tiles in bf16, then one MX quantization launch
+                ff = ops.gemm_mx(ops.layer_norm_mx(h, *b["n3"], 1e-5, out=n8), b["ff1"][0], bias=b["ff1"][1],
+                                 act="geglu", out_dtype=self.dtype)
+                ops.quant_rows_mx(ff, out=ff8)
             ops.gemm_mx(ff8, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
         return self._proj_out(t, h, x, B, HW)
 

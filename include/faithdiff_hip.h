@@ -172,8 +172,8 @@ int fd_gemm_mxe4m3(const void* A8, long long lda, const void* a_bs, long long ld
 /* x[M][K] (bf16 / f16 / f32, row stride ldx) -> MX e4m3 q [M][ldq] + scales s [M][lds].  K % 32 == 0. */
 int fd_quant_rows_mx(const void* x, long long ldx, void* q, long long ldq, void* s, long long lds, int M, int K,
                      int dtype, void* stream);
-/* LayerNorm (as fd_layer_norm, output rounded to dtype) written as MX e4m3 -- bitwise fd_layer_norm then
- * fd_quant_rows_mx.  C % 32 == 0. */
+/* LayerNorm (as fd_layer_norm, output rounded to bf16) written as MX e4m3 -- bitwise fd_layer_norm then
+ * fd_quant_rows_mx.  C % 32 == 0; dtype FD_BF16 only. */
 int fd_layer_norm_mx(const void* x, long long ldx, void* q, long long ldq, void* s, long long lds, const float* gamma,
                      const float* beta, int M, int C, float eps, int dtype, void* stream);
 
