@@ -45,9 +45,11 @@ class HipUNet:
         L.require_device()
         self.fp8_mfma = bool(fp8_mfma)
         # fp8 activations as OCP MX e4m3 (32-element blocks, E8M0 scales) written by their producers -- flash
-        # attention, the GEGLU epilogue, LayerNorm -- instead of per-row scales from separate quantization launches
-        # (FD_FP8_MX=0: the per-row form, A/B)
-        self.fp8_mx = self.fp8_mfma and os.environ.get("FD_FP8_MX", "1") != "0"
+        # attention, LayerNorm -- instead of per-row scales from separate quantization launches.  Opt-in
+        # (FD_FP8_MX=1): on one box the C2 step measured 21.00 ms MX vs 20.88 ms per-row (profiles/r03_fp8_ab_*.json):
+        # the 140 quantization launches it removes are paid back by the MX GEMMs' per-K-step scale traffic
+        # (ff out 23.2 -> 25.0 us, profiles/r03_f8_tiles_mx.jsonl) and the MX epilogues
+        self.fp8_mx = self.fp8_mfma and os.environ.get("FD_FP8_MX", "0") == "1"
         # MX output straight from the GEGLU epilogue (forces 256 x 128 tiles; profiles/r03_f8_tiles_mx.jsonl: 48.1 vs
         # 39.7 + a 2048 x 5120 quantization for the 256 x 160 bf16 form); FD_FP8_MX_GEGLU=1 turns it on (A/B)
         self.fp8_mx_geglu = os.environ.get("FD_FP8_MX_GEGLU", "0") == "1"

@@ -349,11 +349,32 @@ def _fp8_pair():
         ref.load_state_dict(sd)
         ref.eval()
         _FP8["pair"] = (ref, HipUNet(sd, "cuda", torch.bfloat16, fp8_mfma=True))
+        _FP8["sd"] = sd
     return _FP8["pair"]
 
 
+def _fp8_mx_unet():
+    """The same e4m3 weights with MX activations (FD_FP8_MX=1: LayerNorm / flash attention write MX e4m3)."""
+    if "mx" not in _FP8:
+        import os
+        from fdhip.unet import HipUNet
+        _fp8_pair()
+        old = os.environ.get("FD_FP8_MX")
+        os.environ["FD_FP8_MX"] = "1"
+        try:
+            _FP8["mx"] = HipUNet(_FP8["sd"], "cuda", torch.bfloat16, fp8_mfma=True)
+        finally:
+            if old is None:
+                os.environ.pop("FD_FP8_MX", None)
+            else:
+                os.environ["FD_FP8_MX"] = old
+        assert _FP8["mx"].fp8_mx
+    return _FP8["mx"]
+
+
+@pytest.mark.parametrize("mx", [False, True])
 @pytest.mark.parametrize("h,w", [(32, 32), (128, 128)])
-def test_unet_fp8_mfma_matches_oracle(h, w):
+def test_unet_fp8_mfma_matches_oracle(h, w, mx):
     """The opt-in e4m3-MFMA use_fp8 model (HipUNet(fp8_mfma=True): transformer Linears on the e4m3 MFMA) against
     the fp32 oracle on the same quantize_8bit weights, at a small tile and at the C2 tile (128^2).  Stated
     tolerance for this leg: rel-L2 <= 4e-2, cos >= 0.9996 on eps -- about 2x the error measured at 32^2 (1.86e-2,
@@ -361,11 +382,13 @@ def test_unet_fp8_mfma_matches_oracle(h, w):
     bits) at the Linear inputs."""
     from test_unet_gpu import make_inputs, metrics, run_hip, run_ref
     ref, hip = _fp8_pair()
+    if mx:  # MX e4m3 activations (opt-in form): same bar
+        hip = _fp8_mx_unet()
     B, x, cond, ctx, text, tids = make_inputs(h, w, 1, seed=3)
     out = run_hip(hip, B, x, cond, ctx, text, tids, 951.0, h, w)
     exp = run_ref(ref, B, x, cond, ctx, text, tids, 951.0)
     rel, cos = metrics(out, exp)
-    print(f"unet fp8-MFMA {h}x{w}: rel_l2 vs oracle={rel:.3e} cos={cos:.6f}")
+    print(f"unet fp8-MFMA{' MX' if mx else ''} {h}x{w}: rel_l2 vs oracle={rel:.3e} cos={cos:.6f}")
     assert rel < 4e-2 and cos > 0.9996
 
 
