@@ -124,9 +124,8 @@ __global__ void __launch_bounds__(64) gn_finalize_kernel(const float2* __restric
     s += v[u].x;
     q += v[u].y;
   }
-  // nchunks > 1024: the producer-epilogue partials of large images (fd_group_norm_partials at 512^2 / 1024^2:
-  // HW / 256 up to 4096, HW / 128 up to 8192) -- U more loads in flight per round, each lane still summing its
-  // chunks j, j + 64, ... in ascending order (the same bits as one load at a time)
+  // nchunks > 1024 goes to gn_finalize_wide_kernel (up to 8192); beyond that this loop takes U more loads in flight
+  // per round, each lane still summing its chunks j, j + 64, ... in ascending order
   for (int c0 = j + 64 * U; c0 < nchunks; c0 += 64 * U) {
     float2 w[U];
 #pragma unroll
@@ -151,6 +150,62 @@ __global__ void __launch_bounds__(64) gn_finalize_kernel(const float2* __restric
     if (var < 0) var = 0;
     stats[img * groups + g] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
   }
+}
+
+// The same fold for the long partial lists of large images (nchunks > 1024: the producer-epilogue partials of the
+// VAE's 512^2 / 1024^2 levels, HW / 128 up to 8192): 1024 threads per (group, image), thread j summing chunks j,
+// j + 1024, ... (all in flight) in fp64, a butterfly per wave, then the 16 wave sums in wave order.  Fixed order
+// (bitwise reproducible); replaces gn_finalize_kernel's serial 1024-chunk rounds (~12 us per VAE GroupNorm).
+__global__ void __launch_bounds__(1024) gn_finalize_wide_kernel(const float2* __restrict__ part,
+                                                                float2* __restrict__ stats, int HW, int C, int groups,
+                                                                int nchunks, float eps) {
+  __shared__ double red[2][16];
+  const int g = blockIdx.x, img = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const float2* p = part + (long long)img * nchunks * groups + g;
+  constexpr int U = 8;  // nchunks <= 8192
+  float2 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int c = t + 1024 * u;
+    v[u] = c < nchunks ? p[(long long)c * groups] : make_float2(0.f, 0.f);
+  }
+  double s = 0.0, q = 0.0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    s += v[u].x;
+    q += v[u].y;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    q += __shfl_xor(q, o, 64);
+  }
+  if (lane == 0) {
+    red[0][w] = s;
+    red[1][w] = q;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double S = 0.0, Q = 0.0;
+    for (int i = 0; i < 16; ++i) {
+      S += red[0][i];
+      Q += red[1][i];
+    }
+    const double n = (double)HW * (C / groups);
+    const double mean = S / n;
+    double var = Q / n - mean * mean;
+    if (var < 0) var = 0;
+    stats[img * groups + g] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+  }
+}
+
+static void gn_finalize_launch(const float2* part, float2* stats, int nimg, int HW, int C, int groups, int nchunks,
+                               float eps, hipStream_t s) {
+  if (nchunks > 1024 && nchunks <= 8192)
+    hipLaunchKernelGGL(gn_finalize_wide_kernel, dim3(groups, nimg), dim3(1024), 0, s, part, stats, HW, C, groups,
+                       nchunks, eps);
+  else
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, nimg), dim3(64), 0, s, part, stats, HW, C, groups, nchunks,
+                       eps);
 }
 
 template <typename T, int NV, int U = 4>
@@ -330,8 +385,7 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
   }
   FD_LAUNCH_CHECK();
   float2* stats = (float2*)ws + (long long)nimg * nch * groups;
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)ws, stats, HW, C, groups,
-                     nch, eps);
+  gn_finalize_launch((const float2*)ws, stats, nimg, HW, C, groups, nch, eps, s);
   FD_LAUNCH_CHECK();
   return gn_apply_launch(x, y, stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s);
 }
@@ -348,8 +402,7 @@ extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma
       C > GN_MAXC)
     return FD_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)part, (float2*)stats, HW,
-                     C, groups, HW / part_rows, eps);
+  gn_finalize_launch((const float2*)part, (float2*)stats, nimg, HW, C, groups, HW / part_rows, eps, s);
   FD_LAUNCH_CHECK();
   return gn_apply_launch(x, y, (const float2*)stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s);
 }

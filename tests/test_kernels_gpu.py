@@ -402,6 +402,7 @@ def test_flash_attn_d512(dtype, n, T):
     (2, 128, 128, 128, 256, False, True),   # gemm256, two images
     (1, 256, 256, 128, 128, False, True),   # gemm8 256x128, cpg 4 (chunks straddle groups)
     (1, 512, 512, 128, 128, False, True),   # 128-channel conv on a 512^2 image (4-wave 128x128 under FD_GEMM8_N128=1)
+    (1, 1024, 1024, 128, 128, False, True),  # the VAE decoder's 1024^2 level: 4096 partial blocks (wide finalize)
     (2, 128, 128, 320, 320, False, True),   # gemm8 256x160 (the UNet's 128^2 level), cpg 10
     (2, 64, 64, 640, 640, False, None),     # the 64^2 level, cpg 20 (256x160 when the planner takes it)
     (2, 16, 16, 320, 320, False, None),     # small M: whichever tile the planner picks
