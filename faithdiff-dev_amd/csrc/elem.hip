@@ -288,6 +288,92 @@ extern "C" int fd_conv2d_direct(const void* x, const float* w, const float* bias
 }
 
 // ------------------------------------------------------------------------------------------------
+// Narrow 3x3 conv (Cout <= 4, stride 1, pad 1, Cin % 32 == 0): the VAE decoder's conv_out (128 -> 3 at 1024^2),
+// which the implicit-GEMM tiles run at 3 of 64 columns while gathering every input element 9 times (285 us,
+// profiles/r03_vae_pmc_kernel_stats.csv).  One workgroup = 64 consecutive output pixels of one row: the 3 x 66-pixel
+// x Cin input halo is staged once in LDS (pixel pitch Cin + 8 elements: lane-consecutive pixels fall on
+// consecutive 16-B bank groups, conflict-free ds_read_b128); wave w sums channels [w Cin/4, (w+1) Cin/4) of the 9
+// taps for the 64 pixels (lane = pixel) against wave-uniform fp32 weights (scalar loads), and the 4 partial sums
+// are added in wave order.  fp32 accumulation; a different summation order than the GEMM path.
+template <typename T, typename TO>
+__global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                             const float* __restrict__ bias, TO* __restrict__ y,
+                                                             int nimg, int H, int W, int Cin, int Cout) {
+  typedef typename VecT<T>::v8 V8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char nsm[];
+  const int PP = Cin + 8;  // halo pixel pitch (elements)
+  T* halo = (T*)nsm;
+  float* red = (float*)(nsm + (size_t)3 * 66 * PP * sizeof(T));
+  const int tpr = (W + 63) / 64;
+  const long long rowid = blockIdx.x / tpr;  // img * H + oy
+  const int x0 = (blockIdx.x - (int)(rowid * tpr)) * 64;
+  const int oy = (int)(rowid % H);
+  const long long img = rowid / H;
+  const int VPP = Cin / 8;
+  for (int e = threadIdx.x; e < 3 * 66 * VPP; e += 256) {
+    const int v = e % VPP, pp = e / VPP, col = pp % 66, r = pp / 66;
+    const int iy = oy - 1 + r, ix = x0 - 1 + col;
+    V8 val;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      val = *(const V8*)(x + ((img * H + iy) * W + ix) * Cin + v * 8);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) val[i] = (T)0.f;
+    }
+    *(V8*)(halo + pp * PP + v * 8) = val;
+  }
+  __syncthreads();
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int cpw = Cin / 4, c0 = wv * cpw;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int tap = 0; tap < 9; ++tap) {
+    const T* hp = halo + ((tap / 3) * 66 + lane + tap % 3) * PP + c0;
+    const float* wt = w + tap * Cin + c0;
+    for (int cv = 0; cv < cpw; cv += 8) {
+      const V8 xv = *(const V8*)(hp + cv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float f = (float)xv[i];
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          if (n < Cout) acc[n] = __builtin_fmaf(f, wt[(long long)n * 9 * Cin + cv + i], acc[n]);
+      }
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < 4; ++n) red[(wv * 64 + lane) * 4 + n] = acc[n];
+  __syncthreads();
+  if (wv == 0 && x0 + lane < W) {
+    TO* yp = y + (rowid * W + x0 + lane) * Cout;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      if (n < Cout) {
+        const float s = ((red[lane * 4 + n] + red[(64 + lane) * 4 + n]) + red[(128 + lane) * 4 + n]) +
+                        red[(192 + lane) * 4 + n];
+        yp[n] = (TO)(s + (bias ? bias[n] : 0.f));
+      }
+  }
+}
+
+extern "C" int fd_conv3x3_narrow(const void* x, const float* w, const float* bias, void* y, int nimg, int H, int W,
+                                 int Cin, int Cout, int dtype, int out_dtype, void* stream) {
+  if (!x || !w || !y) return FD_ERR_ARG;
+  if (nimg <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cin % 32 || Cout <= 0 || Cout > 4)
+    return FD_ERR_SHAPE;
+  if (((unsigned long long)x) & 15) return FD_ERR_ARG;  // 16-B vector loads of the input rows
+  const long long nblk = (long long)nimg * H * ((W + 63) / 64);
+  if (nblk > 0x7fffffff) return FD_ERR_SHAPE;
+  const size_t lds = (size_t)3 * 66 * (Cin + 8) * 2 + 256 * 4 * sizeof(float);
+  if (lds > 64 * 1024) return FD_ERR_SHAPE;  // dynamic LDS within the default 64 KB (Cin <= 152)
+  hipStream_t s = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv3x3_narrow_kernel<T, TO>), dim3((unsigned)nblk),
+                                                                   dim3(256), lds, s, (const T*)x, w, bias, (TO*)y,
+                                                                   nimg, H, W, Cin, Cout)));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
 // SDXL time features (diffusers get_timestep_embedding: half = dim/2, exponent = -ln(1e4) * i / half,
 // emb = [cos, sin] after flip_sin_to_cos).
 __device__ __forceinline__ float sinus_feat(float t, int i, int dim) {

@@ -434,6 +434,21 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
     return out
 
 
+def conv3x3_narrow(x, w32, bias, nimg, H, W, out_dtype=None, out=None):
+    """3x3 conv (stride 1, pad 1) with Cout <= 4 on NHWC x [nimg*H*W, Cin]: w32 fp32 [Cout, 9*Cin] (tap-major, the
+    pack_conv3x3 layout).  The VAE decoder's conv_out."""
+    Cout, K = w32.shape
+    Cin = K // 9
+    odt = out_dtype or x.dtype
+    if out is None:
+        out = torch.empty((nimg * H * W, Cout), dtype=odt, device=x.device)
+    _timed("conv_narrow", 2.0 * nimg * H * W * Cout * K, 0.0, label=f"conv3x3_narrow M={nimg * H * W} N={Cout} K={K}",
+           launch=lambda: L.check(L.load().fd_conv3x3_narrow(L.ptr(x), L.ptr(w32), L.ptr(bias), L.ptr(out), nimg, H,
+                                                             W, Cin, Cout, L.dtype_code(x.dtype), L.dtype_code(odt),
+                                                             L.stream()), "fd_conv3x3_narrow"))
+    return out
+
+
 def conv_direct(x, w, bias, nimg, H, W, Cin, ksize=3, stride=1, pad=1, in_scale=1.0, out_dtype=None, out=None):
     """Direct conv for Cin < 64: x NHWC, w fp32 [Cout, k, k, Cin]."""
     Cout = w.shape[0]

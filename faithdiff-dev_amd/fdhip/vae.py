@@ -8,6 +8,8 @@ next conv's gather, mid-block single-head d=512 attention with residual.
 The d=512 mid-block attention runs as one flash kernel (fd_flash_attn_d512: online softmax in fp32, QK^T and PV on
 the MFMA, K / V tiles staged through LDS), so no [T, T] score / probability buffer (1.5 GB at T = 16384) exists.
 """
+import os
+
 import torch
 
 from . import arch
@@ -174,6 +176,11 @@ class HipDecoder:
             prev = c
         self.norm_out = (t.f32("decoder.conv_norm_out.weight"), t.f32("decoder.conv_norm_out.bias"))
         self.conv_out = t.conv("decoder.conv_out")
+        # conv_out (128 -> 3) on the direct narrow-N kernel (fd_conv3x3_narrow) with fp32 weights; FD_VAE_NARROW=0:
+        # the implicit-GEMM path (A/B)
+        self.narrow = os.environ.get("FD_VAE_NARROW", "1") != "0"
+        self.conv_out32 = (ops.pack_conv3x3(t.sd[t.prefix + "decoder.conv_out.weight"]).float().to(self.device),
+                           self.conv_out[1])
         self.graphs = GraphCache()
 
     def decode_graphed(self, z, n, h, w):
@@ -196,4 +203,6 @@ class HipDecoder:
                 x = ops.conv3x3(x, *us, n, hh, ww, upsample=True, gn=st)
                 hh, ww = hh * 2, ww * 2
         x = ops.group_norm(x, *self.norm_out, n, hh * ww, 128, 32, 1e-6, silu=True, stats=st)
+        if self.narrow:
+            return ops.conv3x3_narrow(x, *self.conv_out32, n, hh, ww)
         return ops.conv3x3(x, *self.conv_out, n, hh, ww)

@@ -150,6 +150,24 @@ def test_conv3x3(dtype, nimg, H, W, Cin, Cout, stride, pad, up):
     assert rel_l2(out, ref) < TOL[dtype], rel_l2(out, ref)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("nimg,H,W,Cin,Cout", [(1, 1024, 1024, 128, 3), (2, 37, 100, 128, 3), (1, 64, 64, 32, 4),
+                                               (1, 17, 130, 64, 1), (2, 8, 8, 128, 2)])
+def test_conv3x3_narrow(dtype, nimg, H, W, Cin, Cout):
+    """fd_conv3x3_narrow (the VAE decoder's conv_out, 128 -> 3 at 1024^2) vs torch conv2d in fp32 on the same
+    values, incl. row tails (W % 64 != 0) and image borders; and vs the implicit-GEMM conv it replaces."""
+    from fdhip import ops
+    x = rnd(nimg * H * W, Cin, dtype=dtype)
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV) / math.sqrt(9 * Cin)
+    b = torch.randn(Cout, device=DEV) * 0.1
+    out = ops.conv3x3_narrow(x, ops.pack_conv3x3(w).float(), b, nimg, H, W)
+    ref = conv_ref(x, w, b, nimg, H, W, 1, 1)
+    assert out.dtype == dtype and out.shape == (nimg * H * W, Cout)
+    assert rel_l2(out, ref) < TOL[dtype]
+    gemm = ops.conv3x3(x, ops.pack_conv3x3(w.to(dtype)), b, nimg, H, W)
+    assert rel_l2(out, gemm) < 2 * TOL[dtype]
+
+
 def test_conv3x3_concat_temb_residual():
     from fdhip import ops
     nimg, H, W, C1, C2, Cout = 2, 32, 32, 1280, 640, 1280
