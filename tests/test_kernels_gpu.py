@@ -164,8 +164,9 @@ def test_conv3x3_narrow(dtype, nimg, H, W, Cin, Cout):
     ref = conv_ref(x, w, b, nimg, H, W, 1, 1)
     assert out.dtype == dtype and out.shape == (nimg * H * W, Cout)
     assert rel_l2(out, ref) < TOL[dtype]
-    gemm = ops.conv3x3(x, ops.pack_conv3x3(w.to(dtype)), b, nimg, H, W)
-    assert rel_l2(out, gemm) < 2 * TOL[dtype]
+    if Cin % 64 == 0:  # the implicit-GEMM conv needs Cin % 64 == 0
+        gemm = ops.conv3x3(x, ops.pack_conv3x3(w.to(dtype)), b, nimg, H, W)
+        assert rel_l2(out, gemm) < 2 * TOL[dtype]
 
 
 def test_conv3x3_concat_temb_residual():
