@@ -295,27 +295,25 @@ extern "C" int fd_conv2d_direct(const void* x, const float* w, const float* bias
 // consecutive 16-B bank groups, conflict-free ds_read_b128); wave w sums channels [w Cin/4, (w+1) Cin/4) of the 9
 // taps for the 64 pixels (lane = pixel) against wave-uniform fp32 weights (scalar loads), and the 4 partial sums
 // are added in wave order.  fp32 accumulation; a different summation order than the GEMM path.
-template <typename T, typename TO>
+template <typename T, typename TO, int CIN, int NOUT>
 __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                              const float* __restrict__ bias, TO* __restrict__ y,
-                                                             int nimg, int H, int W, int Cin, int Cout) {
+                                                             int nimg, int H, int W) {
   typedef typename VecT<T>::v8 V8;
-  extern __shared__ __attribute__((aligned(16))) unsigned char nsm[];
-  const int PP = Cin + 8;  // halo pixel pitch (elements)
-  T* halo = (T*)nsm;
-  float* red = (float*)(nsm + (size_t)3 * 66 * PP * sizeof(T));
+  constexpr int PP = CIN + 8, VPP = CIN / 8, CPW = CIN / 4;  // halo pixel pitch (elements), channels per wave
+  __shared__ __attribute__((aligned(16))) T halo[3 * 66 * PP];
+  __shared__ float red[256 * 4];
   const int tpr = (W + 63) / 64;
   const long long rowid = blockIdx.x / tpr;  // img * H + oy
   const int x0 = (blockIdx.x - (int)(rowid * tpr)) * 64;
   const int oy = (int)(rowid % H);
   const long long img = rowid / H;
-  const int VPP = Cin / 8;
   for (int e = threadIdx.x; e < 3 * 66 * VPP; e += 256) {
     const int v = e % VPP, pp = e / VPP, col = pp % 66, r = pp / 66;
     const int iy = oy - 1 + r, ix = x0 - 1 + col;
     V8 val;
     if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-      val = *(const V8*)(x + ((img * H + iy) * W + ix) * Cin + v * 8);
+      val = *(const V8*)(x + ((img * H + iy) * W + ix) * CIN + v * 8);
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) val[i] = (T)0.f;
@@ -324,51 +322,71 @@ __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const T* __restrict
   }
   __syncthreads();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int cpw = Cin / 4, c0 = wv * cpw;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  // the wave's weights: a wave-uniform base + compile-time offsets -> scalar loads (SGPR operands of the FMAs)
+  const float* __restrict__ wb = w + wv * CPW;
+  float acc[NOUT];
+#pragma unroll
+  for (int n = 0; n < NOUT; ++n) acc[n] = 0.f;
+#pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
-    const T* hp = halo + ((tap / 3) * 66 + lane + tap % 3) * PP + c0;
-    const float* wt = w + tap * Cin + c0;
-    for (int cv = 0; cv < cpw; cv += 8) {
+    const T* hp = halo + ((tap / 3) * 66 + lane + tap % 3) * PP + wv * CPW;
+#pragma unroll
+    for (int cv = 0; cv < CPW; cv += 8) {
       const V8 xv = *(const V8*)(hp + cv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float f = (float)xv[i];
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
-          if (n < Cout) acc[n] = __builtin_fmaf(f, wt[(long long)n * 9 * Cin + cv + i], acc[n]);
+        for (int n = 0; n < NOUT; ++n) acc[n] = __builtin_fmaf(f, wb[n * 9 * CIN + tap * CIN + cv + i], acc[n]);
       }
     }
   }
 #pragma unroll
-  for (int n = 0; n < 4; ++n) red[(wv * 64 + lane) * 4 + n] = acc[n];
+  for (int n = 0; n < NOUT; ++n) red[(wv * 64 + lane) * 4 + n] = acc[n];
   __syncthreads();
   if (wv == 0 && x0 + lane < W) {
-    TO* yp = y + (rowid * W + x0 + lane) * Cout;
+    TO* yp = y + (rowid * W + x0 + lane) * NOUT;
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-      if (n < Cout) {
-        const float s = ((red[lane * 4 + n] + red[(64 + lane) * 4 + n]) + red[(128 + lane) * 4 + n]) +
+    for (int n = 0; n < NOUT; ++n) {
+      const float sum = ((red[lane * 4 + n] + red[(64 + lane) * 4 + n]) + red[(128 + lane) * 4 + n]) +
                         red[(192 + lane) * 4 + n];
-        yp[n] = (TO)(s + (bias ? bias[n] : 0.f));
-      }
+      yp[n] = (TO)(sum + (bias ? bias[n] : 0.f));
+    }
   }
 }
 
 extern "C" int fd_conv3x3_narrow(const void* x, const float* w, const float* bias, void* y, int nimg, int H, int W,
                                  int Cin, int Cout, int dtype, int out_dtype, void* stream) {
   if (!x || !w || !y) return FD_ERR_ARG;
-  if (nimg <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cin % 32 || Cout <= 0 || Cout > 4)
-    return FD_ERR_SHAPE;
+  if (nimg <= 0 || H <= 0 || W <= 0) return FD_ERR_SHAPE;
   if (((unsigned long long)x) & 15) return FD_ERR_ARG;  // 16-B vector loads of the input rows
   const long long nblk = (long long)nimg * H * ((W + 63) / 64);
   if (nblk > 0x7fffffff) return FD_ERR_SHAPE;
-  const size_t lds = (size_t)3 * 66 * (Cin + 8) * 2 + 256 * 4 * sizeof(float);
-  if (lds > 64 * 1024) return FD_ERR_SHAPE;  // dynamic LDS within the default 64 KB (Cin <= 152)
   hipStream_t s = (hipStream_t)stream;
-  FD_DISPATCH_T(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv3x3_narrow_kernel<T, TO>), dim3((unsigned)nblk),
-                                                                   dim3(256), lds, s, (const T*)x, w, bias, (TO*)y,
-                                                                   nimg, H, W, Cin, Cout)));
+  dim3 g((unsigned)nblk), b(256);
+  // instances: Cin 32 / 64 / 128 (the decoder's conv_out is 128 -> 3), Cout 1..4
+#define FD_NARROW(CI, NO)                                                                                          \
+  FD_DISPATCH_T(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv3x3_narrow_kernel<T, TO, CI, NO>), g, b, 0, s, \
+                                                                   (const T*)x, w, bias, (TO*)y, nimg, H, W)))
+#define FD_NARROW_N(CI)                  \
+  switch (Cout) {                        \
+    case 1: FD_NARROW(CI, 1); break;     \
+    case 2: FD_NARROW(CI, 2); break;     \
+    case 3: FD_NARROW(CI, 3); break;     \
+    case 4: FD_NARROW(CI, 4); break;     \
+    default: return FD_ERR_SHAPE;        \
+  }
+  if (Cin == 128) {
+    FD_NARROW_N(128)
+  } else if (Cin == 64) {
+    FD_NARROW_N(64)
+  } else if (Cin == 32) {
+    FD_NARROW_N(32)
+  } else {
+    return FD_ERR_SHAPE;
+  }
+#undef FD_NARROW_N
+#undef FD_NARROW
   FD_LAUNCH_CHECK();
   return FD_OK;
 }

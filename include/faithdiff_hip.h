@@ -117,8 +117,8 @@ int fd_conv2d_direct(const void* x, const float* w, const float* bias, void* y, 
                      int Cin, int Cout, int ksize, int stride, int pad, float in_scale, int dtype, int out_dtype,
                      void* stream);
 
-/* 3x3 conv, stride 1, pad 1, with few output channels (Cout <= 4, Cin % 32 == 0): the VAE
- * decoder's conv_out (128 -> 3); Cin <= 152 (the input halo in 64 KB of LDS).  x NHWC (dtype bf16 / f16), w fp32
+/* 3x3 conv, stride 1, pad 1, with few output channels (Cout <= 4, Cin in {32, 64, 128}): the VAE
+ * decoder's conv_out (128 -> 3).  x NHWC (dtype bf16 / f16), w fp32
  * [Cout][3][3][Cin] (tap-major like the GEMM's
  * packed conv weights), bias fp32, y NHWC [.., Cout] (out_dtype).  fp32 accumulation, direct (no im2col).
  * Replaces: cuDNN conv2d of decoder.conv_out (diffusers Decoder; pipeline_FaithDiff_tlc.py:1438). */
