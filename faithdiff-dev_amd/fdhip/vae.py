@@ -176,9 +176,11 @@ class HipDecoder:
             prev = c
         self.norm_out = (t.f32("decoder.conv_norm_out.weight"), t.f32("decoder.conv_norm_out.bias"))
         self.conv_out = t.conv("decoder.conv_out")
-        # conv_out (128 -> 3) on the direct narrow-N kernel (fd_conv3x3_narrow) with fp32 weights; FD_VAE_NARROW=0:
-        # the implicit-GEMM path (A/B)
-        self.narrow = os.environ.get("FD_VAE_NARROW", "1") != "0"
+        # conv_out (128 -> 3) on the direct narrow-N kernel (fd_conv3x3_narrow, fp32 weights) with FD_VAE_NARROW=1;
+        # by default the implicit-GEMM path: on one box the decode measured 15.28 / 15.30 ms narrow vs 15.24 / 15.26 ms
+        # GEMM (profiles/r03_vae_narrow_ab.txt) -- the direct kernel reads the input once but at two workgroups per
+        # CU it is latency-bound at the same ~0.3 ms
+        self.narrow = os.environ.get("FD_VAE_NARROW", "0") == "1"
         self.conv_out32 = (ops.pack_conv3x3(t.sd[t.prefix + "decoder.conv_out.weight"]).float().to(self.device),
                            self.conv_out[1])
         self.graphs = GraphCache()
