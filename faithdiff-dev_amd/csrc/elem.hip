@@ -288,109 +288,70 @@ extern "C" int fd_conv2d_direct(const void* x, const float* w, const float* bias
 }
 
 // ------------------------------------------------------------------------------------------------
-// Narrow 3x3 conv (Cout <= 4, stride 1, pad 1, Cin in {32, 64, 128}): the VAE decoder's conv_out (128 -> 3 at 1024^2),
+// Narrow 3x3 conv (Cout <= 4, stride 1, pad 1, Cin % 32 == 0): the VAE decoder's conv_out (128 -> 3 at 1024^2),
 // which the implicit-GEMM tiles run at 3 of 64 columns while gathering every input element 9 times (285 us,
-// profiles/r03_vae_pmc_kernel_stats.csv).  Input rows of a 66-pixel strip live in LDS (pixel pitch Cin + 8
-// elements: lane-consecutive pixels fall on consecutive 16-B bank groups, conflict-free ds_read_b128); wave w sums
-// channels [w Cin/4, (w+1) Cin/4) of the 9 taps for 64 pixels (lane = pixel) against wave-uniform fp32 weights
-// (scalar loads), and the 4 partial sums are added in wave order.  fp32 accumulation; a different summation order
-// than the GEMM path.
-template <typename T, typename TO, int CIN, int NOUT, int ROWS>
+// profiles/r03_vae_pmc_kernel_stats.csv).  One workgroup = 64 consecutive output pixels of one row: the 3 x 66-pixel
+// x Cin input halo is staged once in LDS (pixel pitch Cin + 8 elements: lane-consecutive pixels fall on
+// consecutive 16-B bank groups, conflict-free ds_read_b128); wave w sums channels [w Cin/4, (w+1) Cin/4) of the 9
+// taps for the 64 pixels (lane = pixel) against wave-uniform fp32 weights (scalar loads), and the 4 partial sums
+// are added in wave order.  fp32 accumulation; a different summation order than the GEMM path.
+template <typename T, typename TO, int CIN, int NOUT>
 __global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                              const float* __restrict__ bias, TO* __restrict__ y,
                                                              int nimg, int H, int W) {
-  // One workgroup = a 64-pixel-wide strip of ROWS output rows, walked top to bottom over a 4-slot LDS ring of input
-  // rows (3 in use, the next one loaded through registers while the current row is computed): each input row is
-  // read from memory once per strip instead of three times.
   typedef typename VecT<T>::v8 V8;
-  constexpr int PP = CIN + 8, VPP = CIN / 8, CPW = CIN / 4;  // pixel pitch (elements), channels per wave
-  constexpr int RV = 66 * VPP;                                // 16-B vectors per input row of the strip
-  constexpr int VT = (RV + 255) / 256;                        // ... per thread
-  __shared__ __attribute__((aligned(16))) T ring[4][66 * PP];
+  constexpr int PP = CIN + 8, VPP = CIN / 8, CPW = CIN / 4;  // halo pixel pitch (elements), channels per wave
+  __shared__ __attribute__((aligned(16))) T halo[3 * 66 * PP];
   __shared__ float red[256 * 4];
-  const int tpr = (W + 63) / 64, rbk = (H + ROWS - 1) / ROWS;
-  const int xs = blockIdx.x % tpr;
-  const int t2 = blockIdx.x / tpr;
-  const int y0 = (t2 % rbk) * ROWS;
-  const long long img = t2 / rbk;
-  const int x0 = xs * 64;
-  auto fetch = [&](int iy, V8 (&v)[VT]) {  // input row iy of the strip (cols x0 - 1 .. x0 + 64), zero outside
+  const int tpr = (W + 63) / 64;
+  const long long rowid = blockIdx.x / tpr;  // img * H + oy
+  const int x0 = (blockIdx.x - (int)(rowid * tpr)) * 64;
+  const int oy = (int)(rowid % H);
+  const long long img = rowid / H;
+  for (int e = threadIdx.x; e < 3 * 66 * VPP; e += 256) {
+    const int v = e % VPP, pp = e / VPP, col = pp % 66, r = pp / 66;
+    const int iy = oy - 1 + r, ix = x0 - 1 + col;
+    V8 val;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      val = *(const V8*)(x + ((img * H + iy) * W + ix) * CIN + v * 8);
+    } else {
 #pragma unroll
-    for (int k = 0; k < VT; ++k) {
-      const int e = threadIdx.x + k * 256;
-      const int col = e / VPP, vv = e - col * VPP, ix = x0 - 1 + col;
-      if (e < RV && iy >= 0 && iy < H && ix >= 0 && ix < W) {
-        v[k] = *(const V8*)(x + ((img * H + iy) * W + ix) * CIN + vv * 8);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[k][i] = (T)0.f;
-      }
+      for (int i = 0; i < 8; ++i) val[i] = (T)0.f;
     }
-  };
-  auto put = [&](int slot, const V8 (&v)[VT]) {
-#pragma unroll
-    for (int k = 0; k < VT; ++k) {
-      const int e = threadIdx.x + k * 256;
-      if (e < RV) {
-        const int col = e / VPP, vv = e - col * VPP;
-        *(V8*)(&ring[slot][col * PP + vv * 8]) = v[k];
-      }
-    }
-  };
-  V8 nv[VT];
-  fetch(y0 - 1, nv);
-  put(0, nv);
-  fetch(y0, nv);
-  put(1, nv);
-  fetch(y0 + 1, nv);
-  put(2, nv);
+    *(V8*)(halo + pp * PP + v * 8) = val;
+  }
   __syncthreads();
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const float* __restrict__ wb = w + wv * CPW;  // wave-uniform base + compile-time offsets -> scalar loads
-  const int nrows = min(ROWS, H - y0);
-  for (int r = 0; r < nrows; ++r) {
-    const bool more = r + 1 < nrows;
-    if (more) fetch(y0 + r + 2, nv);  // in flight under this row's FMAs
-    // re-read the weights every row (scalar-cache hits): hoisted out of the row loop they are 9 * Cin / 4 * NOUT SGPRs
-    // per wave, which spilled
-    const float* wr = wb;
-    asm volatile("" : "+s"(wr));
-    float acc[NOUT];
+  // the wave's weights: a wave-uniform base + compile-time offsets -> scalar loads (SGPR operands of the FMAs)
+  const float* __restrict__ wb = w + wv * CPW;
+  float acc[NOUT];
 #pragma unroll
-    for (int n = 0; n < NOUT; ++n) acc[n] = 0.f;
+  for (int n = 0; n < NOUT; ++n) acc[n] = 0.f;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const T* rowp = &ring[(r + ky) & 3][0];
+  for (int tap = 0; tap < 9; ++tap) {
+    const T* hp = halo + ((tap / 3) * 66 + lane + tap % 3) * PP + wv * CPW;
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int tap = ky * 3 + kx;
-        const T* hp = rowp + (lane + kx) * PP + wv * CPW;
+    for (int cv = 0; cv < CPW; cv += 8) {
+      const V8 xv = *(const V8*)(hp + cv);
 #pragma unroll
-        for (int cv = 0; cv < CPW; cv += 8) {
-          const V8 xv = *(const V8*)(hp + cv);
+      for (int i = 0; i < 8; ++i) {
+        const float f = (float)xv[i];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float f = (float)xv[i];
-#pragma unroll
-            for (int n = 0; n < NOUT; ++n) acc[n] = __builtin_fmaf(f, wr[n * 9 * CIN + tap * CIN + cv + i], acc[n]);
-          }
-        }
+        for (int n = 0; n < NOUT; ++n) acc[n] = __builtin_fmaf(f, wb[n * 9 * CIN + tap * CIN + cv + i], acc[n]);
       }
     }
+  }
 #pragma unroll
-    for (int n = 0; n < NOUT; ++n) red[(wv * 64 + lane) * 4 + n] = acc[n];
-    if (more) put((r + 3) & 3, nv);  // the slot of row r - 1, no longer read
-    __syncthreads();
-    if (wv == 0 && x0 + lane < W) {
-      TO* yp = y + ((img * H + y0 + r) * W + x0 + lane) * NOUT;
+  for (int n = 0; n < NOUT; ++n) red[(wv * 64 + lane) * 4 + n] = acc[n];
+  __syncthreads();
+  if (wv == 0 && x0 + lane < W) {
+    TO* yp = y + (rowid * W + x0 + lane) * NOUT;
 #pragma unroll
-      for (int n = 0; n < NOUT; ++n) {
-        const float sum = ((red[lane * 4 + n] + red[(64 + lane) * 4 + n]) + red[(128 + lane) * 4 + n]) +
-                          red[(192 + lane) * 4 + n];
-        yp[n] = (TO)(sum + (bias ? bias[n] : 0.f));
-      }
+    for (int n = 0; n < NOUT; ++n) {
+      const float sum = ((red[lane * 4 + n] + red[(64 + lane) * 4 + n]) + red[(128 + lane) * 4 + n]) +
+                        red[(192 + lane) * 4 + n];
+      yp[n] = (TO)(sum + (bias ? bias[n] : 0.f));
     }
-    __syncthreads();  // red and the ring slot of row r free again
   }
 }
 
@@ -399,14 +360,13 @@ extern "C" int fd_conv3x3_narrow(const void* x, const float* w, const float* bia
   if (!x || !w || !y) return FD_ERR_ARG;
   if (nimg <= 0 || H <= 0 || W <= 0) return FD_ERR_SHAPE;
   if (((unsigned long long)x) & 15) return FD_ERR_ARG;  // 16-B vector loads of the input rows
-  constexpr int ROWS = 32;  // output rows per workgroup (1024^2: 16 strips x 32 row blocks = 512 workgroups)
-  const long long nblk = (long long)nimg * ((H + ROWS - 1) / ROWS) * ((W + 63) / 64);
+  const long long nblk = (long long)nimg * H * ((W + 63) / 64);
   if (nblk > 0x7fffffff) return FD_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   dim3 g((unsigned)nblk), b(256);
   // instances: Cin 32 / 64 / 128 (the decoder's conv_out is 128 -> 3), Cout 1..4
 #define FD_NARROW(CI, NO)                                                                                          \
-  FD_DISPATCH_T(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv3x3_narrow_kernel<T, TO, CI, NO, ROWS>), g, b, 0, s, \
+  FD_DISPATCH_T(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv3x3_narrow_kernel<T, TO, CI, NO>), g, b, 0, s, \
                                                                    (const T*)x, w, bias, (TO*)y, nimg, H, W)))
 #define FD_NARROW_N(CI)                  \
   switch (Cout) {                        \
