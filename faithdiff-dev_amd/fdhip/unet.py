@@ -53,6 +53,10 @@ class HipUNet:
         # MX output straight from the GEGLU epilogue (forces 256 x 128 tiles; profiles/r03_f8_tiles_mx.jsonl: 48.1 vs
         # 39.7 + a 2048 x 5120 quantization for the 256 x 160 bf16 form); FD_FP8_MX_GEGLU=1 turns it on (A/B)
         self.fp8_mx_geglu = os.environ.get("FD_FP8_MX_GEGLU", "0") == "1"
+        # per-row form with MX only where it is free: flash attention writes its output as MX and the out-projections
+        # (K = C: the MX GEMM's speed, profiles/r03_f8_tiles_mx.jsonl) read it, removing the two activation
+        # quantization launches per block (FD_FP8_MX_ATTN=0: off, A/B)
+        self.fp8_mx_attn = self.fp8_mfma and not self.fp8_mx and os.environ.get("FD_FP8_MX_ATTN", "1") != "0"
         self.device, self.dtype = torch.device(device), dtype
         f32 = torch.float32
         W = lambda k: _dev(sd[k], self.device, dtype)  # noqa: E731
@@ -278,6 +282,7 @@ class HipUNet:
         h = lin(h, t["pin"][0], bias=t["pin"][1])
         qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
         att = torch.empty((M, C), dtype=self.dtype, device=self.device)
+        att8 = ops.MX(M, C, self.device) if self.fp8_mx_attn else None
         if self.fp8_mfma:  # LayerNorm writes e4m3 rows + scales straight into the fp8 GEMM's A operand
             q8 = torch.empty((M, C), dtype=torch.uint8, device=self.device)
             s8 = torch.empty((M,), dtype=torch.float32, device=self.device)
@@ -293,12 +298,23 @@ class HipUNet:
                 return lin(n, w, bias=bias, out=out, act=act)
         for b in t["blocks"]:
             ln_lin(b["n1"], b["qkv"], out=qkv)
+            kv = self._kv[self._kv_row0:, b["kv_off"]:]  # [ncfg*77, ...] view; K at +0, V at +C, row stride kv_total
+            Lk, ldkv = self.Lk, self.kv_total
+            if att8 is not None:  # attention output as MX e4m3 -> MX out-projection GEMM (no quantization launch)
+                ops.flash_attn_mx(qkv, qkv[:, C:], qkv[:, 2 * C:], att8, B, heads, HW, HW, 3 * C, 3 * C, 3 * C,
+                                  HW * 3 * C, HW * 3 * C, HW * 3 * C, kv_mod=0, scale=0.125)
+                ops.gemm_mx(att8, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
+                ln_lin(b["n2"], b["q2"], out=qkv[:, :C])
+                ops.flash_attn_mx(qkv, kv, kv[:, C:], att8, B, heads, HW, Lk, 3 * C, ldkv, ldkv,
+                                  HW * 3 * C, Lk * ldkv, Lk * ldkv, kv_mod=self._kv_mod, scale=0.125)
+                ops.gemm_mx(att8, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
+                ff = ln_lin(b["n3"], b["ff1"][0], bias=b["ff1"][1], act="geglu")
+                lin(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
+                continue
             ops.flash_attn(qkv, qkv[:, C:], qkv[:, 2 * C:], att, B, heads, HW, HW, 3 * C, 3 * C, 3 * C, C,
                            HW * 3 * C, HW * 3 * C, HW * 3 * C, HW * C, kv_mod=0, scale=0.125)
             lin(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
             ln_lin(b["n2"], b["q2"], out=qkv[:, :C])  # row stride 3C (the view's)
-            kv = self._kv[self._kv_row0:, b["kv_off"]:]  # [ncfg*77, ...] view; K at +0, V at +C, row stride kv_total
-            Lk, ldkv = self.Lk, self.kv_total
             ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, ldkv, ldkv, C,
                            HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self._kv_mod, scale=0.125)
             lin(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
