@@ -55,8 +55,9 @@ class HipUNet:
         self.fp8_mx_geglu = os.environ.get("FD_FP8_MX_GEGLU", "0") == "1"
         # per-row form with MX only where it is free: flash attention writes its output as MX and the out-projections
         # (K = C: the MX GEMM's speed, profiles/r03_f8_tiles_mx.jsonl) read it, removing the two activation
-        # quantization launches per block (FD_FP8_MX_ATTN=1; A/B pending on hardware)
-        self.fp8_mx_attn = self.fp8_mfma and not self.fp8_mx and os.environ.get("FD_FP8_MX_ATTN", "0") == "1"
+        # quantization launches per block.  C2 step on one box, alternated: 20.57 / 20.57 ms vs 20.65 / 20.67 per-row
+        # everywhere vs 20.84 / 20.89 MX everywhere (profiles/r03_fp8_mxattn_ab_*.json).  FD_FP8_MX_ATTN=0: per-row
+        self.fp8_mx_attn = self.fp8_mfma and not self.fp8_mx and os.environ.get("FD_FP8_MX_ATTN", "1") != "0"
         self.device, self.dtype = torch.device(device), dtype
         f32 = torch.float32
         W = lambda k: _dev(sd[k], self.device, dtype)  # noqa: E731
