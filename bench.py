@@ -466,7 +466,8 @@ def roofline_leg(loop, fp8):
                                                 + tr["file"] + ")") if tr is not None and fp8 else
                                "no PMC pass committed for this workload",
                                "kernel": "gemm8_kernel on e4m3 operands (transformer Linears, e4m3 x e4m3 on "
-                                         "v_mfma_scale_f32_16x16x128_f8f6f4; MX block-scaled A unless FD_FP8_MX=0)",
+                                         "v_mfma_scale_f32_16x16x128_f8f6f4; per-row scaled activations, the "
+                                         "out-projections on MX block-scaled attention outputs)",
                                "launches": n_f, "algorithmic_flops": fl_f, "kernel_ms_per_forward": round(ms_f, 3)}
     flops = arch.unet_flops(loop.k, loop.k, loop.B, prompt_kv=False, cond_embed=False)
     res["forward_graph_ms"] = round(fam["_all"][3], 3)
