@@ -10,6 +10,7 @@ Bars (stated per test):
 import pytest
 import torch
 from parity import rel_l2  # noqa: E402  (records every measured value)
+from mx_ref import mx_ref  # noqa: E402  (host restatement of the MX e4m3 rule)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -207,21 +208,6 @@ def test_gemm_e4m3_eight_wave_bitwise_vs_four_wave(tile, M, N, K, act, out):
 
 
 # ---------------------------------------------------------------------------------------------- MX e4m3 (OCP MX)
-def mx_ref(x, K=None):
-    """Restatement of the MX rule (fd_common.h mx_exp / mx_pack4) on the host: per 32-element block,
-    E = least exponent with amax <= 448 * 2^E (amax = ma * 2^ea, ma in [1, 2): E = ea - 8 if ma <= 1.75 else ea - 7;
-    all-zero block E = 0), q = RNE_e4m3(x * 2^-E), scale byte = E + 127."""
-    x = x.float().cpu()
-    M, K = x.shape
-    xb = x.reshape(M, K // 32, 32)
-    amax = xb.abs().amax(-1)
-    m, e = torch.frexp(amax)  # amax = m * 2^e, m in [0.5, 1)
-    E = torch.where(2 * m <= 1.75, e - 1 - 8, e - 1 - 7)
-    E = torch.where(amax > 0, E, torch.zeros_like(E)).clamp(-127, 127)
-    q = e4m3((xb * torch.exp2(-E.float())[..., None]).reshape(M, K))
-    return q, (E + 127).to(torch.uint8)
-
-
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("M,K", [(1, 32), (77, 2048), (2048, 1280), (513, 5120), (6, 2080)])
 def test_quant_rows_mx_bitexact(dtype, M, K):
