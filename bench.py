@@ -376,15 +376,37 @@ def run_pipeline_image(pipe, img, H, W, steps, target, seed=42):
 
 
 def run_batch(pipe, imgs, prompts, size, steps, seed=42):
-    """One product pipe(lr_img=[...], prompt=[...]) call over several images (C5); returns its EventTimer."""
+    """One product pipe(lr_img=[...], prompt=[...]) call over several images (C5); returns its EventTimer, the
+    images and the final latents (a reference to the device tensor, kept by the step-end callback: no copy, no
+    sync inside the timed call).  check_batch() validates them outside the timed region."""
     tm = EventTimer()
     gen = torch.Generator(device=pipe.device).manual_seed(seed)
+    last = {}
+
+    def keep(p, i, t, k):
+        last["latents"] = k["latents"]
+        return {}
     tm("call_start", 0)
-    pipe(lr_img=imgs, prompt=prompts, negative_prompt="", num_inference_steps=steps, guidance_scale=5.0,
-         generator=gen, start_point="lr", height=size, width=size, overlap=0.5, target_size=(1024, 1024), timer=tm)
+    out = pipe(lr_img=imgs, prompt=prompts, negative_prompt="", num_inference_steps=steps, guidance_scale=5.0,
+               generator=gen, start_point="lr", height=size, width=size, overlap=0.5, target_size=(1024, 1024),
+               timer=tm, callback_on_step_end=keep).images
     tm("call_end", 0)
     torch.cuda.synchronize()
-    return tm
+    return tm, out, last.get("latents")
+
+
+def check_batch(out, latents, n):
+    """C5 output check: one image per input, final latents finite, no flat image (a NaN or a dropped image would
+    otherwise go unnoticed in the timed leg)."""
+    if len(out) != n or latents is None or latents.shape[0] != n:
+        raise RuntimeError(f"C5 batch: {len(out)} images / latents {None if latents is None else tuple(latents.shape)}"
+                           f" for {n} inputs")
+    if not bool(torch.isfinite(latents).all()):
+        raise RuntimeError("C5 batch: non-finite latents")
+    stds = [float(np.asarray(im, dtype=np.float32).std()) for im in out]
+    if min(stds) <= 1.0:
+        raise RuntimeError(f"C5 batch: flat output image (pixel std {min(stds):.3f})")
+    return stds
 
 
 def pipeline_leg(pipe, size, steps=20):
@@ -555,9 +577,10 @@ def main(argv=None):
         run_batch(pipe, imgs, prompts, args.size, 2)  # warm: captures the batched UNet / VAE graphs
         barrier(world)
         t0 = time.perf_counter()
-        tm = run_batch(pipe, imgs, prompts, args.size, args.c5_steps)
+        tm, out, lat = run_batch(pipe, imgs, prompts, args.size, args.c5_steps)
         barrier(world)
         t = max_over_ranks(time.perf_counter() - t0, world, dev)
+        stds = check_batch(out, lat, len(imgs))
         st = tm.step_ms()
         result.update({"metric": "C5 images/sec, 1024px 50-step, batch of 8 split over ranks",
                        "value": round(args.c5_images / t, 4), "unit": "images/s", "scaling": "strong",
@@ -569,7 +592,8 @@ def main(argv=None):
                                   "parallelism": f"replicas x{world}"},
                        "c5": {"s_total": round(t, 3), "loop_s": round(sum(st) / 1e3, 3),
                               "pre_loop_s": round(tm.span_ms("call_start", "loop_start") / 1e3, 3),
-                              "decode_s": round(tm.span_ms("decode_start", "decode") / 1e3, 3)}})
+                              "decode_s": round(tm.span_ms("decode_start", "decode") / 1e3, 3),
+                              "checked": {"latents_finite": True, "min_pixel_std": round(min(stds), 3)}}})
     else:
         loop = C2Loop(pipe, args.size, rank)
         for i in range(args.warmup):

@@ -122,7 +122,12 @@ class UNet2DConditionModel:
                 if k.startswith(p):
                     groups[p][k] = v
         for p, d in groups.items():
-            if not d or p == "agg_net.":
+            if not d:
+                continue
+            if p == "agg_net.":
+                # the reference's agg_net is an empty nn.ModuleList (ext:402-403): every key is unexpected
+                if strict:
+                    raise RuntimeError(f"Error(s) in loading state_dict for ModuleList: unexpected={sorted(d)[:5]}")
                 continue
             want = den_shapes if p == "denoise_encoder." else {k: s for k, s in ext_shapes.items() if k.startswith(p)}
             _check_keys(d, want, strict, p[:-1])

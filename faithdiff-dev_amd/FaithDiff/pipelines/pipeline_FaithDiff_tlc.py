@@ -405,15 +405,23 @@ class FaithDiffStableDiffusionXLPipeline:
                  target_size: Optional[Tuple[int, int]] = None, clip_skip: Optional[int] = None,
                  callback_on_step_end: Optional[Callable[[int, int, Dict], None]] = None,
                  callback_on_step_end_tensor_inputs: List[str] = ["latents"], add_sample: bool = True, **kwargs):
+        if num_images_per_prompt not in (None, 1):
+            # the reference's TLC loop restores one latent canvas per call (pipeline:1278-1409)
+            raise NotImplementedError("num_images_per_prompt > 1 is not supported by the TLC tile loop; pass a list "
+                                      "of images (lr_img=[...]) instead")
         if isinstance(lr_img, (list, tuple)) and len(lr_img) > 1:
-            return self._call_images(lr_img, prompt, height=height, width=width,
-                                     num_inference_steps=num_inference_steps, start_point=start_point,
-                                     timesteps=timesteps, denoising_end=denoising_end, overlap=overlap,
-                                     guidance_scale=guidance_scale, negative_prompt=negative_prompt,
-                                     generator=generator, latents=latents, output_type=output_type,
-                                     return_dict=return_dict, guidance_rescale=guidance_rescale,
-                                     original_size=original_size, target_size=target_size,
-                                     callback_on_step_end=callback_on_step_end, add_sample=add_sample, **kwargs)
+            return self._call_images(
+                lr_img, prompt, prompt_2=prompt_2, height=height, width=width,
+                num_inference_steps=num_inference_steps, start_point=start_point, timesteps=timesteps,
+                denoising_end=denoising_end, overlap=overlap, guidance_scale=guidance_scale,
+                negative_prompt=negative_prompt, negative_prompt_2=negative_prompt_2, generator=generator,
+                latents=latents, prompt_embeds=prompt_embeds, negative_prompt_embeds=negative_prompt_embeds,
+                pooled_prompt_embeds=pooled_prompt_embeds, negative_pooled_prompt_embeds=negative_pooled_prompt_embeds,
+                output_type=output_type, return_dict=return_dict, cross_attention_kwargs=cross_attention_kwargs,
+                guidance_rescale=guidance_rescale, original_size=original_size, target_size=target_size,
+                clip_skip=clip_skip, callback_on_step_end=callback_on_step_end,
+                callback_on_step_end_tensor_inputs=callback_on_step_end_tensor_inputs, add_sample=add_sample,
+                **kwargs)
         callback = kwargs.pop("callback", None)
         callback_steps = kwargs.pop("callback_steps", None)
         posterior_noise = kwargs.pop("posterior_noise", None)  # explicit VAE posterior draw (parity tests)
@@ -571,10 +579,13 @@ class FaithDiffStableDiffusionXLPipeline:
         return FaithDiffStableDiffusionXLPipelineOutput(images=image)
 
     @torch.no_grad()
-    def _call_images(self, imgs, prompt, height=None, width=None, num_inference_steps=50, start_point="noise",
-                     timesteps=None, denoising_end=None, overlap=0.5, guidance_scale=5.0, negative_prompt=None,
-                     generator=None, latents=None, output_type="pil", return_dict=True, guidance_rescale=0.0,
-                     original_size=None, target_size=None, callback_on_step_end=None, add_sample=True, **kwargs):
+    def _call_images(self, imgs, prompt, prompt_2=None, height=None, width=None, num_inference_steps=50,
+                     start_point="noise", timesteps=None, denoising_end=None, overlap=0.5, guidance_scale=5.0,
+                     negative_prompt=None, negative_prompt_2=None, generator=None, latents=None, prompt_embeds=None,
+                     negative_prompt_embeds=None, pooled_prompt_embeds=None, negative_pooled_prompt_embeds=None,
+                     output_type="pil", return_dict=True, cross_attention_kwargs=None, guidance_rescale=0.0,
+                     original_size=None, target_size=None, clip_skip=None, callback_on_step_end=None,
+                     callback_on_step_end_tensor_inputs=("latents",), add_sample=True, **kwargs):
         """Several images of one size in one call (BASELINE configs[4], C5: a batch of 1024^2 restorations; the
         reference restores one image per pipe() call, test_wo_llava.py:53-97).  When each image is a single TLC
         tile (target_size covers the image latent), the images' CFG pairs share UNet forwards (tile_batch images
@@ -582,15 +593,25 @@ class FaithDiffStableDiffusionXLPipeline:
         the per-image work -- prompt encoding, preprocess, denoise encoder, VAE encode / decode, the CFG + Euler
         step and the blend -- unchanged: every image is bitwise the result of its own pipe() call with the same
         prompt, noise (``latents`` [n, 4, h, w]) and posterior draw (``posterior_noise`` [n, 4, h, w]); GPU test.
-        Images with several TLC tiles are restored one call at a time."""
+        Images with several TLC tiles are restored one call at a time.  Per-image tensors (latents, posterior
+        noise, the four precomputed embeddings) carry one row per image; prompt lists one entry per image; every
+        other argument (clip_skip, cross_attention_kwargs, the step callbacks) applies to every image."""
         nimg = len(imgs)
-        prompts = [prompt] * nimg if isinstance(prompt, str) or prompt is None else list(prompt)
-        negs = [negative_prompt] * nimg if negative_prompt is None or isinstance(negative_prompt, str) \
-            else list(negative_prompt)
-        if len(prompts) != nimg or len(negs) != nimg:
-            raise ValueError(f"{nimg} images need {nimg} prompts / negative prompts (got {len(prompts)} / {len(negs)})")
+
+        def per_image(x, what):
+            if x is None or isinstance(x, str):
+                return [x] * nimg
+            if len(x) != nimg:
+                raise ValueError(f"{nimg} images need {nimg} {what} (got {len(x)})")
+            return list(x) if not torch.is_tensor(x) else [x[i:i + 1] for i in range(nimg)]
+        prompts, prompts_2 = per_image(prompt, "prompts"), per_image(prompt_2, "prompt_2 entries")
+        negs, negs_2 = per_image(negative_prompt, "negative prompts"), per_image(negative_prompt_2, "negative_prompt_2")
+        embeds = [per_image(e, "embedding rows") for e in (prompt_embeds, negative_prompt_embeds, pooled_prompt_embeds,
+                                                           negative_pooled_prompt_embeds)]
         posterior_noise = kwargs.pop("posterior_noise", None)
         timer = kwargs.pop("timer", None)
+        callback = kwargs.pop("callback", None)
+        callback_steps = kwargs.pop("callback_steps", None)
         height = height or self.default_sample_size * self.vae_scale_factor
         width = width or self.default_sample_size * self.vae_scale_factor
         original_size = original_size or (height, width)
@@ -603,18 +624,26 @@ class FaithDiffStableDiffusionXLPipeline:
         if grid.ntiles != 1 or self.process_group is not None:
             outs = []
             for i in range(nimg):
-                o = self(lr_img=imgs[i], prompt=prompts[i], height=height, width=width,
+                o = self(lr_img=imgs[i], prompt=prompts[i], prompt_2=prompts_2[i], height=height, width=width,
                          num_inference_steps=num_inference_steps, start_point=start_point, timesteps=timesteps,
                          denoising_end=denoising_end, overlap=overlap, guidance_scale=guidance_scale,
-                         negative_prompt=negs[i], generator=generator, latents=pick(latents, i),
-                         output_type=output_type, return_dict=True, guidance_rescale=guidance_rescale,
-                         original_size=original_size, target_size=target_size, add_sample=add_sample,
-                         posterior_noise=pick(posterior_noise, i))
+                         negative_prompt=negs[i], negative_prompt_2=negs_2[i], generator=generator,
+                         latents=pick(latents, i), prompt_embeds=embeds[0][i], negative_prompt_embeds=embeds[1][i],
+                         pooled_prompt_embeds=embeds[2][i], negative_pooled_prompt_embeds=embeds[3][i],
+                         output_type=output_type, return_dict=True, cross_attention_kwargs=cross_attention_kwargs,
+                         guidance_rescale=guidance_rescale, original_size=original_size, target_size=target_size,
+                         clip_skip=clip_skip, callback_on_step_end=callback_on_step_end,
+                         callback_on_step_end_tensor_inputs=callback_on_step_end_tensor_inputs,
+                         add_sample=add_sample, posterior_noise=pick(posterior_noise, i), timer=timer,
+                         callback=callback, callback_steps=callback_steps, **kwargs)
                 outs.extend(o.images if isinstance(o.images, list) else [o.images])
             return FaithDiffStableDiffusionXLPipelineOutput(images=outs) if return_dict else (outs,)
-        self.check_inputs(imgs[0], prompts[0], None, height, width, None)
+        for i in range(nimg):
+            self.check_inputs(imgs[i], prompts[i], prompts_2[i], height, width, callback_steps, negs[i], negs_2[i],
+                              *[e[i] for e in embeds], callback_on_step_end_tensor_inputs)
         self._guidance_scale, self._guidance_rescale = guidance_scale, guidance_rescale
-        self._clip_skip, self._cross_attention_kwargs, self._denoising_end = None, None, denoising_end
+        self._clip_skip, self._cross_attention_kwargs, self._denoising_end = clip_skip, cross_attention_kwargs, \
+            denoising_end
         self._interrupt = False
         dev = self.device
         if dev.type != "cuda":
@@ -622,8 +651,14 @@ class FaithDiffStableDiffusionXLPipeline:
         unet = self.unet.hip()
         cfg = 2 if self.do_classifier_free_guidance else 1
         # prompts: one encoder pass over every image's prompt and negative prompt (each prompt its own row group)
-        pe, npe, ppe, nppe = self.encode_prompt(prompts, do_classifier_free_guidance=True,
-                                                negative_prompt=negs if any(n is not None for n in negs) else None)
+        def joined(col):
+            return None if col[0] is None else torch.cat(col, 0)
+        pe, npe, ppe, nppe = self.encode_prompt(
+            None if prompts[0] is None else prompts, prompt_2=None if prompts_2[0] is None else prompts_2,
+            do_classifier_free_guidance=True, negative_prompt=negs if any(n is not None for n in negs) else None,
+            negative_prompt_2=None if negs_2[0] is None else negs_2, prompt_embeds=joined(embeds[0]),
+            negative_prompt_embeds=joined(embeds[1]), pooled_prompt_embeds=joined(embeds[2]),
+            negative_pooled_prompt_embeds=joined(embeds[3]), clip_skip=clip_skip)
         if cfg == 2:
             ctx = torch.stack([npe.float(), pe.float()], 1).reshape(2 * nimg, *pe.shape[1:])
             text = torch.stack([nppe.float(), ppe.float()], 1).reshape(2 * nimg, -1)
@@ -703,9 +738,12 @@ class FaithDiffStableDiffusionXLPipeline:
             if timer is not None:
                 timer("step", st)
             if callback_on_step_end is not None:
-                out = callback_on_step_end(self, st, ts[st], {"latents": canvas})
+                cb = {k: (canvas if k == "latents" else None) for k in callback_on_step_end_tensor_inputs}
+                out = callback_on_step_end(self, st, ts[st], cb)
                 if out is not None and out.get("latents") is not None:
                     canvas.copy_(out["latents"].reshape(nimg, 4, h, w))
+            if callback is not None and callback_steps and st % callback_steps == 0:
+                callback(st, ts[st], canvas)
         if output_type == "latent":
             images = canvas.clone()
         else:

@@ -120,3 +120,57 @@ def call_inputs(H, W, seed):
     ppe, nppe = det_tensor((1, 32), seed + 3), det_tensor((1, 32), seed + 4)
     noise, post = det_tensor((1, 4, H // 8, W // 8), seed + 5), det_tensor((1, 4, H // 8, W // 8), seed + 6)
     return img, pe, npe, ppe, nppe, noise, post
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# UNet forward / Encoder.encode / load_state_dict pins (tests/golden/make_unet_golden.py runs the reference's own
+# UNet2DConditionModel.forward ext:480-697, Encoder.encode ext:122-148 and load_state_dict ext:444-478 unbound on the
+# oracle's blocks; tests/test_unet_golden_cpu.py checks the oracle and the product's host logic against them).
+UNET_WEIGHT_SEED = 1  # arch.random_init(arch.unet_param_shapes(), seed=1): the GPU UNet parity tests' weights
+
+
+def unet_inputs(h, w, ntiles=1, seed=0):
+    """(B, x, cond, ctx, text, tids) for a CFG-paired tile batch, as tests/test_unet_gpu.py feeds the UNet."""
+    g = torch.Generator().manual_seed(seed)
+    B = 2 * ntiles
+    x = torch.randn(ntiles, 4, h, w, generator=g).repeat_interleave(2, 0)
+    cond = torch.randn(ntiles, 512, h, w, generator=g).repeat_interleave(2, 0)
+    ctx = torch.randn(2, 77, 2048, generator=g)
+    text = torch.randn(2, 1280, generator=g).repeat(ntiles, 1)
+    tids = torch.tensor([[1024.0, 1024.0, 64.0 * i, 0.0, 1024.0, 1024.0] for i in range(ntiles)]).repeat_interleave(2, 0)
+    return B, x, cond, ctx, text, tids
+
+
+def unet_golden_cases():
+    """(name, h, w, ntiles, t, add_sample, with_embedding).  62x46 is not a multiple of 4, so the reference's
+    forward_upsample_size path (ext:522-529, 665-666) fires: 62 -> 31 -> 16 on the way down, 16 -> 31 -> 62 up."""
+    return [("s32", 32, 32, 1, 951.0, True, True),
+            ("r40x24", 40, 24, 2, 501.0, True, True),
+            ("odd62x46", 62, 46, 1, 951.0, True, True),
+            ("noadd32", 32, 32, 1, 301.0, False, True),
+            ("noemb24", 24, 24, 1, 51.0, True, False)]
+
+
+def lsd_cases(extras, core_key, core_shape):
+    """load_state_dict routing cases (ext:444-478): (name, state_dict, strict).  ``extras`` is a full extras +
+    denoise_encoder state dict; ``core_key`` one real core key of shape ``core_shape``."""
+    first = sorted(k for k in extras if k.startswith("spatial_ch_projs."))[-1]
+    minus = {k: v for k, v in extras.items() if k != first}
+    cne = "condition_embedding.conv_in.weight"
+    bad_shape = dict(extras)
+    bad_shape[cne] = torch.zeros(extras[cne].shape[0], 7, 3, 3)
+    extra_key = dict(extras)
+    extra_key["information_transformer_layes.5.ln_1.weight"] = torch.ones(640)
+    agg = dict(extras)
+    agg["agg_net.0.weight"] = torch.ones(4)
+    core = {core_key: det_tensor(core_shape, 77), "foo.unknown.weight": torch.ones(3)}
+    return [("full_strict", dict(extras), True),
+            ("missing_strict", minus, True),
+            ("missing_loose", minus, False),
+            ("agg_strict", agg, True),
+            ("agg_loose", agg, False),
+            ("unknown_core_strict", {**extras, **core}, True),
+            ("core_only_strict", core, True),
+            ("bad_shape_loose", bad_shape, False),
+            ("extra_key_strict", extra_key, True),
+            ("extra_key_loose", extra_key, False)]

@@ -99,26 +99,56 @@ def test_c5_back_to_back_images_bitwise_fresh_pipeline():
 
 
 def test_c5_images_batched_bitwise_single_calls():
-    """pipe(lr_img=[3 images], prompt=[3 prompts]) -- the images' CFG pairs share each UNet forward (B = 6 rows, each
-    pair attending to its own prompt's K/V) -- gives every image bitwise what its own pipe() call gives: the latents
-    after every step and the decoded pixels."""
-    S = 1024
+    """pipe(lr_img=[8 images], prompt=[8 prompts]) -- C5's shape (BASELINE configs[4], the batch bench.py's C5 leg
+    times): the images' CFG pairs share each UNet forward (B = 16 rows, each pair attending to its own prompt's K/V)
+    -- gives every image bitwise what its own pipe() call gives: the latents after every step and the decoded
+    pixels.  Reference loop: test_wo_llava.py:53-97 (one pipe() per image)."""
+    S, N = 1024, 8
     pipe = _build(seed=3)
-    imgs = [synthetic_degraded(S, S, 31 + i) for i in range(3)]
-    prompts = ["a harbour at dusk", "a handwritten letter", "a cat on a red sofa, restored"]
-    noise = torch.cat([det_tensor((1, 4, S // 8, S // 8), 80 + i) for i in range(3)])
-    post = torch.cat([det_tensor((1, 4, S // 8, S // 8), 90 + i) for i in range(3)])
+    imgs = [synthetic_degraded(S, S, 31 + i) for i in range(N)]
+    prompts = ["a harbour at dusk", "a handwritten letter", "a cat on a red sofa, restored", "a mountain lake",
+               "an old family portrait", "a street market at noon", "a macro shot of a leaf", "a city skyline at night"]
+    noise = torch.cat([det_tensor((1, 4, S // 8, S // 8), 80 + i) for i in range(N)])
+    post = torch.cat([det_tensor((1, 4, S // 8, S // 8), 90 + i) for i in range(N)])
     kw = dict(negative_prompt="", guidance_scale=5.0, start_point="lr", height=S, width=S, overlap=0.5,
               target_size=(1024, 1024), num_inference_steps=50, denoising_end=0.08)
     steps = []
     out = pipe(lr_img=imgs, prompt=prompts, latents=noise, posterior_noise=post,
                callback_on_step_end=lambda p, i, t, k: steps.append(k["latents"].detach().cpu().clone()) or {},
                **kw).images
-    assert len(out) == 3 and len(steps) == 4 and steps[-1].shape == (3, 4, S // 8, S // 8)
-    assert pipe.unet.hip().npairs == 3
-    for i in range(3):
+    assert len(out) == N and len(steps) == 4 and steps[-1].shape == (N, 4, S // 8, S // 8)
+    assert pipe.unet.hip().npairs == N
+    assert torch.isfinite(steps[-1]).all()
+    for i in range(N):
         lat, img, n = _run(pipe, imgs[i], prompts[i], noise[i:i + 1], post[i:i + 1], S, (1024, 1024),
                            num_inference_steps=50, denoising_end=0.08)
         assert n == 4
         assert torch.equal(steps[-1][i:i + 1], lat), f"image {i}: batched latents differ from its own call"
         assert (np.asarray(out[i]) == img).all(), f"image {i}: batched pixels differ from its own call"
+        assert img.std() > 1.0
+
+
+def test_batched_call_forwards_embeddings_and_callbacks():
+    """pipe(lr_img=[...]) forwards every argument the single-image call takes: precomputed
+    prompt / negative / pooled embeddings (one row per image) give bitwise the prompts' result, the legacy
+    ``callback`` / ``callback_steps`` fire, and num_images_per_prompt > 1 is refused instead of ignored."""
+    S = 512
+    pipe = _build(seed=4)
+    imgs = [synthetic_degraded(S, S, 41 + i) for i in range(2)]
+    prompts = ["a restored photo of a red door", "a restored photo of a green field"]
+    noise = torch.cat([det_tensor((1, 4, S // 8, S // 8), 110 + i) for i in range(2)])
+    post = torch.cat([det_tensor((1, 4, S // 8, S // 8), 120 + i) for i in range(2)])
+    kw = dict(guidance_scale=5.0, start_point="lr", height=S, width=S, overlap=0.5, target_size=(512, 512),
+              num_inference_steps=4, latents=noise, posterior_noise=post, output_type="np")
+    a = pipe(lr_img=imgs, prompt=prompts, negative_prompt="", **kw).images
+    pe, npe, ppe, nppe = pipe.encode_prompt(prompts, do_classifier_free_guidance=True, negative_prompt=["", ""])
+    seen = []
+    b = pipe(lr_img=imgs, prompt_embeds=pe, negative_prompt_embeds=npe, pooled_prompt_embeds=ppe,
+             negative_pooled_prompt_embeds=nppe, callback=lambda i, t, lat: seen.append(i), callback_steps=2,
+             **kw).images
+    assert len(a) == len(b) == 2
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert seen == [0, 2]
+    with pytest.raises(NotImplementedError):
+        pipe(lr_img=imgs, prompt=prompts, num_images_per_prompt=2, **kw)

@@ -29,14 +29,8 @@ def unet_pair():
 
 
 def make_inputs(h, w, ntiles=1, seed=0):
-    g = torch.Generator().manual_seed(seed)
-    B = 2 * ntiles
-    x = torch.randn(ntiles, 4, h, w, generator=g).repeat_interleave(2, 0)
-    cond = torch.randn(ntiles, 512, h, w, generator=g).repeat_interleave(2, 0)
-    ctx = torch.randn(2, 77, 2048, generator=g)
-    text = torch.randn(2, 1280, generator=g).repeat(ntiles, 1)
-    tids = torch.tensor([[1024.0, 1024.0, 64.0 * i, 0.0, 1024.0, 1024.0] for i in range(ntiles)]).repeat_interleave(2, 0)
-    return B, x, cond, ctx, text, tids
+    from _det import unet_inputs
+    return unet_inputs(h, w, ntiles, seed)
 
 
 def run_hip(hip, B, x, cond, ctx, text, tids, t, h, w):
@@ -66,14 +60,45 @@ def metrics(a, b):
     return parity.rel_l2(a, b), parity.cos(a, b)
 
 
-@pytest.mark.parametrize("h,w,ntiles,t", [(32, 32, 1, 951.0), (40, 24, 2, 501.0), (128, 128, 1, 951.0)])
+@pytest.mark.parametrize("h,w,ntiles,t", [(32, 32, 1, 951.0), (40, 24, 2, 501.0), (128, 128, 1, 951.0),
+                                           (62, 46, 1, 951.0)])
 def test_unet_forward_matches_oracle(h, w, ntiles, t):
+    """62x46 is not a multiple of 4: diffusers' forward_upsample_size path (ext:522-529, 665-666), 62 -> 31 -> 16 down
+    and 16 -> 31 -> 62 up, as every test_wo_llava.py image whose padded latent is not a multiple of 4 runs."""
     ref, hip = unet_pair()
     B, x, cond, ctx, text, tids = make_inputs(h, w, ntiles)
     out = run_hip(hip, B, x, cond, ctx, text, tids, t, h, w)
     exp = run_ref(ref, B, x, cond, ctx, text, tids, t)
     rel, cos = metrics(out, exp)
     print(f"unet {h}x{w} tiles={ntiles}: rel_l2={rel:.3e} cos={cos:.6f} |eps|={exp.norm().item():.3e}")
+    assert rel < 1.5e-2 and cos > 0.9999
+
+
+@pytest.mark.parametrize("name", ["s32", "odd62x46", "noadd32", "noemb24"])
+def test_unet_forward_matches_reference_golden(name):
+    """HIP UNet directly against the reference's own forward (ext:480-697) run on the oracle's fp32 blocks
+    (tests/golden/make_unet_golden.py): same weights (seed 1), same inputs; covers add_sample=False (ext:579) and
+    no input_embedding (ext:572).  Same bar as against the oracle."""
+    import os
+
+    import numpy as np
+    from _det import unet_golden_cases
+    case = {c[0]: c for c in unet_golden_cases()}[name]
+    _, h, w, ntiles, t, add_sample, with_emb = case
+    _, hip = unet_pair()
+    B, x, cond, ctx, text, tids = make_inputs(h, w, ntiles)
+    dev = "cuda"
+    hip.set_context(ctx)
+    xn = x.permute(0, 2, 3, 1).reshape(B * h * w, 4).to(dev, torch.bfloat16).contiguous()
+    cn = cond.permute(0, 2, 3, 1).reshape(B * h * w, 512).to(dev, torch.bfloat16).contiguous() if with_emb else None
+    eps = hip.forward(xn, torch.full((B,), float(t), device=dev), tids.to(dev), text.to(dev), cn, B, h, w,
+                      add_sample=add_sample)
+    torch.cuda.synchronize()
+    out = eps.float().reshape(B, h, w, 4).permute(0, 3, 1, 2).cpu()
+    gold = torch.from_numpy(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                                 "unet_golden.npz"))[f"unet_{name}"])
+    rel, cos = metrics(out, gold)
+    print(f"unet {name} vs reference-forward golden: rel_l2={rel:.3e} cos={cos:.6f}")
     assert rel < 1.5e-2 and cos > 0.9999
 
 
