@@ -543,13 +543,16 @@ def main(argv=None):
     if rc is not None:
         return rc
     world, rank, local = setup_dist()
+    from fdhip import knobs
     from fdhip import lib as L
+    knobs.apply_env()  # A/B runs set FD_* knobs in the environment; every non-default value is reported below
     L.require_device()
     dev = torch.device("cuda", local)
     pipe = build_pipe(dev, args.fp8, world)
     result = {"n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
               "vs_baseline": None, "dtype": "fp8-e4m3+bf16" if args.fp8 else "bf16",
-              "data": "synthetic (seeded random-init SDXL+FaithDiff weights, synthetic latents/conditions/images)"}
+              "data": "synthetic (seeded random-init SDXL+FaithDiff weights, synthetic latents/conditions/images)",
+              "knobs": knobs.changed()}
     if world > 1:  # rank 0 drew the weights, every other rank received them (FaithDiff_pipeline(process_group=))
         result["weights_broadcast"] = {"bytes": pipe.last_broadcast_bytes, "build_s": round(pipe.build_s, 2),
                                        "backend": dist.get_backend()}

@@ -16,7 +16,7 @@ from types import SimpleNamespace
 
 import torch
 
-from fdhip import arch, ops
+from fdhip import arch, knobs, ops
 from fdhip import lib as L
 
 RANDOM_INIT = "random-init"
@@ -186,7 +186,7 @@ class UNet2DConditionModel:
             sd = arch.quantize_e4m3(self._sd) if self._fp8 else self._sd
             # default: 16-bit MFMA on the widened e4m3 values (exactly the reference's autocast arithmetic);
             # opt-in (quantize_8bit(fp8_mfma=True) or FD_FP8_MFMA=1): transformer Linears on the e4m3 MFMA
-            opt = self._fp8_mfma if self._fp8_mfma is not None else os.environ.get("FD_FP8_MFMA", "0") == "1"
+            opt = self._fp8_mfma if self._fp8_mfma is not None else knobs.get("FD_FP8_MFMA") == 1
             fp8_mfma = self._fp8 and opt
             self._hip = HipUNet(sd, self._device, cdt, fp8_mfma=fp8_mfma)
         return self._hip

@@ -17,7 +17,6 @@ run on the HIP kernels (fdhip/clip.py) when built by from_pretrained, with a see
 only for pipelines constructed without them.
 """
 import inspect
-import os
 import zlib
 from types import SimpleNamespace
 from typing import Any, Callable, Dict, List, Optional, Tuple, Union
@@ -27,7 +26,7 @@ import PIL.Image
 import torch
 import torch.distributed as dist
 
-from fdhip import ops
+from fdhip import knobs, ops
 
 from ..schedulers import DDPMScheduler, EulerDiscreteScheduler
 from .pipeline_output import FaithDiffStableDiffusionXLPipelineOutput
@@ -89,7 +88,7 @@ class FaithDiffStableDiffusionXLPipeline:
         self.device = torch.device("cpu")
         # TLC tiles per UNet forward (B = 2 * tile_batch rows; C3 4096^2: 4 -> 13 tiles = 51.6 -> 53.2 tile-steps/s,
         # scripts/tb_sweep.sh); FD_TILE_BATCH overrides (A/B timing)
-        self.tile_batch = int(os.environ.get("FD_TILE_BATCH", "13"))
+        self.tile_batch = knobs.get("FD_TILE_BATCH")
         self.process_group = None    # torch.distributed group for tile parallelism (None: single GPU)
         self.last_timings = {}
         self._weights_group = None   # the group broadcast_weights last synchronised the weights over

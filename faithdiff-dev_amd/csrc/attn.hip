@@ -502,16 +502,11 @@ static int flash_d64(const void* q, long long ldq, long long qbs, const void* k,
   if (!q || !k || !v || !o) return FD_ERR_ARG;
   if (batch <= 0 || heads <= 0 || Lq <= 0 || Lk <= 0 || kv_mod < 0) return FD_ERR_SHAPE;
   if ((ldq | ldk | ldv | ldo) & 7) return FD_ERR_SHAPE;
-  static int swz = -1, nwv = 0, nqb = 0;
-  if (swz < 0) {
-    const char* e = getenv("FD_FLASH_SWZ");
-    swz = e ? atoi(e) : 1;
-    e = getenv("FD_FLASH_WAVES");  // waves per workgroup: 4 (default), 2 or 8
-    nwv = e ? atoi(e) : 4;
-    e = getenv("FD_FLASH_QPW");  // queries per wave: 32 or 16 (default: by launch size, below)
-    nqb = e ? (atoi(e) == 16 ? 1 : 2) : 0;
-    if (nwv != 2 && nwv != 8) nwv = 4;
-  }
+  const int swz = fd_knob(FDK_FLASH_SWZ);
+  int nwv = fd_knob(FDK_FLASH_WAVES);  // waves per workgroup: 4 (default), 2 or 8
+  const int qpw = fd_knob(FDK_FLASH_QPW);  // queries per wave: 32 or 16 (0: by launch size, below)
+  const int nqb = qpw == 0 ? 0 : (qpw == 16 ? 1 : 2);
+  if (nwv != 2 && nwv != 8) nwv = 4;
   // 16 queries per wave (half the VGPRs: three waves per SIMD, one wave's softmax under another's MFMAs) while
   // the 32-query grid would give at most 4 workgroups per CU (scripts/attn_var.sh: C2's L = 1024 28.3 -> 24.4 us,
   // L = 4096 134 -> 127 us, cross-attention 8.6 -> 7.6 us); past that the 32-query kernel's fewer K/V fragment

@@ -14,6 +14,16 @@ typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 
+// Launch-planner knobs (knobs.hip): tested defaults, switched only by tests / probes through fd_set_knob.
+enum fd_knob_id {
+  FDK_GEMM8, FDK_GEMM8_S, FDK_GEMM8_GM, FDK_GEMM_R4, FDK_GEMM_P128, FDK_GEMM_R4_NS, FDK_GEMM_B4, FDK_GEMM8_W160,
+  FDK_GEMM8_N128, FDK_GEMM8_LNP, FDK_GEMM8_LNP_S, FDK_GEMM8_MIDK, FDK_F8_TILE, FDK_F8_KERNEL, FDK_GEMM_CFG,
+  FDK_GEMM_NS, FDK_GEMM_KS, FDK_GEMM_SWZ, FDK_GEMM_MODE, FDK_GEMV, FDK_GEMM256, FDK_GEMM256_MIN_TILES,
+  FDK_GN_MIN_CHUNKS, FDK_GN_APPLY_V, FDK_GN_APPLY_BLOCKS, FDK_GN_APPLY_U, FDK_FLASH_SWZ, FDK_FLASH_WAVES,
+  FDK_FLASH_QPW, FDK_COUNT
+};
+int fd_knob(int id);
+
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
 template <typename T> struct VecT;

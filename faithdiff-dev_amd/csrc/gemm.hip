@@ -566,13 +566,8 @@ static int pick_cfg(const fd_gemm_params* p) {
   return best;
 }
 
-// Tuning overrides (benchmarks only): FD_GEMM_CFG=<0..3> forces the tile, FD_GEMM_NS=<2|3|4> the ring
-// depth, FD_GEMM_SWZ=<0|1> the tile order.  Read once.
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-static int g_cfg = -2, g_ns = -1, g_swz = -1, g_ks = 0;
+// Tuning overrides (knob table, benchmarks only): FD_GEMM_CFG=<0..3> forces the tile, FD_GEMM_NS=<2|3|4> the ring
+// depth, FD_GEMM_SWZ=<0|1> the tile order.
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
 static int dispatch_ns(const fd_gemm_params* p, hipStream_t s, int ns, int ks, int swz) {
@@ -611,12 +606,8 @@ static bool gn_ok4(const fd_gemm_params* p, int cfg) {
 
 template <typename T, typename TO>
 static int dispatch_tiles(fd_gemm_params* p0, hipStream_t s) {
-  if (g_cfg == -2) {
-    g_cfg = env_int("FD_GEMM_CFG", -1);
-    g_ns = env_int("FD_GEMM_NS", 0);
-    g_ks = env_int("FD_GEMM_KS", 0);
-    g_swz = env_int("FD_GEMM_SWZ", 1) | (env_int("FD_GEMM_MODE", 0) << 4);
-  }
+  const int g_cfg = fd_knob(FDK_GEMM_CFG), g_ns = fd_knob(FDK_GEMM_NS), g_ks = fd_knob(FDK_GEMM_KS);
+  const int g_swz = fd_knob(FDK_GEMM_SWZ) | (fd_knob(FDK_GEMM_MODE) << 4);
   int cfg = g_cfg >= 0 && g_cfg < CFG_COUNT ? g_cfg : pick_cfg(p0);
   if (p0->ln_out) cfg = CFG_64x160;  // LN-fold producer: partials per 160 columns, whatever M (batch-invariant)
   if (p0->act == FD_ACT_GEGLU && cfg == CFG_64x160) cfg = CFG_128x128;
@@ -696,7 +687,7 @@ __global__ void __launch_bounds__(256) gemv_rows_kernel(const fd_gemm_params p) 
 // Returns 1 when the GEMV took the launch, 0 when it does not apply.
 template <typename T, typename TO>
 static int try_gemv_rows(const fd_gemm_params* p, hipStream_t s) {
-  static const int on = env_int("FD_GEMV", 1);
+  const int on = fd_knob(FDK_GEMV);
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if (!on || m_ref > 4 || p->M > 4096 || p->conv || (p->batch > 1) || p->rowbias || p->ln_in || p->ln_out ||
       p->gn_part || p->act == FD_ACT_GEGLU || p->A2 || (p->K % 8) || (p->lda % 8) || (p->ldb % 8))

@@ -341,17 +341,12 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
   if (gn) gn_tile_write(gna, (float2*)(smem + RED_OFF), tid, NTHR, VPR, gcpg, BN, n0, m0, p);
 }
 
-int env256(const char* n, int d) {
-  const char* v = getenv(n);
-  return v ? atoi(v) : d;
-}
-
 }  // namespace
 
 // Returns 1 and launches when this kernel takes the GEMM, 0 when it does not apply, < 0 on error.  Taken for
 // N % 256 == 0, no GEGLU / LayerNorm fold / batching, and at least 192 tiles of 256 x 256 counted from the
 // per-TLC-tile row count m_ref (so batching tiles never changes the kernel choice: bitwise batch-invariant).
-// FD_GEMM256=0 disables it (A/B timing).
+// Knob FD_GEMM256 = 0 disables it (tests: the bitwise gemm8 comparison).
 extern "C" int fd_gemm256_try(fd_gemm_params* p0, void* stream) {
   fd_gemm_params q = *p0;  // the kernel's copy: gn_part kept only where the statistics can be written
   {
@@ -369,9 +364,8 @@ extern "C" int fd_gemm256_try(fd_gemm_params* p0, void* stream) {
     if (!ok) q.gn_part = nullptr;
   }
   const fd_gemm_params* p = &q;
-  static int min_tiles = -1;
-  if (min_tiles < 0) min_tiles = env256("FD_GEMM256_MIN_TILES", 192);
-  const int enabled = env256("FD_GEMM256", 1);  // read per call: tests compare against gemm8 in one process
+  const int min_tiles = fd_knob(FDK_GEMM256_MIN_TILES);
+  const int enabled = fd_knob(FDK_GEMM256);  // tests compare against gemm8 in one process
   if (!enabled || p->batch > 1 || p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out || p->N % 256 || p->K % 32)
     return 0;
   if (p->conv && (p->Cin % 32 || (p->C1 > 0 && p->C1 % 32))) return 0;

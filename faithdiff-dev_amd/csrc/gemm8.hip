@@ -909,11 +909,6 @@ struct Plan8 {
   int bm, bn, nw, waves_m, ns, S, group_m, tiles;
 };
 
-int env_i(const char* n, int d) {
-  const char* v = getenv(n);
-  return v ? atoi(v) : d;
-}
-
 // Split count from the per-tile row count m_ref (not the batched M).  Measured on MI355X (scripts/gemm8_sweep.sh,
 // profiles/r01_gemm8_sweep.txt): one 147 KiB workgroup per CU streams ~40-70 GB/s of operands, so a 256x128 tile
 // K step costs ~1.1-1.4 us whatever the tile count, while the split-K slab round trip (write-through fp32 slabs
@@ -928,7 +923,7 @@ int choose_split(int m_ref, int N, int K, int bn) {
   // mid K on the 32^2 level (ff out 2048 x 1280 x 5120, the K = 5760 conv): three splits of 80 tiles beat the
   // 4-wave 64 x 160 kernel with cold weights, 47.1 -> 41.1 us / 61.2 -> 45.0 us, and stay ahead when 13 TLC tiles
   // share the launch (C3: 520 -> 454 us); N = 640 at 64^2 (160 tiles) gains nothing (profiles/r02e_ksplit.jsonl)
-  static const int midk = env_i("FD_GEMM8_MIDK", 3);  // 0 = off (A/B), else the split count
+  const int midk = fd_knob(FDK_GEMM8_MIDK);  // 0 = off (A/B), else the split count
   if (midk > 0 && K >= 4096 && K < 8192 && N >= 1280 && tiles <= 96) return midk;
   if (K < 8192) return 0;
   int s = (int)(256 / tiles);
@@ -974,19 +969,12 @@ int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
 // the 4-wave kernel sums each K step's two halves in separate waves, these kernels in one accumulator,
 // and any tile shape of the same kernel family gives the same k order.
 static int plan8(const fd_gemm_params* p, Plan8* pl) {
-  static int enabled = -1, force_s = 0, force_gm = 0, r4 = 1, pair128 = 0, r4_ns = 3, b4 = 0, w160 = 1;
-  if (enabled < 0) {
-    enabled = env_i("FD_GEMM8", 1);
-    force_s = env_i("FD_GEMM8_S", 0);
-    force_gm = env_i("FD_GEMM8_GM", 0);
-    // 64 x 160 one-wave-per-SIMD kernel: 0 off (default: 0.5 % slower in the bench step than the 4-wave
-    // kernel though faster in isolation), 1 <= 256 tiles, 2 every non-GEGLU
-    r4 = env_i("FD_GEMM_R4", 0);
-    pair128 = env_i("FD_GEMM_P128", 0);
-    r4_ns = env_i("FD_GEMM_R4_NS", 3);
-    b4 = env_i("FD_GEMM_B4", 0);
-    w160 = env_i("FD_GEMM8_W160", 3);  // bit 0: 256 x 160 tiles where faster; bit 1: also take N = 320 from the 4-wave kernel
-  }
+  const int enabled = fd_knob(FDK_GEMM8), force_s = fd_knob(FDK_GEMM8_S), force_gm = fd_knob(FDK_GEMM8_GM);
+  // 64 x 160 one-wave-per-SIMD kernel: 0 off (default: 0.5 % slower in the bench step than the 4-wave kernel though
+  // faster in isolation), 1 <= 256 tiles, 2 every non-GEGLU
+  const int r4 = fd_knob(FDK_GEMM_R4), pair128 = fd_knob(FDK_GEMM_P128), r4_ns = fd_knob(FDK_GEMM_R4_NS);
+  const int b4 = fd_knob(FDK_GEMM_B4);
+  const int w160 = fd_knob(FDK_GEMM8_W160);  // bit 0: 256 x 160 tiles where faster; bit 1: also take N = 320
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if (!enabled || p->batch > 1 || p->K < 128) return 0;
   // 128-channel 3x3 convs on >= 512^2 images (the VAE decoder's last up block and the encoders' first level at
@@ -994,7 +982,7 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
   // prologue / epilogue under the other's main loop): 15 % faster than gemm8 256 x 128 without GroupNorm
   // statistics (profiles/r03_vae_tile_ab.txt), but only 3 % with them, and the decode as a whole 0.1 ms slower
   // (profiles/r03_n128_ab.txt).  Off by default; FD_GEMM8_N128=1 routes them (A/B).
-  static const int n128 = env_i("FD_GEMM8_N128", 0);
+  const int n128 = fd_knob(FDK_GEMM8_N128);
   if (n128 && p->conv && p->N == 128 && m_ref >= 262144) return 0;
   Plan8 q;
   if (p->ln_out) {
@@ -1002,8 +990,8 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     // of the 32^2 level, 2048 x 1280 x 5120 at C2): 128 x 160 tiles with K split in two (pairwise combine),
     // 0.64x the operand bytes per CU of the 4-wave 64 x 160 producer (probe with cold weights 47.1 -> 40.6 us,
     // profiles/r02e_m2048_split.jsonl); anything else stays on that producer (return 0).
-    static const int lnp = env_i("FD_GEMM8_LNP", 1);
-    static const int lnp_s = env_i("FD_GEMM8_LNP_S", 4);  // A/B knob: splits of the 256 x 160 form (lnp = 2)
+    const int lnp = fd_knob(FDK_GEMM8_LNP);
+    const int lnp_s = fd_knob(FDK_GEMM8_LNP_S);  // splits of the 256 x 160 form (lnp = 2)
     if (!lnp || p->act == FD_ACT_GEGLU || p->conv || p->N % 160 || p->K < 4096 || m_ref < 128) return 0;
     if ((long long)((m_ref + 63) / 64) * (p->N / 160) > 256) return 0;
     if (lnp == 2 && m_ref >= 256) {  // 256 x 160 tiles (0.76x the operand bytes per CU of 128 x 160), S-way K split
@@ -1187,7 +1175,7 @@ int launch8_e4m3(const fd_gemm_params* p, const Plan8& pl, const f8_args& f8, hi
 // K = 1280 tile); FD_F8_TILE = 256160 / 256128 / 128160 / 64160 forces one (A/B, tests).  mx_out: only tiles whose
 // output columns are whole 32-column blocks and lie inside M / N_out (the MX epilogue has no edge path).
 int plan_e4m3(const fd_gemm_params* p, bool mx_out, Plan8* pl) {
-  const int force = env_i("FD_F8_TILE", 0);  // read per call: tests compare the shapes in one process
+  const int force = fd_knob(FDK_F8_TILE);  // tests compare the shapes in one process
   struct Cand { int bm, bn, nw, wm; double a, b; };
   static const Cand cands[4] = {{256, 160, 8, 8, 10.6, 10.2}, {256, 128, 8, 4, 7.5, 7.9},
                                 {128, 160, 4, 2, 7.4, 6.0}, {64, 160, 4, 2, 5.65, 4.42}};

@@ -529,9 +529,9 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
   // K % 128 == 0: LDS-DMA ring kernel -- 64-row tiles with 3 stages (72 KB: two workgroups per CU), 128-row
   // tiles with 2 stages (64 KB; a 3-stage 96-KB ring leaves one workgroup per CU: 8192x640x640 23 -> 38 us).
   // Ragged K, or FD_F8_KERNEL=reg (A/B timing): the register-staged kernel.
-  const char* kenv = getenv("FD_F8_KERNEL");  // per call (tests compare the kernels in one process)
-  // K % 128 == 0: the eight-wave kernel family (gemm8.hip, 256-row tiles) unless FD_F8_KERNEL selects one of these
-  if (!kenv) {
+  const int kf = fd_knob(FDK_F8_KERNEL);  // tests compare the kernels in one process
+  // K % 128 == 0: the eight-wave kernel family (gemm8.hip, 256-row tiles) unless knob FD_F8_KERNEL selects one of these
+  if (kf == 0) {
     fd_gemm_params p{};
     p.A = A;
     p.B = W;
@@ -554,11 +554,11 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
     if (r8 < 0) return r8;
     if (r8 == 1) return FD_OK;
   }
-  const bool dma = (K % F8_BK) == 0 && !(kenv && kenv[0] == 'r');
+  const bool dma = (K % F8_BK) == 0 && kf != 2;
   // 16-B vector epilogue when every output row / residual row starts 16-B aligned (FD_F8_KERNEL=scalar: off)
   const int vec = (nout % 8) == 0 && (ldc % 8) == 0 && (((unsigned long long)C) & 15) == 0 &&
                   (!residual || ((ldr % 8) == 0 && (((unsigned long long)residual) & 15) == 0)) &&
-                  !(kenv && kenv[0] == 's');
+                  kf != 3;
   FD_DISPATCH_O(out_dtype, {
     if (dma) {
       auto kern = small ? gemm_e4m3_dma_kernel<TO, 64, 3> : gemm_e4m3_dma_kernel<TO, 128, 2>;

@@ -1,0 +1,93 @@
+// Launch-planner knobs: ONE table of tested defaults, compiled in.  The library never reads the environment; the
+// product uses these values as they are.  Tests and measurement scripts switch an entry through fd_set_knob (C ABI,
+// include/faithdiff_hip.h) to compare kernel variants in one process (e.g. gemm256 vs gemm8 bitwise, the e4m3 tile
+// shapes); fd_reset_knobs restores the table.  Every bitwise batching invariant the GPU suite certifies is certified
+// for these defaults.
+#include <string.h>
+
+#include "fd_common.h"
+
+namespace {
+struct KnobDef {
+  const char* name;
+  int dflt;
+};
+// order = enum fd_knob_id (fd_common.h)
+const KnobDef kDefs[FDK_COUNT] = {
+    {"FD_GEMM8", 1},          // eight-wave 256-row kernels on (0: everything on the 4-wave kernel)
+    {"FD_GEMM8_S", 0},        // force the split count (0: planner)
+    {"FD_GEMM8_GM", 0},       // force the tile-walk group height (0: planner)
+    {"FD_GEMM_R4", 0},        // 64 x 160 one-wave-per-SIMD instance (measured slower in the step)
+    {"FD_GEMM_P128", 0},      // pairwise 128-row split for M = 2048 (measured slower)
+    {"FD_GEMM_R4_NS", 3},     // ring depth of that instance
+    {"FD_GEMM_B4", 0},        // 4-deep ring for the 256-row kernels (measured slower)
+    {"FD_GEMM8_W160", 3},     // bit 0: 256 x 160 tiles where faster; bit 1: take N = 320 from the 4-wave kernel
+    {"FD_GEMM8_N128", 0},     // 128-channel convs at >= 512^2 on the 4-wave 128 x 128 tiles (decode 0.1 ms slower)
+    {"FD_GEMM8_LNP", 1},      // LN-fold producers with K >= 4096 on the 128 x 160 pairwise split
+    {"FD_GEMM8_LNP_S", 4},    // split count of the 256 x 160 producer form (LNP = 2)
+    {"FD_GEMM8_MIDK", 3},     // K splits for the mid-K launches of the 32^2 level (0: off)
+    {"FD_F8_TILE", 0},        // force the e4m3 eight-wave tile (256160 / 256128 / 128160 / 64160; 0: planner)
+    {"FD_F8_KERNEL", 0},      // e4m3 kernel: 0 eight-wave family, 1 4-wave LDS-DMA, 2 register-staged, 3 scalar epilogue
+    {"FD_GEMM_CFG", -1},      // 4-wave kernel: force the tile config (-1: planner)
+    {"FD_GEMM_NS", 0},        // 4-wave kernel: force the ring depth (0: per config)
+    {"FD_GEMM_KS", 0},        // 4-wave kernel: force the K split across wave groups (0: per config)
+    {"FD_GEMM_SWZ", 1},       // 4-wave kernel: XCD-aware tile order
+    {"FD_GEMM_MODE", 0},      // 4-wave kernel diagnostic build mode (1 loads only, 2 MFMA only; probes only)
+    {"FD_GEMV", 1},           // few-row GEMV for M <= 4
+    {"FD_GEMM256", 1},        // 256 x 256 kernel where it applies (0: gemm8, bitwise-equal reference in tests)
+    {"FD_GEMM256_MIN_TILES", 192},
+    {"FD_GN_MIN_CHUNKS", 256},     // GroupNorm row-chunk floor for small images
+    {"FD_GN_APPLY_V", 2},          // GroupNorm apply: 2 register scale/shift kernel, 1 LDS-table kernel
+    {"FD_GN_APPLY_BLOCKS", 1024},  // GroupNorm apply grid cap
+    {"FD_GN_APPLY_U", 4},          // GroupNorm apply vectors in flight per thread
+    {"FD_FLASH_SWZ", 1},           // flash attention XCD-aware block order
+    {"FD_FLASH_WAVES", 4},         // flash attention waves per workgroup (2, 4, 8)
+    {"FD_FLASH_QPW", 0},           // flash attention queries per wave (0: by launch size, 16, 32)
+};
+int g_knobs[FDK_COUNT];
+bool g_init = false;
+
+void init_knobs() {
+  if (g_init) return;
+  for (int i = 0; i < FDK_COUNT; ++i) g_knobs[i] = kDefs[i].dflt;
+  g_init = true;
+}
+}  // namespace
+
+int fd_knob(int id) {
+  init_knobs();
+  return g_knobs[id];
+}
+
+extern "C" int fd_set_knob(const char* name, int value, int* previous) {
+  init_knobs();
+  if (!name) return FD_ERR_ARG;
+  for (int i = 0; i < FDK_COUNT; ++i) {
+    if (strcmp(name, kDefs[i].name) == 0) {
+      if (previous) *previous = g_knobs[i];
+      g_knobs[i] = value;
+      return FD_OK;
+    }
+  }
+  return FD_ERR_ARG;
+}
+
+extern "C" int fd_get_knob(const char* name, int* value, int* dflt) {
+  init_knobs();
+  if (!name) return FD_ERR_ARG;
+  for (int i = 0; i < FDK_COUNT; ++i) {
+    if (strcmp(name, kDefs[i].name) == 0) {
+      if (value) *value = g_knobs[i];
+      if (dflt) *dflt = kDefs[i].dflt;
+      return FD_OK;
+    }
+  }
+  return FD_ERR_ARG;
+}
+
+extern "C" const char* fd_knob_name(int id) { return (id >= 0 && id < FDK_COUNT) ? kDefs[id].name : nullptr; }
+
+extern "C" void fd_reset_knobs(void) {
+  g_init = false;
+  init_knobs();
+}

@@ -11,11 +11,6 @@
 
 #define GN_MAXC 2560
 
-static int env_gn(const char* n, int d) {
-  const char* v = getenv(n);
-  return v ? atoi(v) : d;
-}
-
 static inline int gn_rows_per_chunk(int nimg, int HW) {
   // chunk count chosen from HW alone: the per-(image, group) reduction order -- and so
   // every bit of the result -- does not depend on how many images share the launch (tile batching, CFG
@@ -23,7 +18,7 @@ static inline int gn_rows_per_chunk(int nimg, int HW) {
   // Large images (the VAE at 512^2 / 1024^2: HW up to 1M rows) get up to 1024 chunks of >= 64 rows: 256 chunks
   // of 4096 rows left one 4-wave block per CU, latency-bound at ~4 TB/s.
   (void)nimg;
-  static const int lo = env_gn("FD_GN_MIN_CHUNKS", 256);  // A/B knob: chunk floor for small images
+  const int lo = fd_knob(FDK_GN_MIN_CHUNKS);  // chunk floor for small images
   const int target = HW / 64 > 1024 ? 1024 : (HW / 64 < lo ? lo : HW / 64);
   int r = 1;
   while ((HW + r - 1) / r > target) r *= 2;
@@ -328,15 +323,15 @@ __global__ void __launch_bounds__(256) gn_apply2_kernel(const T* __restrict__ x,
 }
 
 static int gn_apply_version() {
-  static const int v = env_gn("FD_GN_APPLY_V", 2);  // 1 = the LDS-table kernel (A/B)
+  const int v = fd_knob(FDK_GN_APPLY_V);  // 1 = the LDS-table kernel (A/B)
   return v;
 }
 
 // the apply launch shared by fd_group_norm and fd_group_norm_partials (grid: ~1024 blocks of whole rows)
 static int gn_apply_launch(const void* x, void* y, const float2* stats, const float* gamma, const float* beta, int nimg,
                            int HW, int C, int groups, int silu, int dtype, hipStream_t s) {
-  static const int apply_blocks = env_gn("FD_GN_APPLY_BLOCKS", 1024);
-  static const int apply_u = env_gn("FD_GN_APPLY_U", 4);  // vectors in flight per thread (A/B knob: 4 or 8)
+  const int apply_blocks = fd_knob(FDK_GN_APPLY_BLOCKS);
+  const int apply_u = fd_knob(FDK_GN_APPLY_U);  // vectors in flight per thread (4 or 8)
   int rpb = 1;
   while ((long long)nimg * ((HW + rpb - 1) / rpb) > apply_blocks) rpb *= 2;
   const int nblk = (HW + rpb - 1) / rpb;

@@ -20,16 +20,17 @@ every replay, so they live exactly as long as the graph.  FD_GRAPHS=0 disables c
 A/B timing and debugging.
 """
 import collections
-import os
 
 import torch
+
+from . import knobs
 
 
 class GraphCache:
     def __init__(self, max_graphs=8, min_uses=2):
         self.max_graphs = max_graphs
         self.min_uses = min_uses
-        self.enabled = os.environ.get("FD_GRAPHS", "1") != "0"
+        self.enabled = knobs.get("FD_GRAPHS") != 0
         self._uses = collections.Counter()
         self._graphs = collections.OrderedDict()  # key -> (graph, static inputs, static output)
 

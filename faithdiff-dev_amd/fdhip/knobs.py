@@ -1,0 +1,105 @@
+"""Path and launch-planner knobs: ONE table of tested defaults.
+
+The library's planner knobs live in csrc/knobs.hip (compiled in; the library never reads the environment); the host
+layer's path switches live in ``HOST_DEFAULTS`` below.  The product uses the defaults as they are.  Tests compare
+kernel variants with ``override(...)`` (a context manager that restores the table), and measurement scripts opt in
+to environment overrides with ``apply_env()`` -- nothing under ``faithdiff-dev_amd/`` calls it, so an ``FD_*``
+variable left in a user's environment cannot change what the product computes.  Every bitwise batching invariant
+the GPU suite certifies is certified for these defaults.
+"""
+import ctypes
+import os
+
+from . import lib as L
+
+# host-side path switches (fdhip / FaithDiff modules), name -> default
+HOST_DEFAULTS = {
+    "FD_LN_FOLD": 1,        # LayerNorms folded into the transformer GEMM pairs (0: separate LayerNorm launches)
+    "FD_UNET_GN_EPI": 1,    # UNet GroupNorm statistics from the producing GEMM / conv epilogue
+    "FD_SIDE_STREAM": 0,    # time / add embeddings on a second stream inside the UNet graph (measured slower)
+    "FD_FP8_MFMA": 0,       # use_fp8 model on the e4m3 MFMA (quantize_8bit(fp8_mfma=...) / FaithDiff_pipeline arg)
+    "FD_FP8_MX": 0,         # fp8 model: MX e4m3 activations everywhere
+    "FD_FP8_MX_ATTN": 1,    # fp8 model: MX e4m3 attention outputs only (the measured-fastest form)
+    "FD_FP8_MX_GEGLU": 0,   # fp8 model: MX output straight from the GEGLU epilogue
+    "FD_VAE_NARROW": 0,     # VAE conv_out on the direct narrow kernel (measured no faster)
+    "FD_GRAPHS": 1,         # hipGraph capture / replay of the UNet, VAE and text encoders
+    "FD_TILE_BATCH": 13,    # TLC tiles per UNet forward
+    "FD_CFG_STREAMS": 0,    # UNet forward split into two concurrent row halves after the extras
+}
+_host = dict(HOST_DEFAULTS)
+# string spellings some scripts use for the e4m3 kernel choice
+_F8_KERNEL = {"dma": 1, "reg": 2, "scalar": 3}
+
+
+def _lib_names():
+    out, i = [], 0
+    while True:
+        n = L.load().fd_knob_name(i)
+        if n is None:
+            return out
+        out.append(n.decode())
+        i += 1
+
+
+def names():
+    return list(HOST_DEFAULTS) + _lib_names()
+
+
+def get(name):
+    if name in _host:
+        return _host[name]
+    v, d = ctypes.c_int(), ctypes.c_int()
+    L.check(L.load().fd_get_knob(name.encode(), ctypes.byref(v), ctypes.byref(d)), f"fd_get_knob({name})")
+    return v.value
+
+
+def default(name):
+    if name in HOST_DEFAULTS:
+        return HOST_DEFAULTS[name]
+    v, d = ctypes.c_int(), ctypes.c_int()
+    L.check(L.load().fd_get_knob(name.encode(), ctypes.byref(v), ctypes.byref(d)), f"fd_get_knob({name})")
+    return d.value
+
+
+def set(name, value):  # noqa: A001 -- the table's setter
+    """Set one knob; returns the previous value."""
+    value = int(value)
+    if name in _host:
+        prev, _host[name] = _host[name], value
+        return prev
+    prev = ctypes.c_int()
+    L.check(L.load().fd_set_knob(name.encode(), value, ctypes.byref(prev)), f"fd_set_knob({name})")
+    return prev.value
+
+
+def changed():
+    """Every knob whose current value differs from its default (recorded in bench.py's JSON line)."""
+    return {n: get(n) for n in names() if get(n) != default(n)}
+
+
+class override:
+    """with knobs.override(FD_GEMM256=0): ...  -- restores the previous values on exit."""
+
+    def __init__(self, **kw):
+        self.kw, self.old = kw, {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.old[k] = set(k, _F8_KERNEL.get(v, v) if isinstance(v, str) else v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set(k, v)
+
+
+def apply_env(environ=None):
+    """Measurement scripts only: take FD_<knob>=<int> overrides from the environment; returns what was applied."""
+    environ = os.environ if environ is None else environ
+    done = {}
+    for n in names():
+        if n in environ:
+            v = environ[n]
+            done[n] = _F8_KERNEL[v] if v in _F8_KERNEL else int(v)
+            set(n, done[n])
+    return done

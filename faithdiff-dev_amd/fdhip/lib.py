@@ -85,6 +85,10 @@ _SIGS = {
     "fd_vae_sample_add_noise": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_f, c_f, c_f, c_int, c_int, c_vp]),
     "fd_postprocess_u8": (c_int, [c_vp, c_vp, c_ll, c_int, c_vp]),
     "fd_blend_edge": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "fd_set_knob": (c_int, [c_char_p, c_int, ctypes.POINTER(c_int)]),
+    "fd_get_knob": (c_int, [c_char_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "fd_knob_name": (c_char_p, [c_int]),
+    "fd_reset_knobs": (None, []),
     "fd_device_check": (c_int, []),
     "fd_version": (c_char_p, []),
 }

@@ -21,11 +21,9 @@ MI355X-specific structure (not a translation of the reference's module graph):
     restores them).
 Rows are [tile0 uncond, tile0 cond, tile1 uncond, ...]: several TLC tiles can share one forward.
 """
-import os
-
 import torch
 
-from . import arch
+from . import arch, knobs
 from . import lib as L
 from . import ops
 from .graphs import GraphCache
@@ -49,15 +47,15 @@ class HipUNet:
         # (FD_FP8_MX=1): on one box the C2 step measured 21.00 ms MX vs 20.88 ms per-row (profiles/r03_fp8_ab_*.json):
         # the 140 quantization launches it removes are paid back by the MX GEMMs' per-K-step scale traffic
         # (ff out 23.2 -> 25.0 us, profiles/r03_f8_tiles_mx.jsonl) and the MX epilogues
-        self.fp8_mx = self.fp8_mfma and os.environ.get("FD_FP8_MX", "0") == "1"
+        self.fp8_mx = self.fp8_mfma and knobs.get("FD_FP8_MX") == 1
         # MX output straight from the GEGLU epilogue (forces 256 x 128 tiles; profiles/r03_f8_tiles_mx.jsonl: 48.1 vs
         # 39.7 + a 2048 x 5120 quantization for the 256 x 160 bf16 form); FD_FP8_MX_GEGLU=1 turns it on (A/B)
-        self.fp8_mx_geglu = os.environ.get("FD_FP8_MX_GEGLU", "0") == "1"
+        self.fp8_mx_geglu = knobs.get("FD_FP8_MX_GEGLU") == 1
         # per-row form with MX only where it is free: flash attention writes its output as MX and the out-projections
         # (K = C: the MX GEMM's speed, profiles/r03_f8_tiles_mx.jsonl) read it, removing the two activation
         # quantization launches per block.  C2 step on one box, alternated: 20.57 / 20.57 ms vs 20.65 / 20.67 per-row
         # everywhere vs 20.84 / 20.89 MX everywhere (profiles/r03_fp8_mxattn_ab_*.json).  FD_FP8_MX_ATTN=0: per-row
-        self.fp8_mx_attn = self.fp8_mfma and not self.fp8_mx and os.environ.get("FD_FP8_MX_ATTN", "1") != "0"
+        self.fp8_mx_attn = self.fp8_mfma and not self.fp8_mx and knobs.get("FD_FP8_MX_ATTN") != 0
         self.device, self.dtype = torch.device(device), dtype
         f32 = torch.float32
         W = lambda k: _dev(sd[k], self.device, dtype)  # noqa: E731
@@ -90,9 +88,9 @@ class HipUNet:
                            Fp(p + ".conv_shortcut.bias"))
             return r
 
-        self.ln_fold = os.environ.get("FD_LN_FOLD", "1") != "0" and not self.fp8_mfma
+        self.ln_fold = knobs.get("FD_LN_FOLD") != 0 and not self.fp8_mfma
         # GroupNorm statistics from the producing conv / GEMM epilogue (256-row tiles; FD_UNET_GN_EPI=0: off)
-        self.gn_epi = os.environ.get("FD_UNET_GN_EPI", "1") != "0"
+        self.gn_epi = knobs.get("FD_UNET_GN_EPI") != 0
         self._gn_src = None
         # transformer Linear weights: e4m3 bytes for the fp8 MFMA, else the compute dtype
         LW = (lambda t: ops.pack_e4m3(t.to(self.device))) if self.fp8_mfma else \
@@ -448,7 +446,7 @@ class HipUNet:
         return ops.gemm(semb, self.temb_w, bias=self.temb_b, out_dtype=torch.float32)  # [B, sum C_out]
 
     def _side_stream(self):
-        if os.environ.get("FD_SIDE_STREAM", "0") == "0":
+        if knobs.get("FD_SIDE_STREAM") == 0:
             return None
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)

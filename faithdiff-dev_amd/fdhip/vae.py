@@ -8,11 +8,9 @@ next conv's gather, mid-block single-head d=512 attention with residual.
 The d=512 mid-block attention runs as one flash kernel (fd_flash_attn_d512: online softmax in fp32, QK^T and PV on
 the MFMA, K / V tiles staged through LDS), so no [T, T] score / probability buffer (1.5 GB at T = 16384) exists.
 """
-import os
-
 import torch
 
-from . import arch
+from . import arch, knobs
 from . import lib as L
 from . import ops
 from .graphs import GraphCache
@@ -180,7 +178,7 @@ class HipDecoder:
         # by default the implicit-GEMM path: on one box the decode measured 15.28 / 15.30 ms narrow vs 15.24 / 15.26 ms
         # GEMM (profiles/r03_vae_narrow_ab.txt) -- the direct kernel reads the input once but at two workgroups per
         # CU it is latency-bound at the same ~0.3 ms
-        self.narrow = os.environ.get("FD_VAE_NARROW", "0") == "1"
+        self.narrow = knobs.get("FD_VAE_NARROW") == 1
         self.conv_out32 = (ops.pack_conv3x3(t.sd[t.prefix + "decoder.conv_out.weight"]).float().to(self.device),
                            self.conv_out[1])
         self.graphs = GraphCache()

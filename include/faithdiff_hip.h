@@ -318,6 +318,14 @@ int fd_blend_edge(const void* a, void* b, int Ha, int Wa, int Hb, int Wb, int C,
 int fd_embed_tokens(const int* ids, const void* tok, const void* pos, void* out, int batch, int L, int D, int vocab,
                     int dtype, void* stream);
 
+/* Launch-planner knobs (csrc/knobs.hip): one table of tested defaults compiled into the library, which never reads
+ * the environment.  Tests and measurement scripts switch an entry by name (e.g. "FD_GEMM256" = 0 to compare gemm8
+ * with gemm256 bitwise) and restore it; the product path never calls these.  Unknown name: FD_ERR_ARG. */
+int fd_set_knob(const char* name, int value, int* previous);
+int fd_get_knob(const char* name, int* value, int* dflt);
+const char* fd_knob_name(int id); /* NULL past the last knob */
+void fd_reset_knobs(void);
+
 /* library / device checks */
 int fd_device_check(void);
 const char* fd_version(void);

@@ -13,6 +13,9 @@ import torch  # noqa: E402
 
 from fdhip import lib as L  # noqa: E402
 from fdhip import ops  # noqa: E402
+from fdhip import knobs  # noqa: E402
+
+knobs.apply_env()  # measurement script: FD_* knob overrides from the environment
 
 L.require_device()
 SHAPES = sys.argv[1:] or ["2048x1280x1280", "2048x1280x5120", "2048x3840x1280", "2048x10240x1280:geglu",
@@ -44,20 +47,10 @@ def graph_us(fn):
 
 
 def with_env(env, fn):
-    old = {k: os.environ.get(k) for k in env}
-    for k, v in env.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
-    try:
+    """Graph-time fn with the given planner knobs (None = default)."""
+    kw = {k: knobs.default(k) if v is None else v for k, v in env.items()}
+    with knobs.override(**kw):
         return graph_us(fn)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 dev = "cuda"

@@ -9,6 +9,9 @@ import torch  # noqa: E402
 
 from fdhip import ops  # noqa: E402
 from fdhip import lib as L  # noqa: E402
+from fdhip import knobs  # noqa: E402
+
+knobs.apply_env()  # measurement script: FD_* knob overrides from the environment
 
 L.require_device()
 bf = torch.bfloat16

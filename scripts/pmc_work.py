@@ -74,8 +74,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", choices=("unet", "unet_fp8", "vae", "attn"), required=True)
     a = ap.parse_args()
+    from fdhip import knobs
     from fdhip import lib as L
     from fdhip import ops
+    knobs.apply_env()  # measurement script: FD_* knob overrides from the environment
     L.require_device()
     dev = torch.device("cuda", 0)
     work = {"unet": unet_work, "unet_fp8": lambda d: unet_work(d, fp8=True), "vae": vae_work, "attn": attn_work}

@@ -2,7 +2,7 @@
 # rocprofv3 evidence for one scripts/pmc_work.py workload: a kernel-trace pass (durations), then separate PMC
 # passes (FETCH_SIZE; WRITE_SIZE; SQ group) -- kernel-trace only, never a runtime / sys trace domain, one
 # counter group per pass within the gfx950 slot limits (8 SQ, 4 TCC, 2 GRBM).  Then scripts/pmc_report.py.
-# Usage: scripts/r02_prof.sh <unet|vae|attn> <tag>     (writes gpurun_out/pmc_<what>/ and gpurun_out/<tag>.json)
+# Usage: scripts/prof.sh <unet|vae|attn> <tag>     (writes gpurun_out/pmc_<what>/ and gpurun_out/<tag>.json)
 cd "$(dirname "$0")/.."
 R=$(pwd)
 W=$1; TAG=$2

@@ -13,6 +13,9 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from fdhip import ops  # noqa: E402
+from fdhip import knobs  # noqa: E402
+
+knobs.apply_env()  # measurement script: FD_* knob overrides from the environment
 
 
 def main():

@@ -11,7 +11,7 @@ HDR = os.path.join(ROOT, "include", "faithdiff_hip.h")
 
 def declared_symbols():
     txt = open(HDR).read()
-    return sorted(set(re.findall(r"^(?:int|long long|const char\*)\s+(fd_\w+)\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|long long|const char\*|void)\s+(fd_\w+)\(", txt, flags=re.M)))
 
 
 def test_header_declares_expected_ops():
@@ -56,3 +56,27 @@ def test_gemm_params_struct_matches_header():
     names = re.findall(r"(\w+)(?:,|;)", re.sub(r"/\*.*?\*/", "", body, flags=re.S))
     names = [n for n in names if n not in ("void", "int", "float", "long", "const")]
     assert [f[0] for f in lib.GemmParams._fields_] == names
+
+
+def test_knob_table_defaults_and_no_environment_reads():
+    """The planner knobs are one compiled-in table (csrc/knobs.hip + fdhip/knobs.py): set / restore through the C ABI,
+    no getenv in the library, no FD_* environment read in the product's host code (only measurement scripts call
+    knobs.apply_env)."""
+    from fdhip import knobs
+    from fdhip import lib
+    assert knobs.changed() == {}
+    with knobs.override(FD_GEMM256=0, FD_F8_KERNEL="dma", FD_LN_FOLD=0):
+        assert knobs.changed() == {"FD_GEMM256": 0, "FD_F8_KERNEL": 1, "FD_LN_FOLD": 0}
+    assert knobs.changed() == {}
+    assert lib.load().fd_set_knob(b"FD_NO_SUCH_KNOB", 1, None) != 0
+    assert knobs.apply_env({"FD_GEMM8_MIDK": "2", "UNRELATED": "1"}) == {"FD_GEMM8_MIDK": 2}
+    lib.load().fd_reset_knobs()
+    assert knobs.get("FD_GEMM8_MIDK") == knobs.default("FD_GEMM8_MIDK") == 3
+    data = open(lib.LIB_PATH, "rb").read()
+    assert b"getenv" not in data
+    pkg = os.path.join(ROOT, "faithdiff-dev_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py") and f != "knobs.py":
+                txt = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"environ(\.get)?[\[(]\s*[\"']FD_(?!LIB_PATH)", txt), f

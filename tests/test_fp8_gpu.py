@@ -152,27 +152,20 @@ def test_gemm_e4m3_geglu(M, F, K):
 
 
 class _env:
-    """Temporarily set environment knobs the C ABI reads per call (FD_F8_KERNEL, FD_F8_TILE)."""
+    """Temporarily switch the library's planner knobs (fdhip.knobs; FD_F8_KERNEL, FD_F8_TILE); None = the default."""
 
     def __init__(self, **kw):
-        self.kw = kw
+        from fdhip import knobs
+        self.kw = {k: knobs.default(k) if v is None else (v if v in ("dma", "reg", "scalar") else int(v))
+                   for k, v in kw.items()}
 
     def __enter__(self):
-        import os
-        self.old = {k: os.environ.get(k) for k in self.kw}
-        for k, v in self.kw.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = str(v)
+        from fdhip import knobs
+        self.ctx = knobs.override(**self.kw)
+        self.ctx.__enter__()
 
     def __exit__(self, *a):
-        import os
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        self.ctx.__exit__(*a)
 
 
 @pytest.mark.parametrize("tile", ["256160", "256128", "128160", "64160", None])
@@ -342,18 +335,11 @@ def _fp8_pair():
 def _fp8_mx_unet():
     """The same e4m3 weights with MX activations (FD_FP8_MX=1: LayerNorm / flash attention write MX e4m3)."""
     if "mx" not in _FP8:
-        import os
         from fdhip.unet import HipUNet
         _fp8_pair()
-        old = os.environ.get("FD_FP8_MX")
-        os.environ["FD_FP8_MX"] = "1"
-        try:
+        from fdhip import knobs
+        with knobs.override(FD_FP8_MX=1):
             _FP8["mx"] = HipUNet(_FP8["sd"], "cuda", torch.bfloat16, fp8_mfma=True)
-        finally:
-            if old is None:
-                os.environ.pop("FD_FP8_MX", None)
-            else:
-                os.environ["FD_FP8_MX"] = old
         assert _FP8["mx"].fp8_mx
     return _FP8["mx"]
 

@@ -1,7 +1,6 @@
 """The 256 x 256-tile GEMM / implicit-GEMM conv (csrc/gemm256.hip) that fd_gemm takes for large-M launches with
 N % 256 == 0 (the VAE's 256- / 512-channel convs): against fp32 torch, and bitwise against the 256 x 128 kernel
-(gemm8, one split) on the same launch (FD_GEMM256=0) -- both sum K in the same 32-deep order."""
-import os
+(gemm8, one split) on the same launch (knob FD_GEMM256 = 0) -- both sum K in the same 32-deep order."""
 
 import pytest
 import torch
@@ -15,13 +14,10 @@ DEV = "cuda"
 
 
 def both(fn):
-    os.environ["FD_GEMM256"] = "1"
-    try:
-        a = fn().clone()
-        os.environ["FD_GEMM256"] = "0"
+    from fdhip import knobs
+    a = fn().clone()
+    with knobs.override(FD_GEMM256=0):
         b = fn().clone()
-    finally:
-        os.environ["FD_GEMM256"] = "1"
     torch.cuda.synchronize()
     return a, b
 

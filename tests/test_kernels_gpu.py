@@ -442,7 +442,8 @@ def test_conv_groupnorm_statistics_from_epilogue(nimg, H, W, Cin, Cout, up, expe
     if expect is not None:
         assert st.done == expect
     if st.done:
-        routed = os.environ.get("FD_GEMM8_N128", "0") != "0" and Cout == 128 and nimg * Ho * Wo >= 262144
+        from fdhip import knobs
+        routed = knobs.get("FD_GEMM8_N128") != 0 and Cout == 128 and nimg * Ho * Wo >= 262144
         assert st.rows == (128 if routed else 256)
     g, be = torch.randn(Cout, device=DEV), torch.randn(Cout, device=DEV)
     got = ops.group_norm(y, g, be, nimg, Ho * Wo, Cout, 32, 1e-6, silu=True, stats=st)
