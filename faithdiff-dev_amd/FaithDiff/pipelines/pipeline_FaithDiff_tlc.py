@@ -147,13 +147,15 @@ class FaithDiffStableDiffusionXLPipeline:
         self.vae.disable_tiling()
         self.denoise_encoder.disable_tiling()
 
-    def enable_tile_parallel(self, group=None):
+    def enable_tile_parallel(self, group=None, sync_weights=True):
         """Shard TLC tiles over the ranks of `group` (default WORLD) with one all-gather per step; the tiled VAE
         encode / decode and the tiled denoise encoder shard their tiles the same way (fdhip.tiling.map_tiles).
-        First makes every rank's weights rank 0's (broadcast_weights), unless the pipeline was built or synced over
-        this group already: the tiles of one image must all see the same model."""
+        The tiles of one image must all see the same model: with ``sync_weights`` (default) every rank's weights
+        first become rank 0's (broadcast_weights) unless the pipeline was built or synced over this group already.
+        ``sync_weights=False`` skips that transfer for callers that loaded the same checkpoint on every rank (the
+        reference flow: each process reads the same files) -- their weights are already equal."""
         self.process_group = group if group is not None else dist.group.WORLD
-        if self._weights_group is not self.process_group:
+        if sync_weights and self._weights_group is not self.process_group:
             self.broadcast_weights(self.process_group)
         for m in (self.vae, self.denoise_encoder):
             if m is not None:
@@ -174,14 +176,20 @@ class FaithDiffStableDiffusionXLPipeline:
             self._weights_group, self.last_broadcast_bytes = group, 0
             return 0
         dev = staging_device(group)
+        # every rank must still hold every component's host weights; agree on it collectively first, so that a
+        # rank that released them (release_host_weights) makes ALL ranks raise instead of leaving the others
+        # blocked in a broadcast it never joins
+        owners = [(name, m, getattr(m, "_sd", None)) for name, m in self._weight_owners()]
+        released = [name for name, _, sd in owners if sd is not None and not sd]
+        flag = torch.tensor([len(released)], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, group=group)
+        if int(flag.item()):
+            raise RuntimeError("broadcast_weights: host weights were released (release_host_weights) before they "
+                               f"were synchronised over the group (this rank: {released or 'none'})")
         total = 0
-        for name, m in self._weight_owners():
-            sd = getattr(m, "_sd", None)
+        for name, m, sd in owners:
             if sd is None:
                 continue
-            if not sd:
-                raise RuntimeError(f"broadcast_weights: the {name} host weights were released "
-                                   "(release_host_weights) before they were synchronised over the group")
             total += broadcast_state_dict(sd, group, src, device=dev)
             for attr in ("_hip", "_enc", "_dec"):
                 if getattr(m, attr, None) is not None:

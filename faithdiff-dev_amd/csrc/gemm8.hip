@@ -1268,7 +1268,11 @@ extern "C" int fd_gemm_mxe4m3(const void* A8, long long lda, const void* a_bs, l
   if (out_dtype != FD_BF16 && out_dtype != FD_F16 && out_dtype != FD_F32 && out_dtype != FD_MXE4M3) return FD_ERR_DTYPE;
   const bool mx_out = out_dtype == FD_MXE4M3;
   if (residual && (ldr < nout || out_dtype == FD_F32 || mx_out)) return FD_ERR_SHAPE;
-  if (mx_out && (!c_bs || ldcs < nout / 32 || ldc % 8 || ((unsigned long long)C & 7))) return FD_ERR_SHAPE;
+  // an MX output is written only by the interior 16-B vector epilogue: C (and the bias it reads as vectors unless
+  // GEGLU) must be 16-B aligned, or a tile would be planned that writes nothing
+  if (mx_out && (!c_bs || ldcs < nout / 32 || ldc % 16 || ((unsigned long long)C & 15) ||
+                 (act != FD_ACT_GEGLU && bias && ((unsigned long long)bias & 15))))
+    return FD_ERR_SHAPE;
   fd_gemm_params p{};
   p.A = A8;
   p.B = W8;

@@ -342,6 +342,8 @@ def gemm_mx(a, w8, out=None, bias=None, residual=None, w_scale=1.0, act="none", 
     mx_out = isinstance(out, MX) or out_dtype == "mx"
     if out is None:
         out = MX(M, nout, a.q.device) if mx_out else torch.empty((M, nout), dtype=out_dtype, device=a.q.device)
+    if mx_out and residual is not None:
+        raise ValueError("gemm_mx: an MX output takes no residual (the C entry point rejects it too)")
     if mx_out and not _mx_out_tiles(M, nout, act == "geglu"):
         # no tile shape covers this output with whole 32-column blocks (small test sizes): the fp32 output, then
         # fd_quant_rows_mx -- the same bytes the fused epilogue writes (it quantizes the same fp32 values)

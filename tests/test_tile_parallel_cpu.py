@@ -179,3 +179,46 @@ def test_enable_tile_parallel_broadcasts_rank0_weights():
     assert b0 != b1, "the ranks were meant to start from different weights"
     assert set(d0) == {"unet", "vae", "denoise_encoder", "text_encoder", "text_encoder_2"}
     assert d0 == d1 and n0 == n1 > 10e9 and t0 and t1
+
+
+def _release_worker(rank, world, port, q):
+    """broadcast_weights on a bare pipeline whose components hold small host state dicts; rank 1 has released
+    its UNet weights.  Every rank must raise (a collective agreement first), none may block in the broadcast."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from types import SimpleNamespace
+
+        from FaithDiff.pipelines.pipeline_FaithDiff_tlc import FaithDiffStableDiffusionXLPipeline as P
+        pipe = object.__new__(P)
+        unet = SimpleNamespace(_sd={} if rank == 1 else {"w": torch.full((4,), float(rank))})
+        vae = SimpleNamespace(_sd={"v": torch.full((3,), float(rank))})
+        pipe._weight_owners = lambda: [("unet", unet), ("vae", vae)]
+        pipe._weights_group = None
+        try:
+            pipe.broadcast_weights(dist.group.WORLD)
+            q.put((rank, "no error"))
+        except RuntimeError as e:
+            q.put((rank, "raised" if "released" in str(e) else str(e)))
+        # sync_weights=False: no transfer (each rank keeps its own, e.g. identical checkpoint loads)
+        unet._sd = {"w": torch.full((4,), float(rank))}
+        pipe.vae = pipe.denoise_encoder = None
+        pipe.enable_tile_parallel(sync_weights=False)
+        q.put((rank, float(unet._sd["w"][0])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_weights_released_raises_on_every_rank_and_sync_opt_out():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_release_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(4)], key=lambda r: (r[0], isinstance(r[1], float)))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert res == [(0, "raised"), (0, 0.0), (1, "raised"), (1, 1.0)]
