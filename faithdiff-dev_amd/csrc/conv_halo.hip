@@ -1,0 +1,460 @@
+// 3x3 stride-1 convolution on a halo-staged input patch, with the consumer GroupNorm (+ SiLU) applied in the
+// staging pass (gfx950).
+//
+// Why: the implicit-GEMM conv (gemm8 / gemm256) gathers its A operand per tap, so every input pixel crosses the
+// CU's L2 -> LDS path 9 times (once per tap) -- at the UNet's 128^2 / 64^2 levels and in the VAE that stream, not the
+// MFMA pipe, bounds the convs (conv counter traffic ~2.3x the activations + weights) -- and the
+// GroupNorm (+ SiLU) in front of every resnet conv is a separate read + write pass of the activation.  Here a
+// workgroup owns a TH x 16 output-pixel tile and BN output channels; per 64-channel chunk it stages the
+// (TH + 2) x 18 input patch into LDS ONCE (1.27x / 1.41x the tile's pixels instead of 9x), applies the GroupNorm
+// affine (+ SiLU) to the staged values in place (once per element per workgroup, not per tap and wave), and runs
+// the chunk's 9 taps as 9 MFMA K steps that read shifted windows of the patch.  Weights stream through a 3-deep
+// LDS ring of (tap, chunk) stages as in gemm8.
+//
+// Roles: waves 0-3 DMA the weight stages (global_load_lds, counted vmcnt); waves 4-7 DMA the patches (two patch
+// buffers: chunk c + 2 is issued right after the last read of chunk c, waited for 8 steps later); all 8 waves
+// compute (4 x 2 waves of (TH * 4) x (BN / 2)).  Out-of-image pixels come from a zero page and are written as zero
+// by the affine pass (the reference pads the normalised activation, not the raw one).
+//
+// Numerics: the staged values are exactly the bf16 / fp16 values fd_group_norm would store (same fma, SiLU and
+// rounding), and the sum over K runs chunk by chunk, tap by tap inside the chunk -- per output element the same
+// order whatever the tile shape (TH 16 or 8, BN 160 or 128), so tile choices never change a bit; it differs from
+// the implicit GEMM's tap-major order (not bitwise equal to gemm8, tested against fp32).
+#include "fd_common.h"
+
+__device__ __attribute__((aligned(256))) unsigned char g_zero_halo[256];
+
+namespace {
+
+template <int N>
+__device__ __forceinline__ void hvm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr int PW = 18;  // patch width: 16 output columns + halo
+constexpr int TR = 7;   // tap of chunk c at which chunk c + 1's patch is waited for and transformed
+
+template <typename T, int TH, int BN, bool GNI>
+__global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p) {
+  typedef typename VecT<T>::v8 V8;
+  typedef __attribute__((ext_vector_type(8))) T TO8;
+  constexpr int BM = TH * 16;
+  constexpr int PIX = (TH + 2) * PW;
+  constexpr int PIXR = (PIX + 7) / 8 * 8;
+  constexpr int PATCH = PIXR * 128;
+  constexpr int AFF = GNI ? 1024 : 0;  // the chunk's 64 affine pairs (512 B, DMA'd as 1 KB) after each patch
+  constexpr int PBUF = PATCH + AFF;
+  constexpr int NS = 3;
+  constexpr int STAGE = BN * 128;
+  constexpr int RING = 2 * PBUF;
+  constexpr int SMEM_MAIN = RING + NS * STAGE;
+  constexpr int WM = BM / 4, WN = BN / 2;
+  constexpr int MT = WM / 16, NT = WN / 16;
+  constexpr int B_TOT = BN / 8, PER_B = B_TOT / 4;
+  static_assert(B_TOT % 4 == 0, "B stage split over 4 waves");
+  constexpr int P_TOT = PIXR / 8, P_I = (P_TOT + 3) / 4;
+  constexpr int EROWS = 128, LDE = BN + 4, EPB = EROWS * LDE * 4, VPR = BN / 8;
+  constexpr int SLOT = EPB, RED = SLOT + EROWS * VPR * 16;
+  constexpr int SMEM_EPI = RED + 512 * 8;
+  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  static_assert(SMEM <= 163840, "LDS");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int Ho = p.Hout, Wo = p.Wout, Cin = p.Cin, N = p.N;
+  const int tiles_x = (Wo + 15) / 16, tiles_y = (Ho + TH - 1) / TH;
+  const int nsp = p.nimg * tiles_y * tiles_x;
+  // tile order: XCD-contiguous chunks (bijective remap), output-channel tiles outer, so the ~32 workgroups an XCD
+  // runs at once share one weight panel in its L2
+  const int pid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nt = pid / nsp, sp = pid - nt * nsp;
+  const int img = sp / (tiles_y * tiles_x), spi = sp - img * (tiles_y * tiles_x);
+  const int tyt = spi / tiles_x, txt = spi - tyt * tiles_x;
+  const int y0 = tyt * TH, x0 = txt * 16, n0 = nt * BN;
+  const int nch = Cin / 64, nsteps = 9 * nch;
+  const T* __restrict__ A = (const T*)p.A;
+  const T* __restrict__ Bw = (const T*)p.B;
+  const bool up2 = p.upsample && Ho == 2 * p.Hin && Wo == 2 * p.Win;
+
+  // ---- weight stages (waves 0-3): rows n0 + (w + 4 i) * 8 + lane / 8, source-side XOR swizzle of 128-B rows
+  const T* b_row[PER_B];
+  const T* p_src[P_I];  // patch pixels (waves 4-7): this lane's source 16-B chunk at channel 0, nullptr = outside
+  if (w < 4) {
+#pragma unroll
+    for (int i = 0; i < PER_B; ++i) {
+      const int row = (w + 4 * i) * 8 + (lane >> 3);
+      b_row[i] = Bw + (long long)(n0 + row) * p.ldb + (((lane & 7) ^ ((row >> 1) & 7)) * 8);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < P_I; ++i) {
+      const int j = (w - 4) + 4 * i;
+      const int pix = j * 8 + (lane >> 3);
+      const int py = pix / PW, px = pix - (pix / PW) * PW;
+      const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+      const bool ok = j < P_TOT && pix < PIX && iy >= 0 && iy < Ho && ix >= 0 && ix < Wo;
+      int sy = iy, sx = ix;
+      if (p.upsample) {
+        sy = up2 ? (iy >> 1) : (iy * p.Hin) / Ho;
+        sx = up2 ? (ix >> 1) : (ix * p.Win) / Wo;
+      }
+      p_src[i] = ok ? A + ((long long)(img * p.Hin + sy) * p.Win + sx) * p.lda + (((lane & 7) ^ ((pix >> 1) & 7)) * 8)
+                    : nullptr;
+    }
+  }
+  const float* __restrict__ aff = GNI ? (const float*)p.gi_affine + (long long)img * Cin * 2 : nullptr;
+
+  auto stage_b = [&](int s, int rb) {
+    const int c = s / 9, t = s - (s / 9) * 9;
+    const int off = t * Cin + c * 64;
+    unsigned char* dst = smem + RING + rb * STAGE;
+#pragma unroll
+    for (int i = 0; i < PER_B; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + off), LDS_PTR(dst + (w + 4 * i) * 1024), 16, 0, 0);
+  };
+  auto stage_p = [&](int c) {  // patch of chunk c into buffer c & 1 (+ its affine table)
+    unsigned char* dst = smem + (c & 1) * PBUF;
+#pragma unroll
+    for (int i = 0; i < P_I; ++i) {
+      const int j = (w - 4) + 4 * i;
+      if (j < P_TOT) {
+        const void* s = p_src[i] ? (const void*)(p_src[i] + c * 64) : (const void*)g_zero_halo;
+        __builtin_amdgcn_global_load_lds(s, LDS_PTR(dst + j * 1024), 16, 0, 0);
+      }
+    }
+    if (GNI && w == 4)  // 64 channels x (scale, shift) = 512 B; the upper half of the 1 KB is never read
+      __builtin_amdgcn_global_load_lds((const void*)(aff + (long long)c * 128 + lane * 4), LDS_PTR(dst + PATCH), 16, 0,
+                                       0);
+  };
+  // GroupNorm affine (+ SiLU) in place on patch buffer c & 1: y = silu(fma(x, a, b)) rounded to T (fd_group_norm's
+  // bits), zero outside the image.  Each thread keeps one logical 8-channel slot (tid % 8) for every pixel.
+  auto transform = [&](int c) {
+    unsigned char* buf = smem + (c & 1) * PBUF;
+    const int lc = tid & 7;
+    const float* ab = (const float*)(buf + PATCH) + lc * 16;
+    float a[8], b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a[i] = ab[2 * i];
+      b[i] = ab[2 * i + 1];
+    }
+    const bool silu = p.gi_silu != 0;
+    constexpr int IT = (PIX * 8 + 511) / 512;
+    V8 xs[IT];  // every read issued before the first write (one LDS round trip, not IT)
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int pix = (tid + it * 512) >> 3;
+      if (pix < PIX) xs[it] = *(const V8*)(buf + pix * 128 + ((lc ^ ((pix >> 1) & 7)) << 4));
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int pix = (tid + it * 512) >> 3;
+      if (pix < PIX) {
+        const int py = pix / PW, px = pix - (pix / PW) * PW;
+        const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+        const bool ok = iy >= 0 && iy < Ho && ix >= 0 && ix < Wo;
+        V8 y;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float f = __builtin_fmaf((float)xs[it][i], a[i], b[i]);
+          if (silu) f = silu_f(f);
+          y[i] = ok ? (T)f : (T)0.f;
+        }
+        *(V8*)(buf + pix * 128 + ((lc ^ ((pix >> 1) & 7)) << 4)) = y;
+      }
+    }
+  };
+  auto read_frags = [&](int c, int t, int rb, int h, V8 (&af)[MT], V8 (&bf)[NT]) {
+    const unsigned char* pa = smem + (c & 1) * PBUF;
+    const unsigned char* sb = smem + RING + rb * STAGE;
+    const int ky = t / 3, kx = t - (t / 3) * 3;
+    const int ch = h * 4 + fg;
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const int pix = (wm * MT + mi + ky) * PW + fr + kx;
+      af[mi] = *(const V8*)(pa + pix * 128 + ((ch ^ ((pix >> 1) & 7)) << 4));
+    }
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni) {
+      const int r = wn * WN + ni * 16 + fr;
+      bf[ni] = *(const V8*)(sb + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+    }
+  };
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const V8 (&af)[MT], const V8 (&bf)[NT]) {
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = mfma16x16x32(af[mi], bf[ni], acc[mi][ni]);
+  };
+  // B-waves: all but the youngest `ahead` weight stages landed (ahead <= 2)
+  auto wait_b = [&](int ahead) {
+    if (ahead >= 2) hvm<2 * PER_B>();
+    else if (ahead == 1) hvm<PER_B>();
+    else hvm<0>();
+  };
+
+  // ---- prologue: weight stages 0..NS-1, patches of chunks 0 and 1
+  if (w < 4) {
+#pragma unroll
+    for (int s0 = 0; s0 < NS; ++s0)
+      if (s0 < nsteps) stage_b(s0, s0);
+    wait_b(min(nsteps, NS) - 1);
+  } else {
+    stage_p(0);
+    if (nch > 1) stage_p(1);
+    hvm<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  if (GNI) {
+    transform(0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+  }
+
+  V8 a0[MT], b0[NT], a1[MT], b1[NT];
+  read_frags(0, 0, 0, 0, a0, b0);
+  int c = 0, t = 0, rb = 0;
+  for (int s = 0; s < nsteps - 1; ++s) {
+    read_frags(c, t, rb, 1, a1, b1);
+    mma(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (w < 4) wait_b(min(NS - 2, nsteps - 2 - s));  // stage s + 1 landed
+    else if (t == TR) hvm<0>();                       // chunk c + 1's patch landed
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+    if (w < 4) {
+      if (s + NS < nsteps) stage_b(s + NS, rb);
+    } else if (t == 8 && c + 2 < nch) {
+      stage_p(c + 2);  // buffer c & 1: its last reads (this step's half 1) are behind the barrier
+    }
+    if (GNI && t == TR && c + 1 < nch) transform(c + 1);  // visible to the readers after step (c, 8)'s barrier
+    rb = rb == NS - 1 ? 0 : rb + 1;
+    if (t == 8) {
+      ++c;
+      t = 0;
+    } else {
+      ++t;
+    }
+    read_frags(c, t, rb, 0, a0, b0);
+    mma(a1, b1);
+  }
+  read_frags(c, t, rb, 1, a1, b1);
+  mma(a0, b0);
+  mma(a1, b1);
+
+  // ---- epilogue: two (TH = 16) or one 128-row passes through LDS fp32 [128][BN + 4]; each thread then owns 8
+  // consecutive columns of a row: bias, per-image row bias (time embedding), activation, residual, one 16-B store;
+  // GroupNorm output statistics (gn_part) folded per group in a fixed order.
+  T* __restrict__ C = (T*)p.C;
+  const T* __restrict__ R = (const T*)p.residual;
+  const float* __restrict__ bias = p.bias;
+  const float* __restrict__ rbias = p.rowbias;
+  const float alpha = p.alpha;
+  const int act = p.act;
+  float* ep = (float*)smem;
+  f32x4* const slots = (f32x4*)(smem + SLOT);
+  const bool gn = p.gn_part != nullptr;
+  const int cpg = gn ? N / p.gn_groups : 8;
+  const int G = BN / cpg, TPG = gn ? 512 / G : 512;
+  const int gg = tid / TPG, gj = tid - (tid / TPG) * TPG;
+  float gs = 0.f, gq = 0.f;
+#pragma unroll 1
+  for (int half = 0; half < BM / EROWS; ++half) {
+    __syncthreads();  // the ring / patches (half 0) or the previous half's staging (half 1) fully consumed
+    if ((wm * WM) / EROWS == half) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        const int rl = wm * WM + mi * 16 + fg * 4 - half * EROWS;
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) {
+          const int col = wn * WN + ni * 16 + fr;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ep[(rl + j) * LDE + col] = acc[mi][ni][j] * alpha;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int e = tid; e < EROWS * VPR; e += 512) {
+      const int r = e / VPR, cv = e - (e / VPR) * VPR;
+      const int rt = half * EROWS + r;
+      const int oy = y0 + (rt >> 4), ox = x0 + (rt & 15);
+      const bool ok = oy < Ho && ox < Wo;
+      const long long m = ((long long)img * Ho + oy) * Wo + ox;
+      const int n = n0 + cv * 8;
+      float v[8], bv[8], rv[8];
+      TO8 res;
+      *(f32x4*)&v[0] = *(const f32x4*)(ep + r * LDE + cv * 8);
+      *(f32x4*)&v[4] = *(const f32x4*)(ep + r * LDE + cv * 8 + 4);
+      if (bias) {
+        *(f32x4*)&bv[0] = *(const f32x4*)(bias + n);
+        *(f32x4*)&bv[4] = *(const f32x4*)(bias + n + 4);
+      }
+      if (rbias) {
+        const float* rr = rbias + (long long)(m / p.rows_per_group) * p.rowbias_ld + n;
+        *(f32x4*)&rv[0] = *(const f32x4*)rr;
+        *(f32x4*)&rv[4] = *(const f32x4*)(rr + 4);
+      }
+      if (R && ok) res = *(const TO8*)(R + m * p.ldr + n);
+      if (bias) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += bv[i];
+      }
+      if (rbias) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += rv[i];
+      }
+      if (act != FD_ACT_NONE) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = act_f(v[i], act);
+      }
+      if (R && ok) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += (float)res[i];
+      }
+      TO8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (T)v[i];
+      if (ok) *(TO8*)(C + m * p.ldc + n) = o;
+      if (gn) {  // (sum, sumsq) of the stored values, split at the group boundary inside the chunk
+        const int split = ((cv * 8) / cpg + 1) * cpg - cv * 8;
+        float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float f = (float)o[i];
+          if (i < split) {
+            s0 += f;
+            q0 += f * f;
+          } else {
+            s1 += f;
+            q1 += f * f;
+          }
+        }
+        slots[e] = (f32x4){s0, q0, s1, q1};
+      }
+    }
+    if (gn) {  // thread (group gg, j) folds rows j, j + TPG, ... of its group, chunks in column order
+      __syncthreads();
+      const int cc0 = (gg * cpg) / 8, cc1 = ((gg + 1) * cpg - 1) / 8;
+      for (int r = gj; r < EROWS; r += TPG)
+        for (int cc = cc0; cc <= cc1; ++cc) {
+          const f32x4 v4 = slots[r * VPR + cc];
+          const bool first = (cc * 8) / cpg == gg;
+          gs += first ? v4[0] : v4[2];
+          gq += first ? v4[1] : v4[3];
+        }
+    }
+  }
+  if (gn) {
+    float2* red = (float2*)(smem + RED);
+    red[tid] = make_float2(gs, gq);
+    __syncthreads();
+    if (tid < G) {
+      float S = 0.f, Q = 0.f;
+      for (int k = 0; k < TPG; ++k) {
+        const float2 v2 = red[tid * TPG + k];
+        S += v2.x;
+        Q += v2.y;
+      }
+      const long long blk = (long long)img * (tiles_y * tiles_x) + spi;
+      ((float2*)p.gn_part)[blk * p.gn_groups + n0 / cpg + tid] = make_float2(S, Q);
+    }
+  }
+}
+
+struct HaloPlan {
+  int th, bn, tiles;
+};
+
+// Eligibility and tile plan, from per-image quantities only (m_ref: rows of one TLC tile's forward), so batching
+// tiles never moves a launch between this kernel and the implicit GEMM (bitwise batch invariance).
+int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
+  if (!fd_knob(FDK_CONV_HALO)) return 0;
+  if (!p->conv || p->batch > 1 || p->stride != 1 || p->pad != 1 || p->A2 || p->K != 9 * p->Cin) return 0;
+  if (p->Cin % 64 || p->lda < p->Cin || p->lda % 8 || p->ldb % 8 || p->ldc % 8) return 0;
+  if (p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out || p->dtype != p->out_dtype || p->dtype == FD_F32) return 0;
+  if (p->residual && p->ldr % 8) return 0;
+  if (p->rowbias && p->rowbias_ld % 4) return 0;
+  const unsigned long long al = (unsigned long long)p->A | (unsigned long long)p->B | (unsigned long long)p->C |
+                                (unsigned long long)(p->residual ? p->residual : nullptr) |
+                                (unsigned long long)(p->bias ? p->bias : nullptr) |
+                                (unsigned long long)(p->rowbias ? p->rowbias : nullptr) |
+                                (unsigned long long)(p->gi_affine ? p->gi_affine : nullptr);
+  if (al & 15) return 0;
+  if (p->upsample == 0 && (p->Hin != p->Hout || p->Win != p->Wout)) return 0;
+  const int bn = p->N % 160 == 0 ? 160 : (p->N % 128 == 0 ? 128 : 0);
+  if (!bn) return 0;
+  const long long hw = (long long)p->Hout * p->Wout;
+  const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
+  const long long nimg_ref = m_ref / hw > 0 ? m_ref / hw : 1;
+  auto tiles = [&](int th) { return nimg_ref * ((p->Hout + th - 1) / th) * ((p->Wout + 15) / 16) * (p->N / bn); };
+  const int min_tiles = fd_knob(FDK_CONV_HALO_MIN_TILES);
+  int th = 0;
+  if (tiles(16) >= min_tiles) th = 16;
+  else if (tiles(8) >= min_tiles) th = 8;
+  if (!th || p->Wout < 16 || p->Hout < th) return 0;
+  pl->th = th;
+  pl->bn = bn;
+  pl->tiles = (int)(p->nimg * ((p->Hout + th - 1) / th) * ((p->Wout + 15) / 16) * (p->N / bn));
+  return 1;
+}
+
+template <typename T>
+int launch_halo(const fd_gemm_params* p, const HaloPlan& pl, hipStream_t s) {
+  const bool gi = p->gi_affine != nullptr;
+#define FD_HALO(TH_, BN_)                                                                                           \
+  if (pl.th == TH_ && pl.bn == BN_) {                                                                               \
+    if (gi)                                                                                                         \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true>), dim3(pl.tiles), dim3(512), 0, s, *p);               \
+    else                                                                                                            \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false>), dim3(pl.tiles), dim3(512), 0, s, *p);              \
+    FD_LAUNCH_CHECK();                                                                                              \
+    return FD_OK;                                                                                                   \
+  }
+  FD_HALO(16, 160)
+  FD_HALO(16, 128)
+  FD_HALO(8, 160)
+  FD_HALO(8, 128)
+#undef FD_HALO
+  return FD_ERR_ARG;
+}
+
+}  // namespace
+
+// Rows per GroupNorm-statistics block this conv would write (256 / 128), 0 = the halo kernel does not take it.
+extern "C" int fd_conv_halo_plan(const fd_gemm_params* p) {
+  HaloPlan pl;
+  if (!halo_plan(p, &pl)) return 0;
+  return pl.th * 16;
+}
+
+// Called by fd_gemm for every conv: 1 = launched here, 0 = not eligible (the implicit GEMM takes it), < 0 = error.
+// gn_part is honoured when the tiles are whole (H % TH == 0, W % 16 == 0, N a multiple of the group width and of
+// the tile's groups); p->gn_done reports it.  gi_affine (the consumer GroupNorm) requires this kernel: an ineligible
+// conv with gi_affine set is FD_ERR_SHAPE (callers ask fd_conv_halo_plan first).
+extern "C" int fd_conv_halo_try(fd_gemm_params* p, void* stream) {
+  HaloPlan pl;
+  if (!halo_plan(p, &pl)) return p->gi_affine ? FD_ERR_SHAPE : 0;
+  fd_gemm_params q = *p;
+  p->gn_done = 0;
+  if (q.gn_part) {
+    const int cpg = q.gn_groups > 0 ? q.N / q.gn_groups : 0;
+    const bool ok = q.gn_groups > 0 && q.N % q.gn_groups == 0 && cpg >= 4 && pl.bn % cpg == 0 &&
+                    512 % (pl.bn / cpg) == 0 && q.Hout % pl.th == 0 && q.Wout % 16 == 0 &&
+                    q.gn_hw == q.Hout * q.Wout && q.M == q.nimg * q.gn_hw;
+    if (!ok) q.gn_part = nullptr;
+  }
+  int rc;
+  if (q.dtype == FD_BF16) rc = launch_halo<bf16>(&q, pl, (hipStream_t)stream);
+  else rc = launch_halo<f16>(&q, pl, (hipStream_t)stream);
+  if (rc == FD_OK && q.gn_part) p->gn_done = pl.th * 16;
+  return rc == FD_OK ? 1 : rc;
+}

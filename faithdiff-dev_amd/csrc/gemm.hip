@@ -717,6 +717,13 @@ extern "C" int fd_gemm(fd_gemm_params* p, void* stream) {
                     (p->out_dtype != FD_BF16 && p->out_dtype != FD_F16)))
     return FD_ERR_SHAPE;
   if (p->ln_in && (p->K % 320 || p->K > 1280 || p->batch > 1 || p->conv || !p->ln_c)) return FD_ERR_SHAPE;
+  if (p->conv) {  // 3x3 stride-1 convs: the halo-staged kernel where it applies (the only one taking gi_affine)
+    const int rh = fd_conv_halo_try(p, stream);
+    if (rh < 0) return rh;
+    if (rh == 1) return FD_OK;
+  } else if (p->gi_affine) {
+    return FD_ERR_ARG;
+  }
   if (!p->ln_out) {
     const int r256 = fd_gemm256_try(p, stream);  // large-M, N % 256 == 0: 256 x 256 tiles
     if (r256 < 0) return r256;

@@ -43,6 +43,8 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_FLASH_SWZ", 1},           // flash attention XCD-aware block order
     {"FD_FLASH_WAVES", 4},         // flash attention waves per workgroup (2, 4, 8)
     {"FD_FLASH_QPW", 0},           // flash attention queries per wave (0: by launch size, 16, 32)
+    {"FD_CONV_HALO", 1},           // 3x3 stride-1 convs on the halo-staged kernel where eligible
+    {"FD_CONV_HALO_MIN_TILES", 192},  // ... when it has at least this many tiles (per TLC tile's rows, m_ref)
 };
 int g_knobs[FDK_COUNT];
 bool g_init = false;

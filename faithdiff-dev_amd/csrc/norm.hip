@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
     const int g = c / cpg;
     const float a = rstd_s[g] * (gamma ? gamma[c] : 1.f);
     sc[c] = a;
-    sh[c] = (beta ? beta[c] : 0.f) - mean_s[g] * a;
+    sh[c] = __builtin_fmaf(-mean_s[g], a, beta ? beta[c] : 0.f);
   }
   __syncthreads();
   for (; e < e1; e += 256 * U) {
@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
       V8 out;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float f = (float)val[u][i] * sc[v * 8 + i] + sh[v * 8 + i];
+        float f = __builtin_fmaf((float)val[u][i], sc[v * 8 + i], sh[v * 8 + i]);
         if (silu) f = silu_f(f);
         out[i] = (T)f;
       }
@@ -295,7 +295,7 @@ __global__ void __launch_bounds__(256) gn_apply2_kernel(const T* __restrict__ x,
     const float2 st = stats[img * groups + g];
     const float a = st.y * (gamma ? gamma[c] : 1.f);
     sc[i] = a;
-    sh[i] = (beta ? beta[c] : 0.f) - st.x * a;
+    sh[i] = __builtin_fmaf(-st.x, a, beta ? beta[c] : 0.f);
   }
   for (int r = rb + r0; r < re; r += RPP * U) {
     V8 nxt[U];
@@ -311,7 +311,7 @@ __global__ void __launch_bounds__(256) gn_apply2_kernel(const T* __restrict__ x,
       V8 out;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float f = (float)val[u][i] * sc[i] + sh[i];
+        float f = __builtin_fmaf((float)val[u][i], sc[i], sh[i]);
         if (silu) f = silu_f(f);
         out[i] = (T)f;
       }
@@ -400,6 +400,61 @@ extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma
   gn_finalize_launch((const float2*)part, (float2*)stats, nimg, HW, C, groups, HW / part_rows, eps, s);
   FD_LAUNCH_CHECK();
   return gn_apply_launch(x, y, (const float2*)stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s);
+}
+
+// GroupNorm as a per-(image, channel) affine (a, b) = (rstd * gamma, beta - mean * a): gn_apply2's scale / shift, for
+// a consumer that applies it in its own staging pass (the halo conv, fd_gemm_params.gi_affine).  The 64 channels
+// after the last image are zeroed (the conv DMAs the table 1 KB at a time).
+__global__ void __launch_bounds__(256) gn_affine_kernel(const float2* __restrict__ stats, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float2* __restrict__ aff,
+                                                        int nimg, int C, int groups) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long tot = (long long)nimg * C;
+  if (e >= tot) {
+    if (e < tot + 64) aff[e] = make_float2(0.f, 0.f);
+    return;
+  }
+  const int img = (int)(e / C), c = (int)(e - (long long)img * C);
+  const float2 st = stats[img * groups + c / (C / groups)];
+  const float a = st.y * (gamma ? gamma[c] : 1.f);
+  aff[e] = make_float2(a, __builtin_fmaf(-st.x, a, beta ? beta[c] : 0.f));
+}
+
+extern "C" int fd_group_norm_affine(const void* x, const void* part, int part_rows, const float* gamma,
+                                    const float* beta, int nimg, int HW, int C, int groups, float eps, void* ws,
+                                    void* affine, int dtype, void* stream) {
+  if (!ws || !affine || (!x && !part)) return FD_ERR_ARG;
+  if (nimg <= 0 || HW <= 0 || C <= 0 || groups <= 0 || groups > 64 || C % groups || C % 8 || C > GN_MAXC)
+    return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  float2* stats;
+  if (part) {
+    if ((part_rows != 128 && part_rows != 256) || HW % part_rows) return FD_ERR_ARG;
+    stats = (float2*)ws;
+    gn_finalize_launch((const float2*)part, stats, nimg, HW, C, groups, HW / part_rows, eps, s);
+  } else {
+    if ((groups & (groups - 1))) return FD_ERR_SHAPE;
+    const int rpc = gn_rows_per_chunk(nimg, HW);
+    const int nch = (HW + rpc - 1) / rpc;
+    const int NV = (C / 8 > 256) ? 2 : 1;
+    if (NV == 2 && (C % 16)) return FD_ERR_SHAPE;
+    if (NV == 1) {
+      FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_partial_kernel<T, 1>), dim3(nch, nimg), dim3(256), 0, s,
+                                              (const T*)x, (float2*)ws, HW, C, groups, rpc));
+    } else {
+      FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_partial_kernel<T, 2>), dim3(nch, nimg), dim3(256), 0, s,
+                                              (const T*)x, (float2*)ws, HW, C, groups, rpc));
+    }
+    FD_LAUNCH_CHECK();
+    stats = (float2*)ws + (long long)nimg * nch * groups;
+    gn_finalize_launch((const float2*)ws, stats, nimg, HW, C, groups, nch, eps, s);
+  }
+  FD_LAUNCH_CHECK();
+  const long long n = (long long)nimg * C + 64;
+  hipLaunchKernelGGL(gn_affine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float2*)stats, gamma,
+                     beta, (float2*)affine, nimg, C, groups);
+  FD_LAUNCH_CHECK();
+  return FD_OK;
 }
 
 // ------------------------------------------------------------------------------------------------

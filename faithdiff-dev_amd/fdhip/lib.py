@@ -36,6 +36,7 @@ class GemmParams(ctypes.Structure):
         ("m_ref", c_int), ("ws", c_vp), ("ws_bytes", c_ll),
         ("ln_out", c_vp), ("ln_in", c_vp), ("ln_c", c_vp), ("ln_eps", c_f),
         ("gn_part", c_vp), ("gn_groups", c_int), ("gn_hw", c_int), ("gn_done", c_int),
+        ("gi_affine", c_vp), ("gi_silu", c_int),
     ]
 
 
@@ -43,6 +44,9 @@ class GemmParams(ctypes.Structure):
 _SIGS = {
     "fd_gemm": (c_int, [ctypes.POINTER(GemmParams), c_vp]),
     "fd_gemm_ws_bytes": (c_ll, [ctypes.POINTER(GemmParams)]),
+    "fd_conv_halo_plan": (c_int, [ctypes.POINTER(GemmParams)]),
+    "fd_group_norm_affine": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_vp, c_vp, c_int,
+                                     c_vp]),
     "fd_conv2d_direct": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f,
                                  c_int, c_int, c_vp]),
     "fd_group_norm_ws_bytes": (c_ll, [c_int, c_int, c_int, c_int]),

@@ -393,11 +393,8 @@ def fold_layer_norm(w, gamma, beta, bias=None, dtype=torch.bfloat16):
     return wp.contiguous(), c.contiguous(), d.float().contiguous()
 
 
-def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C1=None, out=None, rowbias=None,
-            residual=None, act="none", out_dtype=None, upsample_size=None, gn=None, lda=None, alpha=1.0):
-    """Implicit-GEMM 3x3 conv on NHWC x [nimg*H*W, Cin] (or concat(x, x2) along C) with packed weight wp.
-    upsample=True: nearest-resize to upsample_size (default 2H x 2W) folded into the gather.  lda: pixel stride
-    of x when it is a channel slice of a wider buffer (default Cin); alpha scales the accumulator (before bias)."""
+def _conv_params(x, wp, bias, nimg, H, W, stride, pad, upsample, x2, C1, out, rowbias, residual, act, out_dtype,
+                 upsample_size, lda, alpha):
     Cout, K = wp.shape
     Cin = K // 9
     Hl, Wl = ((2 * H, 2 * W) if upsample_size is None else tuple(upsample_size)) if upsample else (H, W)
@@ -427,6 +424,23 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
     p.conv, p.nimg, p.Hin, p.Win, p.Cin = 1, nimg, H, W, Cin
     p.Hout, p.Wout, p.stride, p.pad, p.upsample = Hout, Wout, stride, pad, int(upsample)
     p.A2 = x2.data_ptr() if x2 is not None else None
+    groups = _TILE_GROUPS[-1]
+    p.m_ref = p.M // groups if groups > 1 and p.M % groups == 0 else p.M
+    return p, out
+
+
+def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C1=None, out=None, rowbias=None,
+            residual=None, act="none", out_dtype=None, upsample_size=None, gn=None, lda=None, alpha=1.0, gn_in=None):
+    """Implicit-GEMM 3x3 conv on NHWC x [nimg*H*W, Cin] (or concat(x, x2) along C) with packed weight wp.
+    upsample=True: nearest-resize to upsample_size (default 2H x 2W) folded into the gather.  lda: pixel stride
+    of x when it is a channel slice of a wider buffer (default Cin); alpha scales the accumulator (before bias).
+    gn_in = (affine, silu): the consumer GroupNorm (+ SiLU) of x applied in the conv's staging pass
+    (fd_gemm_params.gi_affine; affine from group_norm_affine) -- only where halo_conv_rows() says the halo-staged
+    kernel takes this conv."""
+    p, out = _conv_params(x, wp, bias, nimg, H, W, stride, pad, upsample, x2, C1, out, rowbias, residual, act,
+                          out_dtype, upsample_size, lda, alpha)
+    if gn_in is not None:
+        p.gi_affine, p.gi_silu = gn_in[0].data_ptr(), int(gn_in[1])
     if gn is not None:
         gn.attach(p)
     _attach_ws(p, x.device)
@@ -434,6 +448,16 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
     if gn is not None:
         gn.collect(p)
     return out
+
+
+def halo_conv_rows(x, wp, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, upsample_size=None, lda=None):
+    """Rows per GroupNorm-statistics block the halo-staged conv kernel would write for this conv (256 / 128), 0 when
+    fd_gemm takes it on the implicit GEMM (then a consumer GroupNorm must run as its own pass).  Shapes only."""
+    dummy = torch.empty((1, wp.shape[0]), dtype=x.dtype, device=x.device)
+    p, _ = _conv_params(x, wp, None, nimg, H, W, stride, pad, upsample, x2, None if x2 is None else 0, dummy, None,
+                        None, "none", None, upsample_size, lda, 1.0)
+    p.C, p.ldc = x.data_ptr(), wp.shape[0]  # alignment / stride stand-ins for the real output (fresh allocations)
+    return int(L.load().fd_conv_halo_plan(ctypes.byref(p)))
 
 
 def conv3x3_narrow(x, w32, bias, nimg, H, W, out_dtype=None, out=None):
@@ -485,6 +509,26 @@ def group_norm(x, gamma, beta, nimg, HW, C, groups=32, eps=1e-5, silu=False, out
         L.load().fd_group_norm(L.ptr(x), L.ptr(out), L.ptr(gamma), L.ptr(beta), nimg, HW, C, groups, eps, int(silu),
                                L.dtype_code(x.dtype), L.ptr(ws), L.stream()), "fd_group_norm"))
     return out
+
+
+def group_norm_affine(x, gamma, beta, nimg, HW, C, groups=32, eps=1e-5, stats=None):
+    """The GroupNorm of NHWC x as a per-(image, channel) fp32 affine [nimg * C + 64, 2] (scale, shift) for a consumer
+    that applies it itself (conv3x3(..., gn_in=(affine, silu))).  stats: a GnStats the producer of x filled (no
+    statistics pass)."""
+    aff = torch.empty((nimg * C + 64, 2), dtype=torch.float32, device=x.device)
+    if stats is not None and stats.done:
+        if (stats.nimg, stats.HW, stats.groups) != (nimg, HW, groups):
+            raise ValueError("group_norm_affine: stats were gathered for a different shape")
+        ws = _gn_ws(nimg * groups * 8, x.device)
+        part, rows = L.ptr(stats.part), stats.rows
+    else:
+        ws = _gn_ws(L.load().fd_group_norm_ws_bytes(nimg, HW, C, groups), x.device)
+        part, rows = None, 0
+    _timed("group_norm", 0, 1.0 * nimg * HW * C * x.element_size() * (0 if part else 1), lambda: L.check(
+        L.load().fd_group_norm_affine(L.ptr(x), part, rows, L.ptr(gamma), L.ptr(beta), nimg, HW, C, groups, eps,
+                                      L.ptr(ws), L.ptr(aff), L.dtype_code(x.dtype), L.stream()),
+        "fd_group_norm_affine"))
+    return aff
 
 
 def layer_norm(x, gamma, beta, eps=1e-5, out=None, M=None, ldx=None):

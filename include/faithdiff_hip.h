@@ -103,9 +103,22 @@ typedef struct fd_gemm_params {
   int gn_groups;
   int gn_hw;
   int gn_done;
+  /* Consumer GroupNorm (+ SiLU) folded into a 3x3 stride-1 conv (the halo-staged kernel only: callers check
+   * fd_conv_halo_plan first; an ineligible conv with gi_affine set returns FD_ERR_SHAPE).  gi_affine: fp32
+   * (scale, shift) per (image, input channel), [nimg][Cin][2], from fd_group_norm_affine, with 64 channels of
+   * padding after the last image; the conv reads silu?(x * scale + shift) rounded to the input type, zero outside
+   * the image -- exactly conv(fd_group_norm(x)), without the normalised tensor.  Replaces the GroupNorm + SiLU
+   * in front of every ResnetBlock2D conv (diffusers; UNet and VAE). */
+  const void* gi_affine;
+  int gi_silu;
 } fd_gemm_params;
 
 int fd_gemm(fd_gemm_params* p, void* stream);  /* writes only p->gn_done */
+/* 3x3 stride-1 pad-1 convs (Cin % 64 == 0, Cout % 128 or 160 == 0, no concat source) run on the halo-staged kernel
+ * (csrc/conv_halo.hip: each input patch staged once per 64-channel chunk, 9 taps read from LDS) when it has enough
+ * tiles; the choice reads m_ref, never the batched M.  Returns the rows per GroupNorm-statistics block it writes
+ * (256 or 128), 0 when fd_gemm would use the implicit GEMM for this conv. */
+int fd_conv_halo_plan(const fd_gemm_params* p);
 /* Workspace fd_gemm needs for this launch (0 = none). */
 long long fd_gemm_ws_bytes(const fd_gemm_params* p);
 
@@ -141,6 +154,13 @@ int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta,
 int fd_group_norm_partials(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
                            int groups, float eps, int silu, const void* part, int part_rows, void* stats, int dtype,
                            void* stream);
+/* GroupNorm as a per-(image, channel) affine for a consumer that applies it itself (fd_gemm_params.gi_affine):
+ * statistics from the producer's partials (part != NULL, part_rows = gn_done) or from x (a gn_partial pass; ws of
+ * fd_group_norm_ws_bytes), then affine[i][c] = (rstd * gamma[c], beta[c] - mean * rstd * gamma[c]) -- the exact
+ * scale / shift fd_group_norm applies.  affine: fp32 [nimg * C + 64][2]. */
+int fd_group_norm_affine(const void* x, const void* part, int part_rows, const float* gamma, const float* beta,
+                         int nimg, int HW, int C, int groups, float eps, void* ws, void* affine, int dtype,
+                         void* stream);
 
 /* LayerNorm fused with the per-row e4m3 quantization of fd_quant_rows_e4m3 (use_fp8 model): the row is
  * normalised, rounded to dtype, then q[m][:] = e4m3_RNE(y * 448 / amax_m), scale[m] = amax_m / 448 -- bitwise

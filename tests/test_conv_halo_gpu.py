@@ -1,0 +1,161 @@
+"""The halo-staged 3x3 conv (csrc/conv_halo.hip; fd_gemm takes it for eligible stride-1 convs) and the consumer
+GroupNorm (+ SiLU) folded into its staging pass (fd_gemm_params.gi_affine, group_norm_affine).
+
+Bars: against torch fp32 (CPU) on the same bf16 / fp16 inputs, rel-L2 < 6e-3 (the implicit-GEMM conv's bar,
+tests/test_kernels_gpu.py); GroupNorm folded into the conv BITWISE equal to fd_group_norm followed by the same conv
+(the staging pass stores exactly the values fd_group_norm stores); two images in one launch bitwise equal to one
+launch per image; TH = 8 and TH = 16 tiles bitwise equal (same per-element K order).  Ragged edges (62 x 46, the
+forward_upsample_size latent), nearest x2 and odd-size upsample, residual + per-image row bias + activation, and the
+GroupNorm statistics the epilogue writes for the next GroupNorm are covered.  Reference call sites: diffusers
+ResnetBlock2D (norm1 -> SiLU -> conv1, norm2 -> SiLU -> conv2) from unet_2d_condition_vae_extension.py:611-690 and
+the VAE decode (pipeline_FaithDiff_tlc.py:1438)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from parity import rel_l2  # noqa: E402  (records every measured value)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _knobs(**kw):
+    from fdhip import knobs
+    return knobs.override(**kw)
+
+
+def _inputs(nimg, H, W, Cin, Cout, dtype, seed=0, up=None):
+    g = torch.Generator().manual_seed(seed)
+    Hi, Wi = (H, W) if up is None else up
+    x = torch.randn(nimg, Cin, Hi, Wi, generator=g).to(dtype)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (9 * Cin) ** 0.5).to(dtype)
+    b = torch.randn(Cout, generator=g) * 0.1
+    return x, w, b
+
+
+def _nhwc(x):
+    n, c, h, w = x.shape
+    return x.permute(0, 2, 3, 1).reshape(n * h * w, c).contiguous()
+
+
+def _nchw(y, n, h, w):
+    return y.reshape(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+def _hip_conv(x, w, b, nimg, H, W, **kw):
+    from fdhip import ops
+    wp = ops.pack_conv3x3(w.float()).to(DEV, x.dtype)
+    xs = _nhwc(x).to(DEV)
+    return ops.conv3x3(xs, wp, b.float().to(DEV), nimg, H, W, **kw), xs, wp
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nimg,H,W,Cin,Cout", [(2, 64, 64, 320, 320), (1, 62, 46, 640, 640), (1, 48, 32, 128, 128),
+                                               (2, 32, 48, 256, 512)])
+def test_halo_conv_matches_torch(dtype, nimg, H, W, Cin, Cout):
+    from fdhip import ops
+    x, w, b = _inputs(nimg, H, W, Cin, Cout, dtype)
+    with _knobs(FD_CONV_HALO_MIN_TILES=1):
+        wp = ops.pack_conv3x3(w.float()).to(DEV, dtype)
+        xs = _nhwc(x).to(DEV)
+        assert ops.halo_conv_rows(xs, wp, nimg, H, W) > 0
+        y = ops.conv3x3(xs, wp, b.float().to(DEV), nimg, H, W)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float(), w.float(), b, padding=1)
+    rel = rel_l2(_nchw(y.float().cpu(), nimg, H, W), ref)
+    assert rel < 6e-3, rel
+
+
+@pytest.mark.parametrize("silu", [True, False])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_groupnorm_folded_into_conv_is_bitwise_groupnorm_then_conv(silu, dtype):
+    from fdhip import ops
+    nimg, H, W, Cin, Cout = 2, 64, 48, 640, 320
+    x, w, b = _inputs(nimg, H, W, Cin, Cout, dtype, seed=3)
+    g = torch.Generator().manual_seed(4)
+    gamma = (1 + 0.1 * torch.randn(Cin, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(Cin, generator=g)).to(DEV)
+    with _knobs(FD_CONV_HALO_MIN_TILES=1):
+        wp = ops.pack_conv3x3(w.float()).to(DEV, dtype)
+        xs = _nhwc(x).to(DEV)
+        bd = b.float().to(DEV)
+        aff = ops.group_norm_affine(xs, gamma, beta, nimg, H * W, Cin, 32, 1e-5)
+        fused = ops.conv3x3(xs, wp, bd, nimg, H, W, gn_in=(aff, silu))
+        hn = ops.group_norm(xs, gamma, beta, nimg, H * W, Cin, 32, 1e-5, silu=silu)
+        plain = ops.conv3x3(hn, wp, bd, nimg, H, W)
+    torch.cuda.synchronize()
+    assert torch.equal(fused, plain)
+    xr = F.group_norm(x.float(), 32, gamma.cpu(), beta.cpu(), 1e-5)
+    if silu:
+        xr = F.silu(xr)
+    ref = F.conv2d(xr.to(dtype).float(), w.float(), b, padding=1)
+    rel = rel_l2(_nchw(fused.float().cpu(), nimg, H, W), ref)
+    assert rel < 6e-3, rel
+
+
+def test_halo_conv_batch_and_tile_shape_invariant():
+    """Two images in one launch == one launch per image, and 8-row tiles == 16-row tiles, bitwise."""
+    from fdhip import ops
+    nimg, H, W, C = 2, 64, 64, 320
+    x, w, b = _inputs(nimg, H, W, C, C, torch.bfloat16, seed=5)
+    wp = ops.pack_conv3x3(w.float()).to(DEV, torch.bfloat16)
+    xs = _nhwc(x).to(DEV)
+    bd = b.float().to(DEV)
+    with _knobs(FD_CONV_HALO_MIN_TILES=1):
+        both = ops.conv3x3(xs, wp, bd, nimg, H, W)
+        one = torch.cat([ops.conv3x3(xs[i * H * W:(i + 1) * H * W].contiguous(), wp, bd, 1, H, W) for i in range(2)])
+        assert ops.halo_conv_rows(xs, wp, nimg, H, W) == 256
+    with _knobs(FD_CONV_HALO_MIN_TILES=100000):
+        assert ops.halo_conv_rows(xs, wp, nimg, H, W) == 0  # the implicit GEMM
+    # TH = 8 tiles: a threshold between the two tile counts (16-row: 2 x 4 x 4 x 2 = 64 tiles; 8-row: 128)
+    with _knobs(FD_CONV_HALO_MIN_TILES=100):
+        assert ops.halo_conv_rows(xs, wp, nimg, H, W) == 128
+        th8 = ops.conv3x3(xs, wp, bd, nimg, H, W)
+    torch.cuda.synchronize()
+    assert torch.equal(both, one)
+    assert torch.equal(both, th8)
+
+
+@pytest.mark.parametrize("up", [(32, 32), (31, 23)])
+def test_halo_conv_upsample(up):
+    """Upsample2D: nearest x2, and diffusers' upsample_size path (31 x 23 -> 62 x 46)."""
+    from fdhip import ops
+    H, W = (64, 64) if up == (32, 32) else (62, 46)
+    x, w, b = _inputs(1, H, W, 640, 640, torch.bfloat16, seed=7, up=up)
+    with _knobs(FD_CONV_HALO_MIN_TILES=1):
+        wp = ops.pack_conv3x3(w.float()).to(DEV, torch.bfloat16)
+        xs = _nhwc(x).to(DEV)
+        assert ops.halo_conv_rows(xs, wp, 1, up[0], up[1], upsample=True, upsample_size=(H, W)) > 0
+        y = ops.conv3x3(xs, wp, b.float().to(DEV), 1, up[0], up[1], upsample=True, upsample_size=(H, W))
+    torch.cuda.synchronize()
+    ref = F.conv2d(F.interpolate(x.float(), size=(H, W), mode="nearest"), w.float(), b, padding=1)
+    rel = rel_l2(_nchw(y.float().cpu(), 1, H, W), ref)
+    assert rel < 6e-3, rel
+
+
+def test_halo_conv_epilogue_residual_rowbias_act_and_groupnorm_statistics():
+    """conv1 of a ResnetBlock2D (+ per-image time-embedding row bias) and conv2 (+ residual), the epilogue's
+    GroupNorm statistics feeding the next GroupNorm (GnStats) -- against torch and against a statistics pass."""
+    from fdhip import ops
+    nimg, H, W, C = 2, 32, 32, 640
+    x, w, b = _inputs(nimg, H, W, C, C, torch.bfloat16, seed=9)
+    g = torch.Generator().manual_seed(10)
+    temb = torch.randn(nimg, C, generator=g)
+    res = torch.randn(nimg, C, H, W, generator=g).to(torch.bfloat16)
+    gamma = (1 + 0.1 * torch.randn(C, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(C, generator=g)).to(DEV)
+    with _knobs(FD_CONV_HALO_MIN_TILES=1):
+        wp = ops.pack_conv3x3(w.float()).to(DEV, torch.bfloat16)
+        xs = _nhwc(x).to(DEV)
+        st = ops.GnStats(nimg, H * W, 32, DEV)
+        y = ops.conv3x3(xs, wp, b.float().to(DEV), nimg, H, W, rowbias=temb.to(DEV), residual=_nhwc(res).to(DEV),
+                        act="silu", gn=st)
+        assert st.done and st.rows == 256
+        a1 = ops.group_norm_affine(y, gamma, beta, nimg, H * W, C, 32, 1e-5, stats=st)
+        a2 = ops.group_norm_affine(y, gamma, beta, nimg, H * W, C, 32, 1e-5)
+    torch.cuda.synchronize()
+    ref = F.silu(F.conv2d(x.float(), w.float(), b, padding=1) + temb[:, :, None, None]) + res.float()
+    rel = rel_l2(_nchw(y.float().cpu(), nimg, H, W), ref)
+    assert rel < 6e-3, rel
+    # statistics from the epilogue vs from a pass over y: same (scale, shift) up to fp32 summation order
+    assert rel_l2(a1[:nimg * C].cpu(), a2[:nimg * C].cpu()) < 1e-5

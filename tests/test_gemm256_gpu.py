@@ -8,6 +8,14 @@ import torch.nn.functional as F
 from parity import rel_l2  # noqa: E402  (records every measured value)
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _implicit_gemm_convs():
+    """These tests pin the implicit-GEMM conv kernels (the halo-staged conv has its own, tests/test_conv_halo_gpu.py)."""
+    from fdhip import knobs
+    with knobs.override(FD_CONV_HALO=0):
+        yield
 DEV = "cuda"
 
 
