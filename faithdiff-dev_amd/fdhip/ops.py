@@ -450,6 +450,20 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
     return out
 
 
+def gn_conv3x3(x, gamma, beta, wp, bias, nimg, H, W, eps, silu=True, groups=32, stats=None, **kw):
+    """conv3x3(GroupNorm(+SiLU)(x)) -- the norm -> SiLU -> conv of a ResnetBlock2D.  Where the halo-staged conv
+    takes the conv, the GroupNorm is its per-(image, channel) affine applied in the conv's staging pass (no
+    normalised tensor is written or read); else a GroupNorm pass, then the conv.  stats: GnStats of x from its
+    producer's epilogue (skips the statistics pass either way)."""
+    C = x.shape[-1]
+    if halo_conv_rows(x, wp, nimg, H, W, upsample=kw.get("upsample", False),
+                      upsample_size=kw.get("upsample_size")) > 0:
+        aff = group_norm_affine(x, gamma, beta, nimg, H * W, C, groups, eps, stats=stats)
+        return conv3x3(x, wp, bias, nimg, H, W, gn_in=(aff, silu), **kw)
+    h = group_norm(x, gamma, beta, nimg, H * W, C, groups, eps, silu=silu, stats=stats)
+    return conv3x3(h, wp, bias, nimg, H, W, **kw)
+
+
 def halo_conv_rows(x, wp, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, upsample_size=None, lda=None):
     """Rows per GroupNorm-statistics block the halo-staged conv kernel would write for this conv (256 / 128), 0 when
     fd_gemm takes it on the implicit GEMM (then a consumer GroupNorm must run as its own pass).  Shapes only."""

@@ -248,14 +248,14 @@ class HipUNet:
             cat = torch.empty((B * HW, r["cin"]), dtype=self.dtype, device=self.device)
             ops.concat_channels(x, C1, x2, r["cin"] - C1, cat, B * HW)
             x = cat
-        h = ops.group_norm(x, *r["n1"], B, HW, r["cin"], 32, 1e-5, silu=True, stats=self._gn_stats_of(x))
+        # norm1 -> SiLU -> conv1 (+ time embedding), norm2 -> SiLU -> conv2 (+ shortcut): each GroupNorm folded into
+        # the halo-staged conv's staging pass where that kernel takes the conv (ops.gn_conv3x3), else its own pass
         s1 = self._gn_new(B, HW)
-        h = ops.conv3x3(h, r["c1"][0], r["c1"][1], B, H, Wd,
-                        rowbias=temb[:, r["toff"]:r["toff"] + r["cout"]], gn=s1)
-        h2 = ops.group_norm(h, *r["n2"], B, HW, r["cout"], 32, 1e-5, silu=True, out=h, stats=s1)
+        h = ops.gn_conv3x3(x, *r["n1"], *r["c1"], B, H, Wd, 1e-5, silu=True, stats=self._gn_stats_of(x),
+                           rowbias=temb[:, r["toff"]:r["toff"] + r["cout"]], gn=s1)
         sc = ops.gemm(x, r["sc"][0], bias=r["sc"][1]) if "sc" in r else x
         s2 = self._gn_new(B, HW)
-        out = ops.conv3x3(h2, r["c2"][0], r["c2"][1], B, H, Wd, residual=sc, gn=s2)
+        out = ops.gn_conv3x3(h, *r["n2"], *r["c2"], B, H, Wd, 1e-5, silu=True, stats=s1, residual=sc, gn=s2)
         self._gn_src = (out, s2) if s2 is not None else None
         return out
 

@@ -60,13 +60,13 @@ def run_resnet(r, x, n, H, W, dtype, device, stats=None):
     """ResnetBlock2D.  stats: GroupNorm statistics of x written by its producer (ops.GnStats), None = computed by
     the GroupNorm.  Returns (out, GnStats of out from conv2's epilogue, for the next GroupNorm)."""
     HW = H * W
-    h = ops.group_norm(x, *r["n1"], n, HW, r["cin"], 32, 1e-6, silu=True, stats=stats)
+    # norm -> SiLU -> conv pairs: the GroupNorm folded into the halo-staged conv's staging pass where it applies
+    # (ops.gn_conv3x3), else its own pass
     s1 = ops.GnStats(n, HW, 32, x.device)
-    h = ops.conv3x3(h, *r["c1"], n, H, W, gn=s1)
-    ops.group_norm(h, *r["n2"], n, HW, r["cout"], 32, 1e-6, silu=True, out=h, stats=s1)
+    h = ops.gn_conv3x3(x, *r["n1"], *r["c1"], n, H, W, 1e-6, silu=True, stats=stats, gn=s1)
     sc = ops.gemm(x, r["sc"][0], bias=r["sc"][1]) if "sc" in r else x
     s2 = ops.GnStats(n, HW, 32, x.device)
-    return ops.conv3x3(h, *r["c2"], n, H, W, residual=sc, gn=s2), s2
+    return ops.gn_conv3x3(h, *r["n2"], *r["c2"], n, H, W, 1e-6, silu=True, stats=s1, residual=sc, gn=s2), s2
 
 
 def run_attn(a, x, n, H, W, stats=None):
