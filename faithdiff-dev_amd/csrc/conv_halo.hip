@@ -34,8 +34,9 @@ __device__ __forceinline__ void hvm() {
 constexpr int PW = 18;  // patch width: 16 output columns + halo
 constexpr int TR = 7;   // tap of chunk c at which chunk c + 1's patch is waited for and transformed
 
-template <typename T, int TH, int BN, bool GNI>
-__global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p) {
+template <typename T, int TH, int BN, bool GNI, bool SK>
+__global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, float* __restrict__ slabs,
+                                                          unsigned* __restrict__ counters) {
   typedef typename VecT<T>::v8 V8;
   typedef __attribute__((ext_vector_type(8))) T TO8;
   constexpr int BM = TH * 16;
@@ -68,13 +69,17 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p) 
   const int tiles_x = (Wo + 15) / 16, tiles_y = (Ho + TH - 1) / TH;
   const int nsp = p.nimg * tiles_y * tiles_x;
   // tile order: XCD-contiguous chunks (bijective remap), output-channel tiles outer, so the ~32 workgroups an XCD
-  // runs at once share one weight panel in its L2
+  // runs at once share one weight panel in its L2; SK: the two channel halves of a tile adjacent (same XCD)
   const int pid = xcd_remap(blockIdx.x, gridDim.x);
-  const int nt = pid / nsp, sp = pid - nt * nsp;
+  const int split = SK ? (pid & 1) : 0, tlin = SK ? (pid >> 1) : pid;
+  const int nt = tlin / nsp, sp = tlin - nt * nsp;
   const int img = sp / (tiles_y * tiles_x), spi = sp - img * (tiles_y * tiles_x);
   const int tyt = spi / tiles_x, txt = spi - tyt * tiles_x;
   const int y0 = tyt * TH, x0 = txt * 16, n0 = nt * BN;
-  const int nch = Cin / 64, nsteps = 9 * nch;
+  // input-channel chunks of this workgroup: all, or (SK) one half of them, combined pairwise after the K loop
+  const int nch_all = Cin / 64;
+  const int cb = SK && split ? nch_all / 2 : 0, ce = SK && !split ? nch_all / 2 : nch_all;
+  const int nsteps = 9 * (ce - cb);
   const T* __restrict__ A = (const T*)p.A;
   const T* __restrict__ Bw = (const T*)p.B;
   const bool up2 = p.upsample && Ho == 2 * p.Hin && Wo == 2 * p.Win;
@@ -107,8 +112,8 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p) 
   }
   const float* __restrict__ aff = GNI ? (const float*)p.gi_affine + (long long)img * Cin * 2 : nullptr;
 
-  auto stage_b = [&](int s, int rb) {
-    const int c = s / 9, t = s - (s / 9) * 9;
+  auto stage_b = [&](int s, int rb) {  // s: this workgroup's step (chunk cb + s / 9, tap s % 9)
+    const int c = cb + s / 9, t = s - (s / 9) * 9;
     const int off = t * Cin + c * 64;
     unsigned char* dst = smem + RING + rb * STAGE;
 #pragma unroll
@@ -208,20 +213,20 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p) 
       if (s0 < nsteps) stage_b(s0, s0);
     wait_b(min(nsteps, NS) - 1);
   } else {
-    stage_p(0);
-    if (nch > 1) stage_p(1);
+    stage_p(cb);
+    if (cb + 1 < ce) stage_p(cb + 1);
     hvm<0>();
   }
   __builtin_amdgcn_s_barrier();
   if (GNI) {
-    transform(0);
+    transform(cb);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_s_barrier();
   }
 
   V8 a0[MT], b0[NT], a1[MT], b1[NT];
-  read_frags(0, 0, 0, 0, a0, b0);
-  int c = 0, t = 0, rb = 0;
+  read_frags(cb, 0, 0, 0, a0, b0);
+  int c = cb, t = 0, rb = 0;
   for (int s = 0; s < nsteps - 1; ++s) {
     read_frags(c, t, rb, 1, a1, b1);
     mma(a0, b0);
@@ -232,10 +237,10 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p) 
     __builtin_amdgcn_s_barrier();
     if (w < 4) {
       if (s + NS < nsteps) stage_b(s + NS, rb);
-    } else if (t == 8 && c + 2 < nch) {
+    } else if (t == 8 && c + 2 < ce) {
       stage_p(c + 2);  // buffer c & 1: its last reads (this step's half 1) are behind the barrier
     }
-    if (GNI && t == TR && c + 1 < nch) transform(c + 1);  // visible to the readers after step (c, 8)'s barrier
+    if (GNI && t == TR && c + 1 < ce) transform(c + 1);  // visible to the readers after step (c, 8)'s barrier
     rb = rb == NS - 1 ? 0 : rb + 1;
     if (t == 8) {
       ++c;
@@ -249,6 +254,56 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p) 
   read_frags(c, t, rb, 1, a1, b1);
   mma(a0, b0);
   mma(a1, b1);
+
+  // ---- SK: pairwise combine (gemm8's S = 2 form): the first half to finish publishes its fp32 accumulators with
+  // write-through (sc1) stores and an sc1 flag; the second waits for the flag, adds them to its own (a + b: the
+  // same bits whichever half came first) and runs the epilogue.  It only ever waits on a workgroup that already
+  // took its ticket (running), so no co-residency is assumed; the wait is bounded.
+  if constexpr (SK) {
+    constexpr int SLAB = MT * NT * 512 * 16;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((char*)slabs + (long long)tlin * SLAB, (short)0, SLAB, 0x00020000);
+    unsigned* flag = counters + 32768 + tlin;
+    __syncthreads();  // every wave past its last LDS read: smem[0] is free
+    if (tid == 0) {
+      const unsigned tk = __hip_atomic_fetch_add(counters + tlin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *(volatile unsigned*)smem = tk;
+    }
+    __syncthreads();
+    const unsigned tk = *(volatile unsigned*)smem;
+    if (tk == 0) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][ni]), rs,
+                                                 ((mi * NT + ni) * 512 + tid) * 16, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {
+      for (int it = 0; it < (1 << 24); ++it) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(counters + tlin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    f32x4 part[MT][NT];
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni)
+        part[mi][ni] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((mi * NT + ni) * 512 + tid) * 16, 0, 16));
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = split == 0 ? acc[mi][ni] + part[mi][ni] : part[mi][ni] + acc[mi][ni];
+  }
 
   // ---- epilogue: two (TH = 16) or one 128-row passes through LDS fp32 [128][BN + 4]; each thread then owns 8
   // consecutive columns of a row: bias, per-image row bias (time embedding), activation, residual, one 16-B store;
@@ -371,7 +426,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p) 
 }
 
 struct HaloPlan {
-  int th, bn, tiles;
+  int th, bn, tiles, sk;  // tiles: output tiles (workgroups = tiles * (1 + sk))
 };
 
 // Eligibility and tile plan, from per-image quantities only (m_ref: rows of one TLC tile's forward), so batching
@@ -397,32 +452,42 @@ int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
   const long long nimg_ref = m_ref / hw > 0 ? m_ref / hw : 1;
   auto tiles = [&](int th) { return nimg_ref * ((p->Hout + th - 1) / th) * ((p->Wout + 15) / 16) * (p->N / bn); };
   const int min_tiles = fd_knob(FDK_CONV_HALO_MIN_TILES);
-  int th = 0;
+  int th = 0, sk = 0;
   if (tiles(16) >= min_tiles) th = 16;
   else if (tiles(8) >= min_tiles) th = 8;
+  else if (fd_knob(FDK_CONV_HALO_SPLIT) && p->Cin >= 128 && 2 * tiles(8) >= min_tiles) th = 8, sk = 1;
   if (!th || p->Wout < 16 || p->Hout < th) return 0;
   pl->th = th;
   pl->bn = bn;
+  pl->sk = sk;
   pl->tiles = (int)(p->nimg * ((p->Hout + th - 1) / th) * ((p->Wout + 15) / 16) * (p->N / bn));
+  if (sk && pl->tiles > 32768) return 0;  // one split-K counter / flag per tile
   return 1;
 }
+
+constexpr int slab_bytes(int th, int bn) { return (th * 4 / 16) * (bn / 32) * 512 * 16; }
 
 template <typename T>
 int launch_halo(const fd_gemm_params* p, const HaloPlan& pl, hipStream_t s) {
   const bool gi = p->gi_affine != nullptr;
-#define FD_HALO(TH_, BN_)                                                                                           \
-  if (pl.th == TH_ && pl.bn == BN_) {                                                                               \
-    if (gi)                                                                                                         \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true>), dim3(pl.tiles), dim3(512), 0, s, *p);               \
-    else                                                                                                            \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false>), dim3(pl.tiles), dim3(512), 0, s, *p);              \
-    FD_LAUNCH_CHECK();                                                                                              \
-    return FD_OK;                                                                                                   \
+  float* slabs = pl.sk ? (float*)((char*)p->ws + 65536 * sizeof(unsigned)) : nullptr;
+  unsigned* cnt = pl.sk ? (unsigned*)p->ws : nullptr;
+  const dim3 grid(pl.tiles * (1 + pl.sk));
+#define FD_HALO(TH_, BN_, SK_)                                                                                       \
+  if (pl.th == TH_ && pl.bn == BN_ && pl.sk == SK_) {                                                                \
+    if (gi)                                                                                                          \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true, SK_>), grid, dim3(512), 0, s, *p, slabs, cnt);        \
+    else                                                                                                             \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, SK_>), grid, dim3(512), 0, s, *p, slabs, cnt);       \
+    FD_LAUNCH_CHECK();                                                                                               \
+    return FD_OK;                                                                                                    \
   }
-  FD_HALO(16, 160)
-  FD_HALO(16, 128)
-  FD_HALO(8, 160)
-  FD_HALO(8, 128)
+  FD_HALO(16, 160, 0)
+  FD_HALO(16, 128, 0)
+  FD_HALO(8, 160, 0)
+  FD_HALO(8, 128, 0)
+  FD_HALO(8, 160, 1)
+  FD_HALO(8, 128, 1)
 #undef FD_HALO
   return FD_ERR_ARG;
 }
@@ -436,6 +501,14 @@ extern "C" int fd_conv_halo_plan(const fd_gemm_params* p) {
   return pl.th * 16;
 }
 
+// Split-K workspace of the halo kernel for this conv: -1 = the halo kernel does not take it, else bytes (0 = none).
+extern "C" long long fd_conv_halo_ws_bytes(const fd_gemm_params* p) {
+  HaloPlan pl;
+  if (!p || !halo_plan(p, &pl)) return -1;
+  if (!pl.sk) return 0;
+  return 65536LL * sizeof(unsigned) + (long long)pl.tiles * slab_bytes(pl.th, pl.bn);
+}
+
 // Called by fd_gemm for every conv: 1 = launched here, 0 = not eligible (the implicit GEMM takes it), < 0 = error.
 // gn_part is honoured when the tiles are whole (H % TH == 0, W % 16 == 0, N a multiple of the group width and of
 // the tile's groups); p->gn_done reports it.  gi_affine (the consumer GroupNorm) requires this kernel: an ineligible
@@ -443,6 +516,9 @@ extern "C" int fd_conv_halo_plan(const fd_gemm_params* p) {
 extern "C" int fd_conv_halo_try(fd_gemm_params* p, void* stream) {
   HaloPlan pl;
   if (!halo_plan(p, &pl)) return p->gi_affine ? FD_ERR_SHAPE : 0;
+  if (pl.sk && (!p->ws || p->ws_bytes < 65536LL * (long long)sizeof(unsigned) +
+                                          (long long)pl.tiles * slab_bytes(pl.th, pl.bn)))
+    return FD_ERR_ARG;
   fd_gemm_params q = *p;
   p->gn_done = 0;
   if (q.gn_part) {

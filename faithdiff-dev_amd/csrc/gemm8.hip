@@ -1091,7 +1091,13 @@ planned:
   return 1;
 }
 
+extern "C" long long fd_conv_halo_ws_bytes(const fd_gemm_params* p);
+
 extern "C" long long fd_gemm_ws_bytes(const fd_gemm_params* p) {
+  if (p && p->conv) {  // the halo-staged conv takes it (its own split-K slabs, or none)
+    const long long hb = fd_conv_halo_ws_bytes(p);
+    if (hb >= 0) return hb;
+  }
   Plan8 pl;
   if (!p || !plan8(p, &pl) || pl.S <= 1) return 0;
   const long long slab = (long long)pl.bm * pl.bn * 4;

@@ -45,6 +45,7 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_FLASH_QPW", 0},           // flash attention queries per wave (0: by launch size, 16, 32)
     {"FD_CONV_HALO", 1},           // 3x3 stride-1 convs on the halo-staged kernel where eligible
     {"FD_CONV_HALO_MIN_TILES", 192},  // ... when it has at least this many tiles (per TLC tile's rows, m_ref)
+    {"FD_CONV_HALO_SPLIT", 1},     // ... or twice that many with the input channels split in two (pairwise combine)
 };
 int g_knobs[FDK_COUNT];
 bool g_init = false;

@@ -87,6 +87,23 @@ def main():
     ga = capture(lambda: hip1.forward(x[:half], t[:1], tids[:1], text[:1], cond[:half], 1, h, w), s1)
     gb = capture(lambda: hip1.forward(x[half:], t[1:], tids[1:], text[1:], cond[half:], 1, h, w), s2)
 
+    # one graph with a fork / join inside (does ROCm's graph launch run the two branches concurrently?)
+    sf = torch.cuda.Stream()
+
+    def forked():
+        main = torch.cuda.current_stream()
+        sf.wait_stream(main)
+        hip1.forward(x[:half], t[:1], tids[:1], text[:1], cond[:half], 1, h, w)
+        with torch.cuda.stream(sf):
+            hip1.forward(x[half:], t[1:], tids[1:], text[1:], cond[half:], 1, h, w)
+        main.wait_stream(sf)
+    forked()  # eager: sizes the side stream's workspaces
+    torch.cuda.synchronize()
+    gf = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gf, stream=s0):
+        forked()
+    torch.cuda.synchronize()
+
     def timeit(fn, n=30):
         for _ in range(5):
             fn()
@@ -116,7 +133,8 @@ def main():
 
     for rep in range(2):
         print(f"B=2 one graph: {timeit(lambda: g2.replay()):.3f} ms   B=1 x2 sequential: {timeit(seq):.3f} ms   "
-              f"B=1 x2 concurrent streams: {timeit(both):.3f} ms   one B=1: {timeit(lambda: ga.replay()):.3f} ms",
+              f"B=1 x2 concurrent streams: {timeit(both):.3f} ms   one forked graph: {timeit(lambda: gf.replay()):.3f} ms   "
+              f"one B=1: {timeit(lambda: ga.replay()):.3f} ms",
               flush=True)
 
 

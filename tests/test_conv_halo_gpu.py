@@ -159,3 +159,32 @@ def test_halo_conv_epilogue_residual_rowbias_act_and_groupnorm_statistics():
     assert rel < 6e-3, rel
     # statistics from the epilogue vs from a pass over y: same (scale, shift) up to fp32 summation order
     assert rel_l2(a1[:nimg * C].cpu(), a2[:nimg * C].cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("Cin,Cout", [(1280, 1280), (2560, 1280), (640, 640)])
+def test_halo_conv_channel_split(Cin, Cout):
+    """The 32^2 level (C2: 2 x 32 x 32): too few tiles, so the input channels are split over two workgroups combined
+    pairwise (SK) -- vs torch, bitwise batch-invariant (the split follows m_ref), GroupNorm folded bitwise."""
+    from fdhip import ops
+    nimg, H, W = 2, 32, 32
+    x, w, b = _inputs(nimg, H, W, Cin, Cout, torch.bfloat16, seed=11)
+    g = torch.Generator().manual_seed(12)
+    gamma = (1 + 0.1 * torch.randn(Cin, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(Cin, generator=g)).to(DEV)
+    wp = ops.pack_conv3x3(w.float()).to(DEV, torch.bfloat16)
+    xs = _nhwc(x).to(DEV)
+    bd = b.float().to(DEV)
+    assert ops.halo_conv_rows(xs, wp, nimg, H, W) == 128
+    y = ops.conv3x3(xs, wp, bd, nimg, H, W)
+    one = torch.cat([ops.conv3x3(xs[i * H * W:(i + 1) * H * W].contiguous(), wp, bd, 1, H, W) for i in range(2)]) \
+        if ops.halo_conv_rows(xs[:H * W].contiguous(), wp, 1, H, W) == 128 else None
+    aff = ops.group_norm_affine(xs, gamma, beta, nimg, H * W, Cin, 32, 1e-5)
+    fused = ops.conv3x3(xs, wp, bd, nimg, H, W, gn_in=(aff, True))
+    plain = ops.conv3x3(ops.group_norm(xs, gamma, beta, nimg, H * W, Cin, 32, 1e-5, silu=True), wp, bd, nimg, H, W)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float(), w.float(), b, padding=1)
+    rel = rel_l2(_nchw(y.float().cpu(), nimg, H, W), ref)
+    assert rel < 6e-3, rel
+    assert torch.equal(fused, plain)
+    if one is not None:
+        assert torch.equal(y, one)
