@@ -40,6 +40,13 @@ __device__ __forceinline__ f32x4 mfma16x16x32(f16x8 a, f16x8 b, f32x4 c) {
 
 template <typename T> __device__ __forceinline__ float to_f32(T x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f32(float x) { return (T)x; }
+// Round an fp32 result to T in two steps (fp32 first, then T), as torch's half kernels do.  Without the empty asm
+// the backend may fuse fma + convert into v_fma_mixlo_f16, which rounds the exact product-sum to f16 once: a
+// different f16 value at double-rounding ties, so two kernels that should agree bitwise would not.
+template <typename T> __device__ __forceinline__ T round_f32(float x) {
+  asm("" : "+v"(x));
+  return (T)x;
+}
 
 // load/store helpers over the three storage types
 template <typename T> __device__ __forceinline__ float ldf(const void* p, long long i) {

@@ -459,7 +459,8 @@ extern "C" int fd_group_norm_affine(const void* x, const void* part, int part_ro
 
 // ------------------------------------------------------------------------------------------------
 // LayerNorm: one wave per row, 4 rows per 256-thread block; row kept in registers (C <= 2048).  Every output path
-// computes fma((x - mean) * rstd, gamma, beta) explicitly, so the y / e4m3 / MX forms round identically.
+// computes fma((x - mean) * rstd, gamma, beta) explicitly and rounds it fp32 -> T (round_f32), so the y / e4m3 / MX
+// forms round identically.
 // Q8 = 1: instead of y, write the row quantized to e4m3 for fd_gemm_e4m3 (the use_fp8 model): the LayerNorm output is
 // rounded to T first and then quantized exactly as fd_quant_rows_e4m3 does, so LN + quant fused == LN; quant.
 // Q8 = 2: the same rounded output as MX e4m3 (fd_quant_rows_mx's bytes): a 32-element block = 4 consecutive lanes.
@@ -525,7 +526,8 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
       const int v = lane + k * 64;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        outs[k][i] = v < VPR ? (T)__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3], b4[k][i >> 2][i & 3])
+        outs[k][i] = v < VPR ? round_f32<T>(__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3],
+                                                           b4[k][i >> 2][i & 3]))
                              : (T)0.f;
     }
 #pragma unroll
@@ -556,7 +558,8 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
       if (v < VPR) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          outs[k][i] = (T)__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3], b4[k][i >> 2][i & 3]);
+          outs[k][i] =
+              round_f32<T>(__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3], b4[k][i >> 2][i & 3]));
           amax = fmaxf(amax, fabsf((float)outs[k][i]));
         }
       }
@@ -586,7 +589,7 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
       V8 out;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        out[i] = (T)__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3], b4[k][i >> 2][i & 3]);
+        out[i] = round_f32<T>(__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3], b4[k][i >> 2][i & 3]));
       *(V8*)(yr + v * 8) = out;
     }
   }
@@ -625,9 +628,6 @@ extern "C" int fd_layer_norm_mx(const void* x, long long ldx, void* q, long long
   if (((unsigned long long)q) & 7) return FD_ERR_ARG;
   if (M <= 0 || C <= 0 || C % 32 || C > 2048 || (ldx & 7) || (ldq & 7) || ldq < C || lds < C / 32)
     return FD_ERR_SHAPE;
-  // bf16 only (the use_fp8 model's compute type): the f16 instance rounded exact e4m3 ties differently from
-  // fd_layer_norm + fd_quant_rows_mx (3 of 2.6 M bytes, tests/test_fp8_gpu.py), so it is not offered
-  if (dtype != FD_BF16) return FD_ERR_DTYPE;
   hipStream_t s = (hipStream_t)stream;
   FD_DISPATCH_T(dtype, hipLaunchKernelGGL((layer_norm_kernel<T, 2>), dim3((M + 3) / 4), dim3(256), 0, s,
                                           (const T*)x, ldx, (T*)nullptr, 0, gamma, beta, M, C, eps, (uint8_t*)q, ldq,

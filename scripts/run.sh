@@ -28,7 +28,7 @@ for ph in "$@"; do
       timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ "${K[@]}" > $out.log 2>&1
       rc=$?; tail -4 $out.log ;;
     tfile)
-      f=${arg%%:*}; k=${arg#*:}; [ "$k" = "$arg" ] && k=""
+      f=${arg%%:*}; k=${arg#*:}; [ "$k" = "$arg" ] && k=""; out=gpurun_out/${TAG}_$(basename $f .py)
       if [ -n "$k" ]; then K=(-k "$k"); else K=(); fi
       timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "$f" "${K[@]}" > $out.log 2>&1
       rc=$?; tail -8 $out.log ;;
