@@ -55,10 +55,10 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_FP8_TFLOPS = 5000.0  # dense e4m3 (block-scaled MFMA), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-# committed rocprofv3 PMC traffic passes, newest first (scripts/r02_prof.sh + scripts/traffic_from_pmc.py)
-TRAFFIC_FILES = [os.path.join(ROOT, "profiles", f) for f in
-                 ("r03c_gemm_traffic.json", "r03c_gemm_traffic_fp8.json", "r03_gemm_traffic.json",
-                  "r03_gemm_traffic_fp8.json", "r02f_gemm_traffic.json")]
+# committed rocprofv3 PMC traffic passes (scripts/prof.sh + scripts/traffic_from_pmc.py), newest round first: the
+# file names start with the round tag (r04 > r03c > r03 > r02f), so a reverse name sort is newest first
+TRAFFIC_FILES = sorted((os.path.join(ROOT, "profiles", f) for f in os.listdir(os.path.join(ROOT, "profiles"))
+                        if "_gemm_traffic" in f and f.endswith(".json")), reverse=True)
 
 
 def parse(argv=None):

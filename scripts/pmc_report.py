@@ -23,7 +23,7 @@ def family(name):
     # e4m3 operands: the 4-wave kernels, and gemm8 instantiated on uint8_t (per-row) / mx8_t (MX) operands
     if "gemm_e4m3" in name or "gemm8_kernelIh" in name or "gemm8_kernelI5mx8_t" in name:
         return "gemm_e4m3"
-    if "gemm_kernel" in name or "gemm8_kernel" in name or "gemm256_kernel" in name:
+    if "gemm_kernel" in name or "gemm8_kernel" in name or "gemm256_kernel" in name or "conv_halo_kernel" in name:
         return "gemm"
     if "quant_rows_e4m3" in name or "layer_norm_e4m3" in name:
         return "fp8_quant"

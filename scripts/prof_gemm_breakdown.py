@@ -15,9 +15,9 @@ n = len(starts) - skip
 by = defaultdict(list)
 for r in win:
     k = r["Kernel_Name"]
-    if "gemm" not in k:
+    if "gemm" not in k and "conv_halo" not in k:
         continue
-    m = re.search(r"(gemm8?_kernel)I(.*?)Ev14fd_", k)
+    m = re.search(r"(gemm8?_kernel|conv_halo_kernel)I(.*?)Ev14fd_", k)
     targs = (m.group(1) + " " + m.group(2)) if m else k[:60]
     targs = targs.replace("DF16b", "bf16").replace("DF16_", "f16")
     by[(targs, r["Grid_Size_X"], r["Workgroup_Size_X"])].append(

@@ -16,7 +16,7 @@ PEAK = 2500.0
 
 
 def is_gemm(n):
-    return ("gemm_kernel" in n or "gemm8_kernel" in n or "gemm256_kernel" in n) and "e4m3" not in n and "DF16b" in n
+    return ("gemm_kernel" in n or "gemm8_kernel" in n or "gemm256_kernel" in n or "conv_halo_kernel" in n) and "e4m3" not in n and "DF16b" in n
 
 
 def main(trace, bench_log, warmup=3):

@@ -15,5 +15,6 @@ T=$(find $D -name "*kernel_trace.csv" | head -1)
 python3 scripts/prof_window.py $T 3 > gpurun_out/${TAG}_step_window.txt || exit 1
 python3 scripts/roofline_check.py $T gpurun_out/${TAG}_prof_bench.log 3 > gpurun_out/${TAG}_roofline_check.json || exit 1
 python3 scripts/prof_gemm_breakdown.py $T 3 > gpurun_out/${TAG}_gemm_instances.txt 2>&1 || true
+python3 scripts/prof_positions.py $T 3 > gpurun_out/${TAG}_positions.txt 2>&1 || true
 cp $(find $D -name "*kernel_stats.csv" | head -1) gpurun_out/${TAG}_kernel_stats.csv
 head -20 gpurun_out/${TAG}_step_window.txt; cat gpurun_out/${TAG}_roofline_check.json
