@@ -16,7 +16,10 @@ PEAK = 2500.0
 
 
 def is_gemm(n):
-    return ("gemm_kernel" in n or "gemm8_kernel" in n or "gemm256_kernel" in n or "conv_halo_kernel" in n) and "e4m3" not in n and "DF16b" in n
+    # rocprofv3 leaves some names mangled (DF16b = bf16) and demangles others (__hip_bfloat16, or the template
+    # arguments lost: "conv_halo_kernel<bool _Accum, ...>"); the C2 UNet has no fp16 GEMM / conv launches
+    fam = "gemm_kernel" in n or "gemm8_kernel" in n or "gemm256_kernel" in n or "conv_halo_kernel" in n
+    return fam and "e4m3" not in n and "DF16_" not in n and "__half" not in n
 
 
 def main(trace, bench_log, warmup=3):

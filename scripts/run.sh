@@ -39,12 +39,14 @@ for ph in "$@"; do
     pmc)
       bash scripts/prof.sh $arg ${TAG}_${arg}_pmc > $out.log 2>&1; rc=$?; tail -3 $out.log ;;
     probe)
+      sc=${arg%%,*}; out=gpurun_out/${TAG}_$(basename $sc .py)
       timeout -k 10 400 python -u ${arg//,/ } > $out.log 2>&1; rc=$?; tail -25 $out.log ;;
-    ab)
+    ab|abv)  # abv: with the VAE decode leg (prints vae_decode_ms too)
       IFS=';' read -r reps rest <<< "$arg"; IFS=';' read -ra arms <<< "$rest"; : > $out.txt
+      if [ $name = abv ]; then VA=""; else VA="--no-vae"; fi
       for r in $(seq $reps); do for e in "${arms[@]}"; do
-        env $e timeout -k 10 300 python bench.py --no-cpu-baseline --no-vae --no-c3 --no-pipeline --steps 30 > $out.run 2>&1 || { rc=$?; break 2; }
-        echo "$e $(tail -1 $out.run | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d.get("roofline", {}).get("frac"))')" | tee -a $out.txt
+        env $e timeout -k 10 300 python bench.py --no-cpu-baseline $VA --no-c3 --no-pipeline --steps 30 > $out.run 2>&1 || { rc=$?; break 2; }
+        echo "$e $(tail -1 $out.run | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d.get("roofline", {}).get("frac"), d.get("vae_decode_ms"))')" | tee -a $out.txt
         rc=0
       done; done ;;
     *) echo "unknown phase $ph"; rc=2 ;;
