@@ -899,3 +899,55 @@ extern "C" int fd_softmax_rows(const float* s, void* p, int R, int C, long long 
   FD_LAUNCH_CHECK();
   return FD_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Cross-attention as two GEMMs (fdhip/unet.py, HipUNet.set_context): per prompt row r the score matrix
+// B1[r] = scale * blockdiag_h(K_r,h) . W_q' (rows h * slot + j, one per (head, key), W_q' = W_q diag(gamma) of the
+// folded norm2) is written by a batched GEMM; this kernel adds the LayerNorm-fold constants of those rows:
+//   c[n] = sum_k B1[n][k]                                   (of the stored 16-bit values, fixed order)
+//   d[n] = scale * sum_e K_r[j][h * 64 + e] * dq[h * 64 + e]  (dq = W_q . beta, fp32; 0 for pad keys j >= Lk)
+// so the score GEMM's epilogue computes rstd (x . B1^T - mean c) + d = scale * LN(x) W_q^T K^T.  One wave per row.
+template <typename T>
+__global__ void __launch_bounds__(256) xattn_consts_kernel(const T* __restrict__ B1, long long ldb, int rows, int K,
+                                                            const T* __restrict__ kv, long long ldkv,
+                                                            long long kv_rstride, const float* __restrict__ dq,
+                                                            int heads, int slot, int Lk, float scale,
+                                                            float* __restrict__ c, float* __restrict__ d) {
+  typedef typename VecT<T>::v8 V8;
+  const int lane = threadIdx.x & 63;
+  const long long n = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= rows) return;
+  const T* row = B1 + n * ldb;
+  float s = 0.f;
+  for (int v = lane; v < K / 8; v += 64) {
+    const V8 x = *(const V8*)(row + v * 8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += (float)x[i];
+  }
+  s = wave_sum(s);
+  const int j = (int)(n % slot), h = (int)((n / slot) % heads);
+  const long long r = n / ((long long)slot * heads);
+  float t = 0.f;
+  if (j < Lk) t = (float)kv[r * kv_rstride + (long long)j * ldkv + h * 64 + lane] * dq[h * 64 + lane];
+  t = wave_sum(t);
+  if (lane == 0) {
+    c[n] = s;
+    d[n] = j < Lk ? scale * t : 0.f;
+  }
+}
+
+extern "C" int fd_xattn_consts(const void* B1, long long ldb, int rows, int K, const void* kv, long long ldkv,
+                               long long kv_rstride, const float* dq, int heads, int slot, int Lk, float scale,
+                               float* c, float* d, int dtype, void* stream) {
+  if (!B1 || !kv || !dq || !c || !d) return FD_ERR_ARG;
+  if (rows <= 0 || K <= 0 || K % 8 || ldb % 8 || heads <= 0 || slot <= 0 || Lk <= 0 || Lk > slot ||
+      rows % (slot * heads))
+    return FD_ERR_SHAPE;
+  if ((((unsigned long long)B1) & 15)) return FD_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL(xattn_consts_kernel<T>, dim3((rows + 3) / 4), dim3(256), 0, st,
+                                          (const T*)B1, ldb, rows, K, (const T*)kv, ldkv, kv_rstride, dq, heads,
+                                          slot, Lk, scale, c, d));
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}

@@ -34,7 +34,7 @@ __device__ __forceinline__ void hvm() {
 constexpr int PW = 18;  // patch width: 16 output columns + halo
 constexpr int TR = 7;   // tap of chunk c at which chunk c + 1's patch is waited for and transformed
 
-template <typename T, int TH, int BN, bool GNI, bool SK>
+template <typename T, int TH, int BN, bool GNI, bool SK, int NS>
 __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, float* __restrict__ slabs,
                                                           unsigned* __restrict__ counters) {
   typedef typename VecT<T>::v8 V8;
@@ -45,7 +45,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   constexpr int PATCH = PIXR * 128;
   constexpr int AFF = GNI ? 1024 : 0;  // the chunk's 64 affine pairs (512 B, DMA'd as 1 KB) after each patch
   constexpr int PBUF = PATCH + AFF;
-  constexpr int NS = 3;
+  static_assert(NS >= 3 && NS <= 5, "weight ring depth");
   constexpr int STAGE = BN * 128;
   constexpr int RING = 2 * PBUF;
   constexpr int SMEM_MAIN = RING + NS * STAGE;
@@ -199,9 +199,11 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = mfma16x16x32(af[mi], bf[ni], acc[mi][ni]);
   };
-  // B-waves: all but the youngest `ahead` weight stages landed (ahead <= 2)
+  // B-waves: all but the youngest `ahead` weight stages landed (ahead <= NS - 1)
   auto wait_b = [&](int ahead) {
-    if (ahead >= 2) hvm<2 * PER_B>();
+    if (NS >= 5 && ahead >= 4) hvm<(NS >= 5 ? 4 : 0) * PER_B>();
+    else if (NS >= 4 && ahead >= 3) hvm<(NS >= 4 ? 3 : 0) * PER_B>();
+    else if (ahead >= 2) hvm<2 * PER_B>();
     else if (ahead == 1) hvm<PER_B>();
     else hvm<0>();
   };
@@ -426,13 +428,17 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
 }
 
 struct HaloPlan {
-  int th, bn, tiles, sk;  // tiles: output tiles (workgroups = tiles * (1 + sk))
+  int th, bn, tiles, sk, ns;  // tiles: output tiles (workgroups = tiles * (1 + sk)); ns: weight ring depth
 };
 
 // Eligibility and tile plan, from per-image quantities only (m_ref: rows of one TLC tile's forward), so batching
 // tiles never moves a launch between this kernel and the implicit GEMM (bitwise batch invariance).
 int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
-  if (!fd_knob(FDK_CONV_HALO)) return 0;
+  // FD_CONV_HALO: 0 off; 1 on, except the convs the 256 x 256 kernel takes (the VAE's 256 / 512-channel levels at
+  // 256^2 - 512^2 and the upsample convs: its intake beats the 128 / 160-column halo tile there even with the
+  // GroupNorm pass, probes/conv_ab.py); 2 on wherever eligible
+  const int mode = fd_knob(FDK_CONV_HALO);
+  if (!mode || (mode == 1 && gemm256_takes(p))) return 0;
   if (!p->conv || p->batch > 1 || p->stride != 1 || p->pad != 1 || p->A2 || p->K != 9 * p->Cin) return 0;
   if (p->Cin % 64 || p->lda < p->Cin || p->lda % 8 || p->ldb % 8 || p->ldc % 8) return 0;
   if (p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out || p->dtype != p->out_dtype || p->dtype == FD_F32) return 0;
@@ -460,6 +466,9 @@ int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
   pl->th = th;
   pl->bn = bn;
   pl->sk = sk;
+  // a 128-row tile's K step is half the MFMA work of a 256-row one: its weight stages need a deeper ring to cover
+  // the L2 latency (the 256-row tile's LDS holds only 3 stages)
+  pl->ns = th == 8 ? fd_knob(FDK_CONV_HALO_NS8) : 3;
   pl->tiles = (int)(p->nimg * ((p->Hout + th - 1) / th) * ((p->Wout + 15) / 16) * (p->N / bn));
   if (sk && pl->tiles > 32768) return 0;  // one split-K counter / flag per tile
   return 1;
@@ -473,21 +482,25 @@ int launch_halo(const fd_gemm_params* p, const HaloPlan& pl, hipStream_t s) {
   float* slabs = pl.sk ? (float*)((char*)p->ws + 65536 * sizeof(unsigned)) : nullptr;
   unsigned* cnt = pl.sk ? (unsigned*)p->ws : nullptr;
   const dim3 grid(pl.tiles * (1 + pl.sk));
-#define FD_HALO(TH_, BN_, SK_)                                                                                       \
-  if (pl.th == TH_ && pl.bn == BN_ && pl.sk == SK_) {                                                                \
+#define FD_HALO(TH_, BN_, SK_, NS_)                                                                                  \
+  if (pl.th == TH_ && pl.bn == BN_ && pl.sk == SK_ && pl.ns == NS_) {                                                \
     if (gi)                                                                                                          \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true, SK_>), grid, dim3(512), 0, s, *p, slabs, cnt);        \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true, SK_, NS_>), grid, dim3(512), 0, s, *p, slabs, cnt);   \
     else                                                                                                             \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, SK_>), grid, dim3(512), 0, s, *p, slabs, cnt);       \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, SK_, NS_>), grid, dim3(512), 0, s, *p, slabs, cnt);  \
     FD_LAUNCH_CHECK();                                                                                               \
     return FD_OK;                                                                                                    \
   }
-  FD_HALO(16, 160, 0)
-  FD_HALO(16, 128, 0)
-  FD_HALO(8, 160, 0)
-  FD_HALO(8, 128, 0)
-  FD_HALO(8, 160, 1)
-  FD_HALO(8, 128, 1)
+  FD_HALO(16, 160, 0, 3)
+  FD_HALO(16, 128, 0, 3)
+  FD_HALO(8, 160, 0, 3)
+  FD_HALO(8, 128, 0, 3)
+  FD_HALO(8, 160, 1, 3)
+  FD_HALO(8, 128, 1, 3)
+  FD_HALO(8, 160, 0, 5)
+  FD_HALO(8, 128, 0, 5)
+  FD_HALO(8, 160, 1, 5)
+  FD_HALO(8, 128, 1, 5)
 #undef FD_HALO
   return FD_ERR_ARG;
 }

@@ -27,14 +27,14 @@ __device__ __forceinline__ void wait_vmcnt() {
 // its own 4 MiB L2).  swz = 1: give each XCD a contiguous chunk of the tile space (bijective remap,
 // cdna_hip_programming.md section 5 "XCD swizzle must be bijective"), and walk that chunk in groups of
 // GROUP_M tile rows so the ~32 tiles an XCD runs at once share A row-panels and B column-panels in L2.
-__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int swz, int& tm, int& tn) {
+__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int swz, int GROUP_M, int& tm,
+                                            int& tn) {
   if (!swz) {
     tm = bid / tiles_n;
     tn = bid % tiles_n;
     return;
   }
   const int pid = xcd_remap(bid, nwg);
-  constexpr int GROUP_M = 4;
   const int group = pid / (GROUP_M * tiles_n);
   const int first_m = group * GROUP_M;
   const int gsz = min(tiles_m - first_m, GROUP_M);
@@ -93,11 +93,17 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
   // swz bits 4-5: diagnostic mode (FD_GEMM_MODE, benchmarks only): 1 = operand loads only (no LDS reads,
   // no MFMA), 2 = LDS reads + MFMA only (no global loads).  0 in every product launch.
-  const int mode = swz >> 4;
+  const int mode = (swz >> 4) & 3;
+  const int group_m = (swz >> 8) > 0 ? (swz >> 8) : 4;  // bits 8+: tile-row group height (host-planned)
   swz &= 1;
   int tm, tn;
-  tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, swz, tm, tn);
+  tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, swz, group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
+  // batch offsets (two-level: z -> (z / batch_inner, z % batch_inner)) and the per-row-group B slot (bsel)
+  const int zb = blockIdx.z;
+  const int zi = p.batch_inner > 1 ? zb % p.batch_inner : zb, zo = p.batch_inner > 1 ? zb / p.batch_inner : 0;
+  const int bslot = p.bsel_rows > 0 ? (p.bsel_mod > 0 ? (m0 / p.bsel_rows) % p.bsel_mod : m0 / p.bsel_rows) : 0;
+  const long long bsn = (long long)bslot * p.bsel_strideN;
   // residual prefetch (64 x 160 tiles, one workgroup per CU for the M = 2048 projections): the epilogue's
   // residual rows are requested before the first operand stage, so no memory round trip is left between
   // the last MFMA and the stores
@@ -108,7 +114,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   const bool pf = PREF && p.residual && (p.ldr % 8 == 0) && ((((unsigned long long)p.residual) & 15) == 0) &&
                   m0 + BM <= p.M && n0 + BN <= p.N;
   if (PREF && pf) {
-    const TO* Rp = (const TO*)p.residual + (long long)blockIdx.z * p.strideR;
+    const TO* Rp = (const TO*)p.residual + (long long)zb * p.strideR;
 #pragma unroll
     for (int it = 0; it < (PREF ? PF_ITER : 1); ++it) {
       const int e = threadIdx.x + it * 256 * KS;
@@ -129,11 +135,11 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
 #pragma unroll
       for (int i = 0; i < (LNF ? 4 : 1); ++i) lnv4[i] = src[min(i, lnP / 2 - 1)];
     }
-    if (tid < BN) lncv = p.ln_c[min(n0 + tid, p.N - 1)];
+    if (tid < BN) lncv = p.ln_c[bsn + min(n0 + tid, p.N - 1)];
   }
-  const long long bz = blockIdx.z;
-  const T* __restrict__ A = (const T*)p.A + bz * p.strideA;
-  const T* __restrict__ Bw = (const T*)p.B + bz * p.strideB;
+  const long long bz = zb;
+  const T* __restrict__ A = (const T*)p.A + zi * p.strideA + zo * p.strideA_o;
+  const T* __restrict__ Bw = (const T*)p.B + zi * p.strideB + zo * p.strideB_o + bslot * p.bsel_strideB;
   const int M = p.M, N = p.N, K = p.K;
   const int lrow = lane >> 3, slot = lane & 7;
 
@@ -299,7 +305,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   // phase 1 writes alpha * acc (GEGLU: the combined h * gelu(g), bias hoisted); phase 2 (whole-row, 8 columns
   // per thread) adds bias / row-group bias, applies the activation and the residual with 16-B vector loads
   // issued together -- no per-element branches or dependent loads (they serialise a 1-WG/CU launch).
-  const float* __restrict__ bias = p.bias;
+  const float* __restrict__ bias = p.bias ? p.bias + bsn : nullptr;
   const float* __restrict__ rbias = p.rowbias;
   const int act = p.act;
   if (lnf) {  // (mean, rstd) per row from the partials, fp64 fold in a fixed order
@@ -372,7 +378,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
   __syncthreads();
 
   // ---- phase 2
-  TO* __restrict__ C = (TO*)p.C + bz * p.strideC;
+  TO* __restrict__ C = (TO*)p.C + zi * p.strideC + zo * p.strideC_o;
   const TO* __restrict__ R = p.residual ? (const TO*)p.residual + bz * p.strideR : nullptr;
   const int Nout = GEGLU ? N / 2 : N;
   const int n0o = GEGLU ? n0 / 2 : n0;
@@ -604,6 +610,30 @@ static bool gn_ok4(const fd_gemm_params* p, int cfg) {
          (!p->rowbias || p->rowbias_ld % 4 == 0);
 }
 
+// Tile-row group height of the XCD-chunked walk (tile_coords): the ~tiles/8 tiles of one XCD chunk should touch as
+// few A rows and B columns as possible (each XCD's L2 fetches its chunk's panels once).  Counted exactly on the
+// first chunk's tiles for every power-of-two height; ties keep the smaller height.
+static int plan_group_m(long long tiles_total, int tiles_m, int tiles_n, int bm, int bn) {
+  if (!fd_knob(FDK_GEMM_GMP)) return 4;
+  const int per_xcd = (int)((tiles_total + 7) / 8);
+  if (per_xcd > 4096) return 4;
+  int best = 4;
+  long long bestc = -1;
+  for (int g = 1; g <= tiles_m && g <= 64; g *= 2) {
+    // rows / columns touched by pids [0, per_xcd) under tile_coords (the remap is bijective and chunk-contiguous)
+    const int rows_seen = per_xcd >= g * tiles_n ? g * (int)((per_xcd + g * tiles_n - 1) / (g * tiles_n))
+                                                 : g;
+    const int cols_seen = per_xcd >= g * tiles_n ? tiles_n : (per_xcd + g - 1) / g;
+    const long long c = (long long)(rows_seen < tiles_m ? rows_seen : tiles_m) * bm +
+                        (long long)(cols_seen < tiles_n ? cols_seen : tiles_n) * bn;
+    if (bestc < 0 || c < bestc) {
+      bestc = c;
+      best = g;
+    }
+  }
+  return best;
+}
+
 template <typename T, typename TO>
 static int dispatch_tiles(fd_gemm_params* p0, hipStream_t s) {
   const int g_cfg = fd_knob(FDK_GEMM_CFG), g_ns = fd_knob(FDK_GEMM_NS), g_ks = fd_knob(FDK_GEMM_KS);
@@ -623,12 +653,14 @@ static int dispatch_tiles(fd_gemm_params* p0, hipStream_t s) {
   // covers the launch (one WG per CU either way).
   const int ns = g_ns ? g_ns : ((tiles <= 256 && p->K >= 512) ? 4 : 2);
   const int ks = g_ks ? g_ks : 2;
+  const int tm_ = (p->M + CFG_BM[cfg] - 1) / CFG_BM[cfg], tn_ = (p->N + CFG_BN[cfg] - 1) / CFG_BN[cfg];
+  const int swz = g_swz | (plan_group_m(tm_ * (long long)tn_, tm_, tn_, CFG_BM[cfg], CFG_BN[cfg]) << 8);
   int rc;
   switch (cfg) {
-    case CFG_128x128: rc = dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, ks, g_swz); break;
-    case CFG_64x160: rc = dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, ks, g_swz); break;
-    case CFG_128x64: rc = dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, ks, g_swz); break;
-    default: rc = dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, ks, g_swz);
+    case CFG_128x128: rc = dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, ks, swz); break;
+    case CFG_64x160: rc = dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, ks, swz); break;
+    case CFG_128x64: rc = dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, ks, swz); break;
+    default: rc = dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, ks, swz);
   }
   if (rc == FD_OK && q.gn_part) p0->gn_done = 128;
   return rc;
@@ -717,6 +749,21 @@ extern "C" int fd_gemm(fd_gemm_params* p, void* stream) {
                     (p->out_dtype != FD_BF16 && p->out_dtype != FD_F16)))
     return FD_ERR_SHAPE;
   if (p->ln_in && (p->K % 320 || p->K > 1280 || p->batch > 1 || p->conv || !p->ln_c)) return FD_ERR_SHAPE;
+  const bool sm = p->act == FD_ACT_SOFTMAX;
+  if (sm && (p->N % 160 || p->sm_group != 80 || p->sm_len < 1 || p->sm_len > 80 || p->residual || p->rowbias ||
+             p->conv || p->batch > 1 || p->ln_out || p->gn_part || p->dtype == FD_F32 ||
+             (p->out_dtype != FD_BF16 && p->out_dtype != FD_F16)))
+    return FD_ERR_SHAPE;
+  const bool bsel = p->bsel_rows > 0;
+  if (bsel && (p->bsel_rows % 256 || p->batch > 1 || p->conv || p->bsel_mod < 0)) return FD_ERR_SHAPE;
+  if (p->batch_inner > 1 && (p->batch <= 1 || p->batch % p->batch_inner || bsel)) return FD_ERR_SHAPE;
+  if (sm || bsel) {  // the eight-wave kernels (softmax: only there), else the 4-wave kernel (bsel)
+    const int r8 = fd_gemm8_try(p, stream);
+    if (r8 < 0) return r8;
+    if (r8 == 1) return FD_OK;
+    if (sm) return FD_ERR_SHAPE;
+    FD_DISPATCH_T(p->dtype, FD_DISPATCH_O(p->out_dtype, return dispatch_tiles<T, TO>(p, (hipStream_t)stream)));
+  }
   if (p->conv) {  // 3x3 stride-1 convs: the halo-staged kernel where it applies (the only one taking gi_affine)
     const int rh = fd_conv_halo_try(p, stream);
     if (rh < 0) return rh;

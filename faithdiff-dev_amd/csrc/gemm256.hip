@@ -343,6 +343,24 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
 
 }  // namespace
 
+// Whether fd_gemm256_try takes this launch (also asked by the halo-staged conv's planner, which leaves these convs
+// to this kernel).
+int gemm256_takes(const fd_gemm_params* p) {
+  const int min_tiles = fd_knob(FDK_GEMM256_MIN_TILES);
+  const int enabled = fd_knob(FDK_GEMM256);  // tests compare against gemm8 in one process
+  if (!enabled || p->batch > 1 || p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out || p->N % 256 || p->K % 32 ||
+      p->bsel_rows > 0 || p->act == FD_ACT_SOFTMAX)
+    return 0;
+  if (p->conv && (p->Cin % 32 || (p->C1 > 0 && p->C1 % 32))) return 0;
+  const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
+  if ((long long)((m_ref + 255) / 256) * (p->N / 256) < min_tiles) return 0;
+  if (p->K % 64 || (p->conv && (p->Cin % 64 || (p->C1 > 0 && p->C1 % 64)))) return 0;  // 64-deep K tiles
+  // 32-bit element offsets inside the kernel (B rows; conv source pixels)
+  if ((long long)p->N * p->ldb >= (1LL << 31)) return 0;
+  if (p->conv && (long long)p->nimg * p->Hin * p->Win * (p->lda > p->Cin ? p->lda : p->Cin) >= (1LL << 31)) return 0;
+  return 1;
+}
+
 // Returns 1 and launches when this kernel takes the GEMM, 0 when it does not apply, < 0 on error.  Taken for
 // N % 256 == 0, no GEGLU / LayerNorm fold / batching, and at least 192 tiles of 256 x 256 counted from the
 // per-TLC-tile row count m_ref (so batching tiles never changes the kernel choice: bitwise batch-invariant).
@@ -364,17 +382,7 @@ extern "C" int fd_gemm256_try(fd_gemm_params* p0, void* stream) {
     if (!ok) q.gn_part = nullptr;
   }
   const fd_gemm_params* p = &q;
-  const int min_tiles = fd_knob(FDK_GEMM256_MIN_TILES);
-  const int enabled = fd_knob(FDK_GEMM256);  // tests compare against gemm8 in one process
-  if (!enabled || p->batch > 1 || p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out || p->N % 256 || p->K % 32)
-    return 0;
-  if (p->conv && (p->Cin % 32 || (p->C1 > 0 && p->C1 % 32))) return 0;
-  const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
-  if ((long long)((m_ref + 255) / 256) * (p->N / 256) < min_tiles) return 0;
-  if (p->K % 64 || (p->conv && (p->Cin % 64 || (p->C1 > 0 && p->C1 % 64)))) return 0;  // 64-deep K tiles
-  // 32-bit element offsets inside the kernel (B rows; conv source pixels)
-  if ((long long)p->N * p->ldb >= (1LL << 31)) return 0;
-  if (p->conv && (long long)p->nimg * p->Hin * p->Win * (p->lda > p->Cin ? p->lda : p->Cin) >= (1LL << 31)) return 0;
+  if (!gemm256_takes(p)) return 0;
   const int tiles_m = (p->M + 255) / 256, tiles_n = p->N / 256;
   const long long tiles = (long long)tiles_m * tiles_n;
   if (tiles > 0x7fffffff) return FD_ERR_SHAPE;

@@ -122,7 +122,12 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   constexpr int SC_OFF = LNC_OFF + (LNF ? BM * 8 + BN * 4 : 0);
   constexpr int SCL_OFF = SC_OFF + (F8 && !MXI ? BM * 4 : 0);
   // MX: the ring's block-scale dwords (NS stages x BM rows) after that
-  constexpr int SMEM = SCL_OFF + (MXI ? NS * SCR : 0);
+  constexpr int SMX_END = SCL_OFF + (MXI ? NS * SCR : 0);
+  // softmax epilogue (fd_gemm_params.sm_*, the cross-attention score GEMM): 160-column 16-bit plain tiles; the
+  // tile's bias columns in LDS after that
+  constexpr bool SMK = BN == 160 && !GEGLU && !CONV && !F8;
+  constexpr int SMB_OFF = SMX_END;
+  constexpr int SMEM = SMX_END + (SMK ? BN * 4 : 0);
   static_assert(SMEM <= 163840, "LDS");
   static_assert(!GEGLU || (WN % 32 == 0), "GEGLU pairs must not straddle waves");
   // GroupNorm output statistics (fd_gemm_params.gn_part): one 8-column chunk per thread, reduction scratch after the
@@ -137,6 +142,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   float2* const ln_tab = (float2*)(smem + LNC_OFF);
   float* const ln_cs = (float*)(smem + LNC_OFF + BM * 8);
   float* const sc_tab = (float*)(smem + SC_OFF);
+  float* const sm_bias = (float*)(smem + SMB_OFF);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -164,6 +170,10 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   }
   const int tile_id = tm * tiles_n + tn;
   const int m0 = tm * BM, n0 = tn * BN;
+  // per-row-group B slot (bsel: each image row block multiplies its own prompt's matrices)
+  const int bslot = p.bsel_rows > 0 ? (p.bsel_mod > 0 ? (m0 / p.bsel_rows) % p.bsel_mod : m0 / p.bsel_rows) : 0;
+  const long long bsn = (long long)bslot * p.bsel_strideN;
+  const bool sm = SMK && p.act == FD_ACT_SOFTMAX;
   // LN-fold consumer: the producer's (sum, sumsq) partials of this tile's rows and ln_c of its columns,
   // requested before the first operand stage so their latency is hidden by the K loop (unconditional
   // 16-B loads, index clamped, lnP even: a conditional load per partial gets sunk into the fold's
@@ -177,8 +187,10 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
 #pragma unroll
       for (int i = 0; i < (LNF ? 4 : 1); ++i) lnv4[i] = src[min(i, lnP / 2 - 1)];
     }
-    if (tid < BN) lncv = p.ln_c[min(n0 + tid, p.N - 1)];
+    if (tid < BN) lncv = p.ln_c[bsn + min(n0 + tid, p.N - 1)];
   }
+  float smbv = 0.f;  // softmax: this thread's bias column, staged in LDS with ln_cs
+  if (SMK && sm && p.bias && tid < BN) smbv = p.bias[bsn + min(n0 + tid, p.N - 1)];
   float scv = 0.f;  // e4m3: this thread's row scale, requested ahead of the operand stages like the LN partials
   if (F8 && !MXI && tid < BM) scv = f8.a_scale[min(m0 + tid, M - 1)] * p.alpha;
   const int nk = K / KS;
@@ -186,7 +198,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   const int nkl = ke - kb;
 
   const T* __restrict__ A = (const T*)p.A;
-  const T* __restrict__ Bw = (const T*)p.B;
+  const T* __restrict__ Bw = (const T*)p.B + bslot * p.bsel_strideB;
   const T* __restrict__ A2 = (const T*)p.A2;
   const int lrow = lane >> 3, slot = lane & 7;
   const bool hi = (B_TOT % NW == 0) || w < B_TOT % NW;  // this wave issues B_I (not B_LO) B loads
@@ -337,6 +349,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   wait_ahead(min(nkl - 1, NS - 1));
   if (F8 && !MXI && tid < BM) sc_tab[tid] = scv;
   if (LNF && tid < BN) ln_cs[tid] = lncv;
+  if (SMK && tid < BN) sm_bias[tid] = smbv;
   if (LNF && tid < BM) {  // (mean, rstd) per row, fp64 fold in a fixed order; written once stage 0 (issued after
     // the partials) has landed, so the 17 partial registers are not live across the K loop; read after its barriers
     double s = 0.0, q = 0.0;
@@ -624,7 +637,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
   // stalled epilogue, so no per-element branches or loads.
   TO* __restrict__ C = (TO*)p.C;
   const TO* __restrict__ R = (const TO*)p.residual;
-  const float* __restrict__ bias = p.bias;
+  const float* __restrict__ bias = p.bias ? p.bias + bsn : nullptr;
   const float* __restrict__ rbias = p.rowbias;
   const int Nout = GEGLU ? N / 2 : N;
   const int n0o = GEGLU ? n0 / 2 : n0;
@@ -720,6 +733,52 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
       }
     }
     __syncthreads();
+    if constexpr (SMK) {
+      if (sm) {
+        // softmax over each row's two 80-column head groups: 4 lanes per (row, group), 20 columns each; the LayerNorm
+        // fold and the bias are applied here (phase 2 only rounds and stores); columns >= sm_len become 0
+        const int sl = p.sm_len;
+#pragma unroll 1
+        for (int e = tid; e < EROWS * 8; e += NTHR) {
+          const int r = e >> 3, g = (e >> 2) & 1, q = e & 3;
+          const int c0 = g * 80 + q * 20;
+          float v[20];
+#pragma unroll
+          for (int i = 0; i < 5; ++i) *(f32x4*)&v[4 * i] = *(const f32x4*)(ep + r * LDE + c0 + 4 * i);
+          float mu = 0.f, rs = 1.f;
+          if (lnf) {
+            const float2 st = ln_tab[half * EROWS + r];
+            mu = st.x;
+            rs = st.y;
+          }
+          float mx = -INFINITY;
+#pragma unroll
+          for (int i = 0; i < 20; ++i) {
+            float x = v[i];
+            if (lnf) x = rs * (x - mu * ln_cs[c0 + i]);
+            x += sm_bias[c0 + i];
+            v[i] = q * 20 + i < sl ? x : -INFINITY;
+            mx = fmaxf(mx, v[i]);
+          }
+          mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+          mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+          float sum = 0.f;
+#pragma unroll
+          for (int i = 0; i < 20; ++i) {
+            v[i] = q * 20 + i < sl ? __expf(v[i] - mx) : 0.f;
+            sum += v[i];
+          }
+          sum += __shfl_xor(sum, 1, 64);
+          sum += __shfl_xor(sum, 2, 64);
+          const float inv = 1.0f / sum;
+#pragma unroll
+          for (int i = 0; i < 20; ++i) v[i] *= inv;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) *(f32x4*)(ep + r * LDE + c0 + 4 * i) = *(const f32x4*)&v[4 * i];
+        }
+        __syncthreads();
+      }
+    }
     if (interior) {
 #pragma unroll 1
     for (int e0 = 0; e0 < EROWS * VPR; e0 += NTHR * ITER) {
@@ -732,7 +791,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
         *(f32x4*)&v[it][0] = *(const f32x4*)(ep + r * LDE + cv * 8);
         *(f32x4*)&v[it][4] = *(const f32x4*)(ep + r * LDE + cv * 8 + 4);
-        if (!GEGLU && bias) {
+        if (!GEGLU && !sm && bias) {
           *(f32x4*)&bv[it][0] = *(const f32x4*)(bias + n);
           *(f32x4*)&bv[it][4] = *(const f32x4*)(bias + n + 4);
         }
@@ -748,7 +807,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         const int e = e0 + tid + it * NTHR;
         const int r = e / VPR, cv = e % VPR;
         const int m = m0 + half * EROWS + r, n = n0o + cv * 8;
-        if (!GEGLU) {
+        if (!GEGLU && !sm) {
           if (lnf) {
             const float2 st = ln_tab[half * EROWS + r];
 #pragma unroll
@@ -836,7 +895,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         float ls = 0.f, lq = 0.f;
         for (int i = 0; i < 8 && n + i < Nout; ++i) {
           float x = ep[r * LDE + cv * 8 + i];
-          if (!GEGLU) {
+          if (!GEGLU && !sm) {
             if (lnf) {
               const float2 st = ln_tab[half * EROWS + r];
               x = st.y * (x - st.x * ln_cs[cv * 8 + i]);
@@ -985,6 +1044,29 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
   const int n128 = fd_knob(FDK_GEMM8_N128);
   if (n128 && p->conv && p->N == 128 && m_ref >= 262144) return 0;
   Plan8 q;
+  if (p->act == FD_ACT_SOFTMAX) {
+    // the attention-score GEMM: 160-column tiles (two 80-column head groups), one K pass (no split, so every tile
+    // shape gives the same bits and the actual M may pick it): the tile with the fewest operand bytes per CU,
+    // rounds on 256 CUs x (BM + BN)
+    if (p->N % 160) return 0;
+    int best = 0;
+    long long bc = 0;
+    for (int bm = 256; bm >= 64; bm /= 2) {
+      const long long tiles = (long long)((p->M + bm - 1) / bm) * (p->N / 160);
+      const long long c = (tiles + 255) / 256 * (bm + 160);
+      if (!best || c < bc) {
+        best = bm;
+        bc = c;
+      }
+    }
+    q.bm = best;
+    q.bn = 160;
+    q.nw = best == 256 ? 8 : 4;
+    q.waves_m = best == 256 ? 8 : 2;
+    q.ns = 3;
+    q.S = 1;
+    goto planned;
+  }
   if (p->ln_out) {
     // LN-fold producer: only a 160-column tile writes the partial layout the consumers read.  Long K (the ff out
     // of the 32^2 level, 2048 x 1280 x 5120 at C2): 128 x 160 tiles with K split in two (pairwise combine),

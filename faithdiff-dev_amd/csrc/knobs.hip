@@ -43,9 +43,11 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_FLASH_SWZ", 1},           // flash attention XCD-aware block order
     {"FD_FLASH_WAVES", 4},         // flash attention waves per workgroup (2, 4, 8)
     {"FD_FLASH_QPW", 0},           // flash attention queries per wave (0: by launch size, 16, 32)
-    {"FD_CONV_HALO", 1},           // 3x3 stride-1 convs on the halo-staged kernel where eligible
+    {"FD_CONV_HALO", 1},           // 3x3 stride-1 convs on the halo-staged kernel where eligible (1: not the gemm256 ones; 2: all)
     {"FD_CONV_HALO_MIN_TILES", 192},  // ... when it has at least this many tiles (per TLC tile's rows, m_ref)
     {"FD_CONV_HALO_SPLIT", 1},     // ... or twice that many with the input channels split in two (pairwise combine)
+    {"FD_CONV_HALO_NS8", 5},       // weight-ring depth of its 128-row tiles (3 or 5)
+    {"FD_GEMM_GMP", 1},            // 4-wave kernel: tile-row group height planned per launch (0: fixed 4)
 };
 int g_knobs[FDK_COUNT];
 bool g_init = false;

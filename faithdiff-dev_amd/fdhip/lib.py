@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FD_LIB_PATH") or os.path.join(_HERE, "libfaithdiff_hip.so")
 
 FD_BF16, FD_F16, FD_F32 = 0, 1, 2
-ACT = {"none": 0, "silu": 1, "gelu": 2, "quickgelu": 3, "geglu": 4, "lrelu": 5}
+ACT = {"none": 0, "silu": 1, "gelu": 2, "quickgelu": 3, "geglu": 4, "lrelu": 5, "softmax": 6}
 _ERR = {-1: "FD_ERR_SHAPE", -2: "FD_ERR_DTYPE", -3: "FD_ERR_ARCH", -4: "FD_ERR_HIP", -5: "FD_ERR_ARG"}
 
 c_vp, c_int, c_ll, c_f, c_char_p = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_char_p
@@ -37,6 +37,9 @@ class GemmParams(ctypes.Structure):
         ("ln_out", c_vp), ("ln_in", c_vp), ("ln_c", c_vp), ("ln_eps", c_f),
         ("gn_part", c_vp), ("gn_groups", c_int), ("gn_hw", c_int), ("gn_done", c_int),
         ("gi_affine", c_vp), ("gi_silu", c_int),
+        ("batch_inner", c_int), ("strideA_o", c_ll), ("strideB_o", c_ll), ("strideC_o", c_ll),
+        ("bsel_rows", c_int), ("bsel_mod", c_int), ("bsel_strideB", c_ll), ("bsel_strideN", c_ll),
+        ("sm_group", c_int), ("sm_len", c_int),
     ]
 
 
@@ -71,6 +74,8 @@ _SIGS = {
     "fd_flash_attn_d512": (c_int, [c_vp, c_vp, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_int, c_int, c_f, c_int, c_vp]),
     "fd_mha_seq_axis": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "fd_softmax_rows": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_f, c_int, c_vp]),
+    "fd_xattn_consts": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_ll, c_ll, c_vp, c_int, c_int, c_int, c_f, c_vp, c_vp,
+                                c_int, c_vp]),
     "fd_concat_channels": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_ll, c_int, c_vp]),
     "fd_unary": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_vp]),
     "fd_add_strided": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_int, c_int, c_vp]),

@@ -182,11 +182,16 @@ class GnStats:
 
 def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=1, alpha=1.0, act="none",
          out_dtype=None, batch=1, M=None, N=None, K=None, lda=None, ldw=None, ldc=None, ldr=None,
-         stride_a=0, stride_w=0, stride_c=0, stride_r=0, ln_out=None, ln_in=None, ln_c=None, ln_eps=1e-5, gn=None):
+         stride_a=0, stride_w=0, stride_c=0, stride_r=0, ln_out=None, ln_in=None, ln_c=None, ln_eps=1e-5, gn=None,
+         batch_inner=1, stride_a_o=0, stride_w_o=0, stride_c_o=0, bsel=None, sm_len=None):
     """out[M, N (N/2 for geglu)] = epi(alpha * a[M, K] @ w[N, K]^T); strides default to the tensors'.
     ln_out: fp32 [M, N/160, 2] -- also write per-row (sum, sumsq) partials of the stored output (LayerNorm
     producer).  ln_in / ln_c: fold LayerNorm(a) into this GEMM (w = W * gamma, ln_c = rowsum(w), bias =
-    W . beta + b; see fold_layer_norm)."""
+    W . beta + b; see fold_layer_norm).
+    batch_inner > 1: two-level batch, operand offsets (z % batch_inner) * stride_x + (z // batch_inner) * stride_x_o.
+    bsel = (rows, mod, stride_w, stride_n): rows [g*rows, (g+1)*rows) multiply w + s * stride_w (ln_c / bias +
+    s * stride_n), s = g % mod (mod > 0) or g.  act="softmax" with sm_len: softmax over the first sm_len columns of
+    every 80-column group of the epilogue (the rest 0) -- fd_gemm_params.sm_* (include/faithdiff_hip.h)."""
     K = a.shape[-1] if K is None else K
     N = w.shape[-2] if N is None else N
     ldw = w.stride(-2) if ldw is None else ldw
@@ -222,11 +227,73 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
         p.ln_in, p.ln_c, p.ln_eps = ln_in.data_ptr(), ln_c.data_ptr(), ln_eps
     if gn is not None and batch == 1:
         gn.attach(p)
+    if batch_inner > 1:
+        p.batch_inner, p.strideA_o, p.strideB_o, p.strideC_o = batch_inner, stride_a_o, stride_w_o, stride_c_o
+    if bsel is not None:
+        p.bsel_rows, p.bsel_mod, p.bsel_strideB, p.bsel_strideN = bsel
+    if act == "softmax":
+        p.sm_group, p.sm_len = 80, int(sm_len)
     _attach_ws(p, a.device)
     _launch_gemm(p, "fd_gemm")
     if gn is not None:
         gn.collect(p)
     return out
+
+
+XSLOT = 80  # keys per head group of the two-GEMM cross-attention (two heads per 160-column score tile)
+
+
+class XAttnMats:
+    """The per-prompt matrices of one attn2 block for cross-attention as two GEMMs (R prompt rows, C channels, H
+    heads of 64): b1 [R, H*80, C] = 0.125 K_r,h W_q' (score matrix, rows h*80 + j), c / d [R, H*80] its LayerNorm-fold
+    constants, b2 [R, C, KP] with b2[r][n][h*80 + j] = W_o[n, h] . V_r[j, h] (KP = H*80 rounded up to 64).  Pad rows
+    and columns (keys j >= Lk, K past H*80) are zero: allocated zeroed, never written."""
+
+    def __init__(self, R, C, H, dtype, device):
+        self.R, self.C, self.H = R, C, H
+        self.HP = H * XSLOT
+        self.KP = (self.HP + 63) // 64 * 64
+        self.b1 = torch.zeros((R, self.HP, C), dtype=dtype, device=device)
+        self.c = torch.empty((R, self.HP), dtype=torch.float32, device=device)
+        self.d = torch.empty((R, self.HP), dtype=torch.float32, device=device)
+        self.b2 = torch.zeros((R, C, self.KP), dtype=dtype, device=device)
+
+
+def xattn_prepare(m, k, v, ldkv, Lk, wq_t, dq, wo, scale=0.125):
+    """Fill XAttnMats m from the prompt keys / values of one block: k, v views whose row r*Lk + j (stride ldkv) is
+    prompt r's key / value j (heads at columns h*64); wq_t = W_q'^T [C, C] (W_q' = W_q diag(gamma2) of the folded
+    norm2), dq = W_q . beta2 fp32 [C], wo = W_o [C, C].  Three launches, once per prompt."""
+    R, C, H, HP, KP, S = m.R, m.C, m.H, m.HP, m.KP, XSLOT
+    if Lk > S:
+        raise ValueError(f"xattn_prepare: {Lk} keys > {S} per head group")
+    # b1: out[j][k] = scale sum_d K_r[j][h*64 + d] W_q'^T[k][h*64 + d], batched over (r, h)
+    gemm(k, wq_t, out=m.b1, M=Lk, N=C, K=64, lda=ldkv, ldw=C, ldc=C, alpha=scale, batch=R * H, batch_inner=H,
+         stride_a=64, stride_a_o=Lk * ldkv, stride_w=64, stride_w_o=0, stride_c=S * C, stride_c_o=HP * C)
+    xattn_consts(m.b1, R * HP, C, k, ldkv, Lk * ldkv, dq, H, S, Lk, scale, m.c, m.d)
+    # b2: out[n][h*80 + j] = sum_d W_o[n][h*64 + d] V_r[j][h*64 + d], batched over (r, h)
+    gemm(wo, v, out=m.b2, M=C, N=Lk, K=64, lda=C, ldw=ldkv, ldc=KP, batch=R * H, batch_inner=H, stride_a=64,
+         stride_a_o=0, stride_w=64, stride_w_o=Lk * ldkv, stride_c=S, stride_c_o=C * KP)
+
+
+def xattn_attend(h, st, m, P, rows_per_img, mod, s0, Lk, bias_o, st_out=None):
+    """h += attn2(LN2(h)) in place, as two GEMMs: P = softmax_h(LN(h) . b1^T) (the score GEMM folds the LayerNorm
+    from the producer's partials st and applies the 80-column softmax in its epilogue), h = P . b2^T + b_o + h
+    (writing st_out, the next LayerNorm's partials).  Image g of h (rows_per_img rows each, a multiple of 256) uses
+    prompt row s0 + (g % mod if mod else g).  P: [M, KP] buffer whose columns past H*80 are zero."""
+    HP, KP, C = m.HP, m.KP, m.C
+    gemm(h, m.b1[s0:], out=P, N=HP, K=C, ldw=C, ldc=KP, ln_in=st, ln_c=m.c[s0:], bias=m.d[s0:], act="softmax",
+         sm_len=Lk, bsel=(rows_per_img, mod, HP * C, HP))
+    gemm(P, m.b2[s0:], N=C, K=KP, ldw=KP, bias=bias_o, residual=h, out=h, ln_out=st_out,
+         bsel=(rows_per_img, mod, C * KP, 0))
+    return h
+
+
+def xattn_consts(b1, rows, K, kv, ldkv, kv_rstride, dq, heads, slot, Lk, scale, c, d):
+    """LayerNorm-fold constants of the cross-attention score matrix rows (fd_xattn_consts): c = rowsum(b1 rows),
+    d = scale * K_j,h . dq_h (0 for pad keys)."""
+    L.check(L.load().fd_xattn_consts(L.ptr(b1), b1.stride(-2), rows, K, L.ptr(kv), ldkv, kv_rstride, L.ptr(dq), heads,
+                                     slot, Lk, scale, L.ptr(c), L.ptr(d), L.dtype_code(b1.dtype), L.stream()),
+            "fd_xattn_consts")
 
 
 def pack_e4m3(w):

@@ -89,6 +89,10 @@ class HipUNet:
             return r
 
         self.ln_fold = knobs.get("FD_LN_FOLD") != 0 and not self.fp8_mfma
+        # attn2 as two GEMMs against per-prompt products (scores with the softmax in the epilogue, then P . (V W_o)):
+        # the folded 16-bit model only (FD_XATTN_GEMM=0: Q projection + flash attention + out-projection)
+        self.xattn = self.ln_fold and knobs.get("FD_XATTN_GEMM") != 0
+        self._pbuf = {}
         # GroupNorm statistics from the producing conv / GEMM epilogue (256-row tiles; FD_UNET_GN_EPI=0: off)
         self.gn_epi = knobs.get("FD_UNET_GN_EPI") != 0
         self._gn_src = None
@@ -107,10 +111,14 @@ class HipUNet:
                 b = f"{p}.transformer_blocks.{i}"
                 ffw, ffb = ops.pack_geglu(sd[b + ".ff.net.0.proj.weight"], sd[b + ".ff.net.0.proj.bias"])
                 if self.ln_fold:
+                    q2_f = fold(sd[b + ".attn2.to_q.weight"], b + ".norm2")
                     blocks.append(dict(
                         qkv_f=fold(torch.cat([sd[f"{b}.attn1.to_{n}.weight"] for n in "qkv"], 0), b + ".norm1"),
                         o1=(W(b + ".attn1.to_out.0.weight"), Fp(b + ".attn1.to_out.0.bias")),
-                        q2_f=fold(sd[b + ".attn2.to_q.weight"], b + ".norm2"),
+                        q2_f=q2_f,
+                        # cross-attention as two GEMMs (set_context / _t2d_folded): W_q'^T for the per-prompt score
+                        # matrix, W_q . beta for its bias
+                        q2_t=q2_f[0].t().contiguous() if self.xattn else None, q2_d=q2_f[2],
                         kv2=_dev(torch.cat([sd[b + ".attn2.to_k.weight"], sd[b + ".attn2.to_v.weight"]], 0),
                                  self.device, dtype),
                         o2=(W(b + ".attn2.to_out.0.weight"), Fp(b + ".attn2.to_out.0.bias")),
@@ -236,9 +244,28 @@ class HipUNet:
             self.ctx = c.contiguous().clone()
             self._kv = torch.empty((c.shape[0], self.kv_total), dtype=self.dtype, device=self.device)
             self.graphs.clear()
+        new_shape = self.ncfg != ncfg or getattr(self, "Lk", None) != ctx.shape[1]
         self.ncfg, self.Lk = ncfg, ctx.shape[1]
         self.npairs = ctx.shape[0] // ncfg
         ops.gemm(self.ctx, self.kv_w, out=self._kv)  # [rows*77, sum 2C]: every attn2 K/V
+        if self.xattn and self.Lk <= self.XSLOT:
+            self._xattn_prep(ctx.shape[0], new_shape)
+
+    XSLOT = ops.XSLOT
+
+    def _xattn_prep(self, R, realloc):
+        """Cross-attention as two GEMMs (ops.XAttnMats / xattn_prepare): per prompt row and attn2 block, the score
+        matrix 0.125 K W_q' with its LayerNorm-fold constants and V W_o -- the prompt-only products of the reference's
+        attn2 (diffusers Attention: to_q, SDPA, to_out, recomputed every UNet call at pipeline:1350) taken out of the
+        denoise loop; each forward then runs two launches per block instead of three."""
+        Lk, kv, ldkv = self.Lk, self._kv, self.kv_total
+        for t in self._all_t2d():
+            for b in t["blocks"]:
+                if realloc or b.get("xm") is None or b["xm"].R != R:
+                    b["xm"] = ops.XAttnMats(R, t["c"], t["heads"], self.dtype, self.device)
+                off = b["kv_off"]
+                ops.xattn_prepare(b["xm"], kv[:, off:], kv[:, off + t["c"]:], ldkv, Lk, b["q2_t"], b["q2_d"],
+                                  b["o2"][0])
 
     # ------------------------------------------------------------------------------------------ blocks
     def _resnet(self, r, x, B, H, Wd, temb, x2=None, C1=None):
@@ -376,6 +403,8 @@ class HipUNet:
         M = B * HW
         st = torch.empty((M, C // 160, 2), dtype=torch.float32, device=self.device)
         h = ops.gemm(hn, t["pin"][0], bias=t["pin"][1], ln_out=st)
+        # the two-GEMM cross-attention needs its matrices (Lk <= 80) and whole 256-row groups per image
+        xa = self.xattn and self.Lk <= self.XSLOT and HW % 256 == 0 and t["blocks"][0].get("xm") is not None
         qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
         att = torch.empty((M, C), dtype=self.dtype, device=self.device)
         nb = len(t["blocks"])
@@ -385,17 +414,32 @@ class HipUNet:
             ops.flash_attn(qkv, qkv[:, C:], qkv[:, 2 * C:], att, B, heads, HW, HW, 3 * C, 3 * C, 3 * C, C,
                            HW * 3 * C, HW * 3 * C, HW * 3 * C, HW * C, kv_mod=0, scale=0.125)
             ops.gemm(att, b["o1"][0], bias=b["o1"][1], residual=h, out=h, ln_out=st)
-            w, c, d = b["q2_f"]
-            ops.gemm(h, w, bias=d, out=qkv[:, :C], ldc=3 * C, ln_in=st, ln_c=c)
-            kv = self._kv[self._kv_row0:, b["kv_off"]:]
-            Lk, ldkv = self.Lk, self.kv_total
-            ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, ldkv, ldkv, C,
-                           HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self._kv_mod, scale=0.125)
-            ops.gemm(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h, ln_out=st)
+            if xa:  # scores with the softmax in the epilogue, then P . V W_o + b_o + h (ops.xattn_attend)
+                xm = b["xm"]
+                ops.xattn_attend(h, st, xm, self._pbuf_get(M, xm.KP), HW, self._kv_mod, self._kv_row0 // self.Lk,
+                                 self.Lk, b["o2"][1], st_out=st)
+            else:
+                w, c, d = b["q2_f"]
+                ops.gemm(h, w, bias=d, out=qkv[:, :C], ldc=3 * C, ln_in=st, ln_c=c)
+                kv = self._kv[self._kv_row0:, b["kv_off"]:]
+                Lk, ldkv = self.Lk, self.kv_total
+                ops.flash_attn(qkv, kv, kv[:, C:], att, B, heads, HW, Lk, 3 * C, ldkv, ldkv, C,
+                               HW * 3 * C, Lk * ldkv, Lk * ldkv, HW * C, kv_mod=self._kv_mod, scale=0.125)
+                ops.gemm(att, b["o2"][0], bias=b["o2"][1], residual=h, out=h, ln_out=st)
             w, c, d = b["ff1_f"]
             ff = ops.gemm(h, w, bias=d, act="geglu", ln_in=st, ln_c=c)
             ops.gemm(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h, ln_out=st if i + 1 < nb else None)
         return self._proj_out(t, h, x, B, HW)
+
+    def _pbuf_get(self, M, KP):
+        """The probability buffer of the two-GEMM cross-attention [M, KP]: persistent per shape (hipGraph replays
+        reuse it) and zeroed once -- the score GEMM writes H*80 columns, the pad up to KP stays 0."""
+        key = (M, KP)
+        if key not in self._pbuf:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("two-GEMM cross-attention buffer first needed inside graph capture")
+            self._pbuf[key] = torch.zeros((M, KP), dtype=self.dtype, device=self.device)
+        return self._pbuf[key]
 
     def _cond_embed(self, cond, B, H, Wd, out=None):
         """condition_embedding (ext:528-534, the CNE: GroupNorm -> conv 512->512 + SiLU -> conv 512->320) of the

@@ -31,7 +31,8 @@ typedef enum {
 } fd_status;
 
 enum { FD_BF16 = 0, FD_F16 = 1, FD_F32 = 2 };
-enum { FD_ACT_NONE = 0, FD_ACT_SILU = 1, FD_ACT_GELU = 2, FD_ACT_QUICKGELU = 3, FD_ACT_GEGLU = 4, FD_ACT_LRELU = 5 };
+enum { FD_ACT_NONE = 0, FD_ACT_SILU = 1, FD_ACT_GELU = 2, FD_ACT_QUICKGELU = 3, FD_ACT_GEGLU = 4, FD_ACT_LRELU = 5,
+       FD_ACT_SOFTMAX = 6 };
 
 /* ---------------------------------------------------------------------------------------------
  * GEMM / implicit-GEMM convolution on MFMA (v_mfma_f32_16x16x32_{bf16,f16}), operands staged through
@@ -111,6 +112,21 @@ typedef struct fd_gemm_params {
    * in front of every ResnetBlock2D conv (diffusers; UNet and VAE). */
   const void* gi_affine;
   int gi_silu;
+  /* Two-level batch (the 4-wave kernel, batch > 1): z -> (zo, zi) = (z / batch_inner, z % batch_inner); the
+   * operands sit at zi * strideX + zo * strideX_o.  batch_inner <= 1: one level (z * strideX). */
+  int batch_inner;
+  long long strideA_o, strideB_o, strideC_o;
+  /* Per-row-group B operand (cross-attention as two GEMMs: each image row of a batched forward multiplies its own
+   * prompt's matrices).  bsel_rows > 0: rows [g * bsel_rows, (g + 1) * bsel_rows) use slot
+   * s = bsel_mod > 0 ? g % bsel_mod : g, i.e. B + s * bsel_strideB and ln_c / bias + s * bsel_strideN
+   * (bsel_strideN 0: shared).  bsel_rows % 256 == 0 (no tile straddles two groups), batch 1. */
+  int bsel_rows, bsel_mod;
+  long long bsel_strideB, bsel_strideN;
+  /* act == FD_ACT_SOFTMAX (attention probabilities straight from the score GEMM): the N columns are groups of
+   * sm_group = 80 (one head's keys, two heads per 160-column tile); in each group the first sm_len (<= 80) columns
+   * become softmax over those values of the epilogue before the activation (LayerNorm fold, bias, alpha), the rest
+   * are written as 0.  N % 160 == 0, no residual / row bias / GEGLU, 16-bit output. */
+  int sm_group, sm_len;
 } fd_gemm_params;
 
 int fd_gemm(fd_gemm_params* p, void* stream);  /* writes only p->gn_done */
@@ -258,6 +274,17 @@ int fd_flash_attn_d512(const void* q, const void* k, const void* v, long long ld
 /* Row softmax of fp32 scores s[R][C] (scaled by `scale`) into p[R][ldp] (dtype).  With fd_gemm this forms
  * a materialised single-head attention (kept for head dims other than 512; the VAE uses fd_flash_attn_d512). */
 int fd_softmax_rows(const float* s, void* p, int R, int C, long long ldp, float scale, int dtype, void* stream);
+
+/* Cross-attention as two GEMMs (attn2 of every BasicTransformerBlock, diffusers Attention called from
+ * unet_2d_condition_vae_extension.py:571-690 through pipeline_FaithDiff_tlc.py:1350-1360; the prompt K / V are
+ * fixed for the whole denoise loop).  Per prompt row r the score matrix B1[r] = scale * K_r,h . W_q' (row
+ * (r * heads + h) * slot + j per head h and key j, written by a batched fd_gemm) gets its LayerNorm-fold
+ * constants here: c[n] = sum_k B1[n][k] (stored values, fixed order), d[n] = scale * K_r[j][h*64..] . dq[h*64..]
+ * (dq = W_q . beta fp32; 0 for pad keys j >= Lk).  kv: K rows of prompt r at kv + r * kv_rstride + j * ldkv
+ * (head h at column h * 64).  rows = R * heads * slot.  dtype: of B1 and kv. */
+int fd_xattn_consts(const void* B1, long long ldb, int rows, int K, const void* kv, long long ldkv,
+                    long long kv_rstride, const float* dq, int heads, int slot, int Lk, float scale, float* c,
+                    float* d, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Elementwise / layout helpers (all HBM-bound).

@@ -20,6 +20,13 @@ SHAPES = [("unet128_320", 2, 128, 128, 320, 320, torch.bfloat16, False),
           ("unet64_640", 2, 64, 64, 640, 640, torch.bfloat16, False),
           ("unet64_1280to640", 2, 64, 64, 1280, 640, torch.bfloat16, False),
           ("unet32_1280", 2, 32, 32, 1280, 1280, torch.bfloat16, False),
+          ("unet32_2560to1280", 2, 32, 32, 2560, 1280, torch.bfloat16, False),
+          ("unet32_1920to1280", 2, 32, 32, 1920, 1280, torch.bfloat16, False),
+          ("unet32_640to1280", 2, 32, 32, 640, 1280, torch.bfloat16, False),
+          ("unet64_1920to640", 2, 64, 64, 1920, 640, torch.bfloat16, False),
+          ("unet64_960to640", 2, 64, 64, 960, 640, torch.bfloat16, False),
+          ("unet64_320to640", 2, 64, 64, 320, 640, torch.bfloat16, False),
+          ("unet128_960to320", 2, 128, 128, 960, 320, torch.bfloat16, False),
           ("unet_up64_1280", 2, 32, 32, 1280, 1280, torch.bfloat16, True),
           ("unet_up128_640", 2, 64, 64, 640, 640, torch.bfloat16, True),
           ("vae128_512", 1, 128, 128, 512, 512, torch.float16, False),

@@ -1,0 +1,110 @@
+"""Cross-attention as two GEMMs (ops.XAttnMats / xattn_prepare / xattn_attend; fdhip/unet.py _t2d_folded) against
+the reference's attn2 computed in fp32: x + to_out(SDPA(to_q(LayerNorm(x)), K, V)) with per-image prompt rows
+(diffusers BasicTransformerBlock attn2, unet_2d_condition_vae_extension.py:571-690 via pipeline_FaithDiff_tlc.py:1350).
+
+The score GEMM folds the LayerNorm from the producer's partials and applies the per-head softmax over the Lk keys of
+each 80-column group in its epilogue; the second GEMM multiplies the probabilities by the per-prompt V W_o.  Both
+round their operands to bf16 (the reference rounds Q and the attention output instead), so the bar is the bf16
+storage tolerance on the attention delta (rel-L2 <= 1.5e-2) and on the output."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+from parity import rel_l2  # noqa: E402  (records every measured value)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _dev():
+    from fdhip import lib
+    lib.require_device()
+
+
+def _case(B, HW, C, Lk, mod, R, s0, seed=0):
+    from fdhip import ops
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    H = C // 64
+    bf = torch.bfloat16
+    M = B * HW
+    wq = (torch.randn(C, C, device=DEV, generator=g) / math.sqrt(C)).to(bf)
+    wo = (torch.randn(C, C, device=DEV, generator=g) / math.sqrt(C)).to(bf)
+    bo = torch.randn(C, device=DEV, generator=g) * 0.1
+    gamma = 1 + 0.2 * torch.randn(C, device=DEV, generator=g)
+    beta = 0.2 * torch.randn(C, device=DEV, generator=g)
+    kv = (torch.randn(R * Lk, 2 * C, device=DEV, generator=g) * 1.5).to(bf)  # [K | V] per prompt row
+    # the residual stream h and its LayerNorm partials come from a producer GEMM (as proj_in / ff out write them)
+    a0 = torch.randn(M, C, device=DEV, generator=g).to(bf)
+    w0 = (torch.randn(C, C, device=DEV, generator=g) / math.sqrt(C)).to(bf)
+    st = torch.empty((M, C // 160, 2), dtype=torch.float32, device=DEV)
+    h = ops.gemm(a0, w0, bias=torch.randn(C, device=DEV, generator=g) * 0.5, ln_out=st)
+    wq_f, _, dq = ops.fold_layer_norm(wq.float(), gamma, beta, None, bf)
+    m = ops.XAttnMats(R, C, H, bf, DEV)
+    ops.xattn_prepare(m, kv[:, :C], kv[:, C:], 2 * C, Lk, wq_f.t().contiguous(), dq, wo)
+    P = torch.zeros((M, m.KP), dtype=bf, device=DEV)
+    out = h.clone()
+    st_out = torch.empty_like(st)
+    ops.xattn_attend(out, st, m, P, HW, mod, s0, Lk, bo, st_out=st_out)
+    torch.cuda.synchronize()
+    # fp32 reference on the same bf16 inputs / weights
+    x = h.float()
+    ln = F.layer_norm(x, (C,), gamma, beta, 1e-5)
+    q = ln @ wq.float().t()
+    ref = torch.empty_like(x)
+    for i in range(B):
+        r = s0 + (i % mod if mod else i)
+        k = kv[r * Lk:(r + 1) * Lk, :C].float().view(Lk, H, 64).permute(1, 0, 2)
+        v = kv[r * Lk:(r + 1) * Lk, C:].float().view(Lk, H, 64).permute(1, 0, 2)
+        qi = q[i * HW:(i + 1) * HW].view(HW, H, 64).permute(1, 0, 2)
+        o = F.scaled_dot_product_attention(qi, k, v).permute(1, 0, 2).reshape(HW, C)
+        ref[i * HW:(i + 1) * HW] = x[i * HW:(i + 1) * HW] + o @ wo.float().t() + bo
+    return out, ref, x, m, P, st_out, (h, st, bo)
+
+
+@pytest.mark.parametrize("B,HW,C,Lk,mod,R,s0", [
+    (2, 1024, 1280, 77, 2, 2, 0),   # the 32^2 level of a C2 tile: one prompt pair, CFG rows alternate
+    (2, 4096, 640, 77, 2, 2, 0),    # the 64^2 level (K = 832: 32 zero columns past the 10 heads)
+    (6, 256, 640, 50, 2, 2, 0),     # three tiles batched, a shorter prompt (30 masked keys per head group)
+    (4, 512, 1280, 77, 0, 8, 2)])   # images batched (C5): image g uses prompt row 2 + g
+def test_xattn_two_gemm_matches_attention(B, HW, C, Lk, mod, R, s0):
+    out, ref, x, m, P, st_out, _ = _case(B, HW, C, Lk, mod, R, s0)
+    assert torch.isfinite(out.float()).all()
+    d_rel = rel_l2(out.float() - x, ref - x)
+    assert d_rel < 1.5e-2, d_rel
+    assert rel_l2(out, ref) < 6e-3
+    # probabilities: every head group sums to 1 over its Lk keys, the pad keys and the K padding are exactly 0
+    pg = P[:, :m.HP].float().view(-1, m.H, 80)
+    assert torch.allclose(pg[..., :Lk].sum(-1), torch.ones_like(pg[..., 0]), atol=2e-2)
+    assert (pg[..., Lk:] == 0).all()
+    assert (P[:, m.HP:] == 0).all()
+    # the LayerNorm partials written for the next consumer: (sum, sumsq) of the stored output per 160 columns
+    o = out.float().view(-1, C // 160, 160)
+    assert torch.allclose(st_out[..., 0], o.sum(-1), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(st_out[..., 1], (o * o).sum(-1), rtol=1e-4, atol=1e-2)
+
+
+def test_xattn_consts_are_the_fold_constants():
+    """c = row sums of the stored score matrix, d = 0.125 K . (W_q beta) per (head, key), 0 for pad keys."""
+    from fdhip import ops
+    _, _, _, m, _, _, _ = _case(2, 256, 640, 77, 2, 2, 0, seed=3)
+    c = m.b1.float().sum(-1)
+    assert torch.allclose(m.c, c, rtol=1e-5, atol=1e-4)
+    assert (m.d.view(2, m.H, 80)[..., 77:] == 0).all()
+    assert (m.b1.view(2, m.H, 80, -1)[:, :, 77:] == 0).all()
+
+
+def test_xattn_batched_rows_bitwise_single():
+    """Images batched along M (C5: image g uses prompt row g) give each image the bits of its own launch: the prompt
+    slot is chosen per 256-row group, and every tile shape of the score GEMM sums K in the same order."""
+    from fdhip import ops
+    B, HW, C, Lk, R = 4, 256, 640, 77, 4
+    out, _, _, m, _, _, (h, st, bo) = _case(B, HW, C, Lk, 0, R, 0, seed=5)
+    for i in range(B):
+        rows = slice(i * HW, (i + 1) * HW)
+        out1 = h[rows].clone()
+        P1 = torch.zeros((HW, m.KP), dtype=torch.bfloat16, device=DEV)
+        ops.xattn_attend(out1, st[rows].clone(), m, P1, HW, 0, i, Lk, bo)
+        torch.cuda.synchronize()
+        assert torch.equal(out1, out[rows]), i
