@@ -1061,8 +1061,9 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     }
     q.bm = best;
     q.bn = 160;
-    q.nw = best == 256 ? 8 : 4;
-    q.waves_m = best == 256 ? 8 : 2;
+    const int w8 = fd_knob(FDK_GEMM8_W128);
+    q.nw = (best == 256 || (best == 128 && w8)) ? 8 : 4;
+    q.waves_m = best == 256 ? 8 : (best == 128 && w8) ? 4 : 2;
     q.ns = 3;
     q.S = 1;
     goto planned;
@@ -1087,8 +1088,9 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     }
     q.bm = 128;
     q.bn = 160;
-    q.nw = 4;
-    q.waves_m = 2;
+    // eight waves of 32 x 80 (two per SIMD: one wave's fragment reads under the other's MFMAs) or four of 64 x 80
+    q.nw = fd_knob(FDK_GEMM8_W128) ? 8 : 4;
+    q.waves_m = q.nw == 8 ? 4 : 2;
     q.ns = 3;
     q.S = 2;
     goto planned;
@@ -1223,6 +1225,8 @@ extern "C" int fd_gemm8_try(fd_gemm_params* p0, void* stream) {
     FD_G8(256, 160, 8, 8, 3);
   } else if (pl.bm == 256) {
     FD_G8(256, 128, 8, 4, 3);
+  } else if (pl.bm == 128 && pl.nw == 8) {
+    FD_G8(128, 160, 8, 4, 3);
   } else if (pl.bm == 128) {
     FD_G8(128, 160, 4, 2, 3);
   } else if (pl.ns >= 5) {
