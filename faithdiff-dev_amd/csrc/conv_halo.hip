@@ -20,6 +20,8 @@
 // rounding), and the sum over K runs chunk by chunk, tap by tap inside the chunk -- per output element the same
 // order whatever the tile shape (TH 16 or 8, BN 160 or 128), so tile choices never change a bit; it differs from
 // the implicit GEMM's tap-major order (not bitwise equal to gemm8, tested against fp32).
+#include <type_traits>
+
 #include "fd_common.h"
 
 __device__ __attribute__((aligned(256))) unsigned char g_zero_halo[256];
@@ -32,7 +34,8 @@ __device__ __forceinline__ void hvm() {
 }
 
 constexpr int PW = 18;  // patch width: 16 output columns + halo
-constexpr int TR = 7;   // tap of chunk c at which chunk c + 1's patch is waited for and transformed
+constexpr int TR = 4;   // tap of chunk c at which chunk c + 1's patch is waited for
+constexpr int NPART = 8 - TR;  // ... and transformed in NPART pieces at taps TR .. 7 (published by tap 8's barrier)
 
 template <typename T, int TH, int BN, bool GNI, bool SK, int NS>
 __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, float* __restrict__ slabs,
@@ -135,8 +138,11 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
                                        0);
   };
   // GroupNorm affine (+ SiLU) in place on patch buffer c & 1: y = silu(fma(x, a, b)) rounded to T (fd_group_norm's
-  // bits), zero outside the image.  Each thread keeps one logical 8-channel slot (tid % 8) for every pixel.
-  auto transform = [&](int c) {
+  // bits), zero outside the image.  Each thread keeps one logical 8-channel slot (tid % 8) for every pixel.  Piece
+  // `part` of `nparts` covers pixels [part * PIX / nparts, (part + 1) * PIX / nparts): the main loop transforms the
+  // next chunk's patch a piece per tap, issued behind that tap's MFMAs so the VALU work runs under them.
+  auto transform = [&](int c, int part, auto npc) {
+    constexpr int NP = decltype(npc)::value;
     unsigned char* buf = smem + (c & 1) * PBUF;
     const int lc = tid & 7;
     const float* ab = (const float*)(buf + PATCH) + lc * 16;
@@ -147,17 +153,20 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       b[i] = ab[2 * i + 1];
     }
     const bool silu = p.gi_silu != 0;
-    constexpr int IT = (PIX * 8 + 511) / 512;
+    const int e0 = ((part * PIX) / NP) * 8, e1 = (((part + 1) * PIX) / NP) * 8;
+    constexpr int IT = (((PIX + NP - 1) / NP + 1) * 8 + 511) / 512;
     V8 xs[IT];  // every read issued before the first write (one LDS round trip, not IT)
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-      const int pix = (tid + it * 512) >> 3;
-      if (pix < PIX) xs[it] = *(const V8*)(buf + pix * 128 + ((lc ^ ((pix >> 1) & 7)) << 4));
+      const int e = e0 + tid + it * 512;
+      const int pix = e >> 3;
+      if (e < e1) xs[it] = *(const V8*)(buf + pix * 128 + ((lc ^ ((pix >> 1) & 7)) << 4));
     }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-      const int pix = (tid + it * 512) >> 3;
-      if (pix < PIX) {
+      const int e = e0 + tid + it * 512;
+      const int pix = e >> 3;
+      if (e < e1) {
         const int py = pix / PW, px = pix - (pix / PW) * PW;
         const int iy = y0 - 1 + py, ix = x0 - 1 + px;
         const bool ok = iy >= 0 && iy < Ho && ix >= 0 && ix < Wo;
@@ -221,7 +230,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   }
   __builtin_amdgcn_s_barrier();
   if (GNI) {
-    transform(cb);
+    transform(cb, 0, std::integral_constant<int, 1>());
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_s_barrier();
   }
@@ -242,7 +251,9 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     } else if (t == 8 && c + 2 < ce) {
       stage_p(c + 2);  // buffer c & 1: its last reads (this step's half 1) are behind the barrier
     }
-    if (GNI && t == TR && c + 1 < ce) transform(c + 1);  // visible to the readers after step (c, 8)'s barrier
+    // chunk c + 1's patch: a piece per tap TR .. 7 behind this step's half-1 MFMAs (below); visible to the readers
+    // after step (c, 8)'s barrier
+    const int tc = (GNI && t >= TR && t < 8 && c + 1 < ce) ? c + 1 : -1, tp = t - TR;
     rb = rb == NS - 1 ? 0 : rb + 1;
     if (t == 8) {
       ++c;
@@ -252,6 +263,10 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     }
     read_frags(c, t, rb, 0, a0, b0);
     mma(a1, b1);
+    if (GNI && tc >= 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      transform(tc, tp, std::integral_constant<int, NPART>());
+    }
   }
   read_frags(c, t, rb, 1, a1, b1);
   mma(a0, b0);

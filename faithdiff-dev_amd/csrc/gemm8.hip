@@ -1291,6 +1291,10 @@ int plan_e4m3(const fd_gemm_params* p, bool mx_out, Plan8* pl) {
   pl->bn = cands[best].bn;
   pl->nw = cands[best].nw;
   pl->waves_m = cands[best].wm;
+  if (pl->bm == 128 && fd_knob(FDK_GEMM8_W128)) {  // eight waves of 32 x 80 (as the 16-bit 128 x 160 tiles)
+    pl->nw = 8;
+    pl->waves_m = 4;
+  }
   pl->ns = 3;
   pl->S = 1;
   const int tiles_m = (p->M + pl->bm - 1) / pl->bm, tiles_n = (p->N + pl->bn - 1) / pl->bn;
@@ -1314,6 +1318,7 @@ int launch_e4m3(const fd_gemm_params* p, const Plan8& pl, const f8_args& f8, int
 #define FD_G8F(TO_)                                                                            \
   if (pl.bm == 256 && pl.bn == 160) rc = launch8_e4m3<T, TO_, 256, 160, 8, 8>(p, pl, f8, s);   \
   else if (pl.bm == 256) rc = launch8_e4m3<T, TO_, 256, 128, 8, 4>(p, pl, f8, s);              \
+  else if (pl.bm == 128 && pl.nw == 8) rc = launch8_e4m3<T, TO_, 128, 160, 8, 4>(p, pl, f8, s); \
   else if (pl.bm == 128) rc = launch8_e4m3<T, TO_, 128, 160, 4, 2>(p, pl, f8, s);              \
   else rc = launch8_e4m3<T, TO_, 64, 160, 4, 2>(p, pl, f8, s);
   if (out_dtype == FD_BF16) {

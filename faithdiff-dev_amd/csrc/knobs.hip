@@ -46,7 +46,7 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_CONV_HALO", 1},           // 3x3 stride-1 convs on the halo-staged kernel where eligible (1: not the gemm256 ones; 2: all)
     {"FD_CONV_HALO_MIN_TILES", 192},  // ... when it has at least this many tiles (per TLC tile's rows, m_ref)
     {"FD_CONV_HALO_SPLIT", 1},     // ... or twice that many with the input channels split in two (pairwise combine)
-    {"FD_CONV_HALO_NS8", 5},       // weight-ring depth of its 128-row tiles (3 or 5)
+    {"FD_CONV_HALO_NS8", 3},       // weight-ring depth of its 128-row tiles (3 or 5: no faster, profiles/r04d_*)
     {"FD_GEMM_GMP", 1},            // 4-wave kernel: tile-row group height planned per launch (0: fixed 4)
     {"FD_GEMM8_W128", 1},          // gemm8 128 x 160 tiles on eight waves of 32 x 80 (0: four of 64 x 80)
 };

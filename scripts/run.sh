@@ -41,9 +41,10 @@ for ph in "$@"; do
     probe)
       sc=${arg%%,*}; out=gpurun_out/${TAG}_$(basename $sc .py)
       timeout -k 10 400 python -u ${arg//,/ } > $out.log 2>&1; rc=$?; tail -25 $out.log ;;
-    ab|abv)  # abv: with the VAE decode leg (prints vae_decode_ms too)
+    ab|abv|abf)  # abv: with the VAE decode leg (prints vae_decode_ms too); abf: the use_fp8 model (--fp8)
       IFS=';' read -r reps rest <<< "$arg"; IFS=';' read -ra arms <<< "$rest"; : > $out.txt
       if [ $name = abv ]; then VA=""; else VA="--no-vae"; fi
+      if [ $name = abf ]; then VA="$VA --fp8"; fi
       for r in $(seq $reps); do for e in "${arms[@]}"; do
         env $e timeout -k 10 300 python bench.py --no-cpu-baseline $VA --no-c3 --no-pipeline --steps 30 > $out.run 2>&1 || { rc=$?; break 2; }
         echo "$e $(tail -1 $out.run | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d.get("roofline", {}).get("frac"), d.get("vae_decode_ms"))')" | tee -a $out.txt
