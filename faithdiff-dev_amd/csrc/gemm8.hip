@@ -1075,7 +1075,10 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     // profiles/r02e_m2048_split.jsonl); anything else stays on that producer (return 0).
     const int lnp = fd_knob(FDK_GEMM8_LNP);
     const int lnp_s = fd_knob(FDK_GEMM8_LNP_S);  // splits of the 256 x 160 form (lnp = 2)
-    if (!lnp || p->act == FD_ACT_GEGLU || p->conv || p->N % 160 || p->K < 4096 || m_ref < 128) return 0;
+    // FD_GEMM8_LNP_K: the least K routed here (4096: the ff outs; 1024 also takes the K = 1280 / 1600 producers of
+    // the 32^2 level -- attention out-projections, proj_in -- on the eight-wave 128 x 160 pairwise split)
+    if (!lnp || p->act == FD_ACT_GEGLU || p->conv || p->N % 160 || p->K < fd_knob(FDK_GEMM8_LNP_K) || m_ref < 128)
+      return 0;
     if ((long long)((m_ref + 63) / 64) * (p->N / 160) > 256) return 0;
     if (lnp == 2 && m_ref >= 256) {  // 256 x 160 tiles (0.76x the operand bytes per CU of 128 x 160), S-way K split
       q.bm = 256;

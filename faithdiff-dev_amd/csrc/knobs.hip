@@ -49,6 +49,7 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_CONV_HALO_NS8", 3},       // weight-ring depth of its 128-row tiles (3 or 5: no faster, profiles/r04d_*)
     {"FD_GEMM_GMP", 1},            // 4-wave kernel: tile-row group height planned per launch (0: fixed 4)
     {"FD_GEMM8_W128", 1},          // gemm8 128 x 160 tiles on eight waves of 32 x 80 (0: four of 64 x 80)
+    {"FD_GEMM8_LNP_K", 4096},      // least K of the LN-fold producers taken by the 128 x 160 pairwise split
 };
 int g_knobs[FDK_COUNT];
 bool g_init = false;
