@@ -420,6 +420,48 @@ __global__ void __launch_bounds__(256) gn_affine_kernel(const float2* __restrict
   aff[e] = make_float2(a, __builtin_fmaf(-st.x, a, beta ? beta[c] : 0.f));
 }
 
+// gn_finalize_kernel + gn_affine_kernel in one launch (the per-resnet GroupNorm of the halo conv: two ~5 us
+// latency-bound launches -> one): one wave per (group, image) folds the partials exactly as gn_finalize_kernel, then
+// writes the group's channels' (a, b) exactly as gn_affine_kernel; block (0, 0) also zeroes the 64-channel pad.
+__global__ void __launch_bounds__(64) gn_finalize_affine_kernel(const float2* __restrict__ part,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float2* __restrict__ aff,
+                                                                int HW, int C, int groups, int nchunks, float eps) {
+  const int g = blockIdx.x, img = blockIdx.y, j = threadIdx.x, nimg = gridDim.y;
+  const int cpg = C / groups;
+  const float2* p = part + (long long)img * nchunks * groups + g;
+  constexpr int U = 16;
+  double s = 0.0, q = 0.0;
+  for (int c0 = j; c0 < nchunks; c0 += 64 * U) {
+    float2 w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + 64 * u;
+      w[u] = c < nchunks ? p[(long long)c * groups] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s += w[u].x;
+      q += w[u].y;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    q += __shfl_xor(q, o, 64);
+  }
+  const double n = (double)HW * cpg;
+  const double mean = s / n;
+  double var = q / n - mean * mean;
+  if (var < 0) var = 0;
+  const float2 st = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+  for (int k = j; k < cpg; k += 64) {
+    const int c = g * cpg + k;
+    const float a = st.y * (gamma ? gamma[c] : 1.f);
+    aff[(long long)img * C + c] = make_float2(a, __builtin_fmaf(-st.x, a, beta ? beta[c] : 0.f));
+  }
+  if (g == 0 && img == 0) aff[(long long)nimg * C + j] = make_float2(0.f, 0.f);
+}
+
 extern "C" int fd_group_norm_affine(const void* x, const void* part, int part_rows, const float* gamma,
                                     const float* beta, int nimg, int HW, int C, int groups, float eps, void* ws,
                                     void* affine, int dtype, void* stream) {
@@ -431,7 +473,14 @@ extern "C" int fd_group_norm_affine(const void* x, const void* part, int part_ro
   if (part) {
     if ((part_rows != 128 && part_rows != 256) || HW % part_rows) return FD_ERR_ARG;
     stats = (float2*)ws;
-    gn_finalize_launch((const float2*)part, stats, nimg, HW, C, groups, HW / part_rows, eps, s);
+    const int nch = HW / part_rows;
+    if (nch <= 1024) {  // one launch (the wide fold's long lists keep the two-launch form)
+      hipLaunchKernelGGL(gn_finalize_affine_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)part, gamma,
+                         beta, (float2*)affine, HW, C, groups, nch, eps);
+      FD_LAUNCH_CHECK();
+      return FD_OK;
+    }
+    gn_finalize_launch((const float2*)part, stats, nimg, HW, C, groups, nch, eps, s);
   } else {
     if ((groups & (groups - 1))) return FD_ERR_SHAPE;
     const int rpc = gn_rows_per_chunk(nimg, HW);
