@@ -50,6 +50,7 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_GEMM_GMP", 1},            // 4-wave kernel: tile-row group height planned per launch (0: fixed 4)
     {"FD_GEMM8_W128", 1},          // gemm8 128 x 160 tiles on eight waves of 32 x 80 (0: four of 64 x 80)
     {"FD_GEMM8_LNP_K", 4096},      // least K of the LN-fold producers taken by the 128 x 160 pairwise split
+    {"FD_XATTN_SPLIT", 0},         // cross-attention score GEMM: 128 x 160 tiles with K split in two
 };
 int g_knobs[FDK_COUNT];
 bool g_init = false;
