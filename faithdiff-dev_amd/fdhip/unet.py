@@ -96,6 +96,7 @@ class HipUNet:
         # weights of the next transformer block read into the Infinity Cache on a side stream while this block runs
         # (the forward's 5 GB of weights do not fit the 256 MB cache: every GEMM would start on HBM misses)
         self.prefetch = knobs.get("FD_PREFETCH") != 0
+        self.prefetch_convs = knobs.get("FD_PREFETCH") >= 2  # also the next resnet's conv weights
         self._pf_stream = None
         # GroupNorm statistics from the producing conv / GEMM epilogue (256-row tiles; FD_UNET_GN_EPI=0: off)
         self.gn_epi = knobs.get("FD_UNET_GN_EPI") != 0
@@ -179,6 +180,11 @@ class HipUNet:
                 blk["us"] = (_dev(ops.pack_conv3x3(sd[p + ".weight"]), self.device, dtype), Fp(p + ".bias"))
             self.up.append(blk)
             prev = co
+        # forward order of the resnets: each prefetches the next one's conv weights (FD_PREFETCH=2)
+        order = [r for blk in self.down for r in blk["resnets"]] + [self.mid["r0"], self.mid["r1"]] + \
+                [r for blk in self.up for r in blk["resnets"]]
+        for a, b in zip(order, order[1:]):
+            a["next"] = b
         self.norm_out = (Fp("conv_norm_out.weight"), Fp("conv_norm_out.bias"))
         self.conv_out = (_dev(ops.pack_conv3x3(sd["conv_out.weight"]), self.device, dtype), Fp("conv_out.bias"))
         self.temb_w = _dev(torch.cat(temb_w, 0), self.device, dtype)
@@ -275,6 +281,9 @@ class HipUNet:
     def _resnet(self, r, x, B, H, Wd, temb, x2=None, C1=None):
         """x: [M, cin] (or concat(x [M,C1], x2) when x2 is given)."""
         HW = H * Wd
+        if self.prefetch_convs and "next" in r:
+            nx = r["next"]
+            self._prefetch([nx["c1"][0], nx["c2"][0]] + ([nx["sc"][0]] if "sc" in nx else []))
         if x2 is not None:
             cat = torch.empty((B * HW, r["cin"]), dtype=self.dtype, device=self.device)
             ops.concat_channels(x, C1, x2, r["cin"] - C1, cat, B * HW)
