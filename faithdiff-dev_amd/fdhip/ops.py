@@ -7,6 +7,7 @@ import ctypes
 
 import torch
 
+from . import knobs
 from . import lib as L
 
 _GN_WS = {}
@@ -530,8 +531,11 @@ def gn_conv3x3(x, gamma, beta, wp, bias, nimg, H, W, eps, silu=True, groups=32, 
     normalised tensor is written or read); else a GroupNorm pass, then the conv.  stats: GnStats of x from its
     producer's epilogue (skips the statistics pass either way)."""
     C = x.shape[-1]
-    if halo_conv_rows(x, wp, nimg, H, W, upsample=kw.get("upsample", False),
-                      upsample_size=kw.get("upsample_size")) > 0:
+    # the in-staging transform costs ~1.2-1.5 us per 64-channel chunk, a GroupNorm apply pass ~10-14 us at the UNet's
+    # sizes: folding pays up to ~10 chunks (probes/conv_ab.py, profiles/r04d_conv_ab.jsonl, r04e_conv_ab.jsonl);
+    # wider inputs take the apply pass and the plain halo conv
+    if C <= knobs.get("FD_HALO_GN_CIN_MAX") and halo_conv_rows(x, wp, nimg, H, W, upsample=kw.get("upsample", False),
+                                                            upsample_size=kw.get("upsample_size")) > 0:
         aff = group_norm_affine(x, gamma, beta, nimg, H * W, C, groups, eps, stats=stats)
         return conv3x3(x, wp, bias, nimg, H, W, gn_in=(aff, silu), **kw)
     h = group_norm(x, gamma, beta, nimg, H * W, C, groups, eps, silu=silu, stats=stats)
