@@ -126,38 +126,6 @@ extern "C" int fd_axpby(const void* x, long long ldx, const void* z, long long l
 }
 
 // ------------------------------------------------------------------------------------------------
-// Weight prefetch: read a buffer once (16-B loads, grid-stride) so its lines sit in the memory-side Infinity Cache
-// (256 MB) when the GEMM that needs it starts.  The UNet's 5 GB of weights do not fit there, so every GEMM of a
-// forward otherwise starts on HBM misses; HipUNet issues these one transformer block ahead on a side stream inside
-// the captured graph.  The loaded values feed an XOR that is stored only on an impossible match (keeps the loads).
-__device__ unsigned g_prefetch_sink;
-
-__global__ void __launch_bounds__(256) prefetch_kernel(const uint4* __restrict__ p, long long n16,
-                                                       unsigned* __restrict__ sink) {
-  unsigned acc = 0;
-  const long long stride = (long long)gridDim.x * 256;
-  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {  // four loads in flight per lane
-    const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
-    acc ^= a.x ^ b.y ^ c.z ^ d.w;
-  }
-  for (; i < n16; i += stride) acc ^= p[i].x;
-  if (acc == 0x9E3779B9u && n16 == 12345) sink[0] = acc;
-}
-
-extern "C" int fd_prefetch(const void* p, long long bytes, int nwg, void* stream) {
-  if (!p || bytes < 0 || nwg <= 0) return FD_ERR_ARG;
-  if (((unsigned long long)p) & 15) return FD_ERR_ARG;
-  const long long n16 = bytes / 16;
-  if (n16 == 0) return FD_OK;
-  static unsigned* sink = nullptr;  // resolved on the first (eager) call, before any graph capture
-  if (!sink && hipGetSymbolAddress((void**)&sink, HIP_SYMBOL(g_prefetch_sink)) != hipSuccess) return FD_ERR_HIP;
-  hipLaunchKernelGGL(prefetch_kernel, dim3(nwg), dim3(256), 0, (hipStream_t)stream, (const uint4*)p, n16, sink);
-  FD_LAUNCH_CHECK();
-  return FD_OK;
-}
-
-// ------------------------------------------------------------------------------------------------
 // layout transposes.  NCHW [n][C][HW] <-> NHWC [n][HW][C]; 32x32 LDS tiles.
 template <typename TI, typename TO, bool TO_NHWC>
 __global__ void layout_kernel(const TI* __restrict__ x, TO* __restrict__ y, int C, int HW, float scale) {

@@ -27,7 +27,6 @@ HOST_DEFAULTS = {
     "FD_CFG_STREAMS": 0,    # UNet forward split into two concurrent row halves after the extras
     "FD_XATTN_GEMM": 1,     # attn2 as two GEMMs (scores + softmax epilogue, P . V W_o) against per-prompt products
     "FD_HALO_GN_CIN_MAX": 640,  # GroupNorm folded into the halo conv's staging pass up to this many input channels
-    "FD_PREFETCH": 0,       # weights prefetched into the Infinity Cache one block ahead (side stream): 1 transformer blocks, 2 + resnet convs
 }
 _host = dict(HOST_DEFAULTS)
 # string spellings some scripts use for the e4m3 kernel choice

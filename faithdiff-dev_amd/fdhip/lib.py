@@ -80,7 +80,6 @@ _SIGS = {
     "fd_unary": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_vp]),
     "fd_add_strided": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_int, c_int, c_vp]),
     "fd_axpby": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_f, c_f, c_int, c_vp]),
-    "fd_prefetch": (c_int, [c_vp, c_ll, c_int, c_vp]),
     "fd_nchw_to_nhwc": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_f, c_int, c_int, c_vp]),
     "fd_nhwc_to_nchw": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_f, c_int, c_int, c_vp]),
     "fd_transpose": (c_int, [c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_int, c_ll, c_ll, c_int, c_vp]),

@@ -241,13 +241,6 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
     return out
 
 
-def prefetch(tensors, nwg=128):
-    """fd_prefetch each tensor (weights one block ahead: their lines land in the Infinity Cache)."""
-    for t in tensors:
-        if t is not None and t.numel():
-            L.check(L.load().fd_prefetch(L.ptr(t), t.numel() * t.element_size(), nwg, L.stream()), "fd_prefetch")
-
-
 XSLOT = 80  # keys per head group of the two-GEMM cross-attention (two heads per 160-column score tile)
 
 

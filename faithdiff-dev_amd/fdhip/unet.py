@@ -93,11 +93,7 @@ class HipUNet:
         # the folded 16-bit model only (FD_XATTN_GEMM=0: Q projection + flash attention + out-projection)
         self.xattn = self.ln_fold and knobs.get("FD_XATTN_GEMM") != 0
         self._pbuf = {}
-        # weights of the next transformer block read into the Infinity Cache on a side stream while this block runs
-        # (the forward's 5 GB of weights do not fit the 256 MB cache: every GEMM would start on HBM misses)
-        self.prefetch = knobs.get("FD_PREFETCH") != 0
-        self.prefetch_convs = knobs.get("FD_PREFETCH") >= 2  # also the next resnet's conv weights
-        self._pf_stream = None
+
         # GroupNorm statistics from the producing conv / GEMM epilogue (256-row tiles; FD_UNET_GN_EPI=0: off)
         self.gn_epi = knobs.get("FD_UNET_GN_EPI") != 0
         self._gn_src = None
@@ -180,11 +176,6 @@ class HipUNet:
                 blk["us"] = (_dev(ops.pack_conv3x3(sd[p + ".weight"]), self.device, dtype), Fp(p + ".bias"))
             self.up.append(blk)
             prev = co
-        # forward order of the resnets: each prefetches the next one's conv weights (FD_PREFETCH=2)
-        order = [r for blk in self.down for r in blk["resnets"]] + [self.mid["r0"], self.mid["r1"]] + \
-                [r for blk in self.up for r in blk["resnets"]]
-        for a, b in zip(order, order[1:]):
-            a["next"] = b
         self.norm_out = (Fp("conv_norm_out.weight"), Fp("conv_norm_out.bias"))
         self.conv_out = (_dev(ops.pack_conv3x3(sd["conv_out.weight"]), self.device, dtype), Fp("conv_out.bias"))
         self.temb_w = _dev(torch.cat(temb_w, 0), self.device, dtype)
@@ -281,9 +272,6 @@ class HipUNet:
     def _resnet(self, r, x, B, H, Wd, temb, x2=None, C1=None):
         """x: [M, cin] (or concat(x [M,C1], x2) when x2 is given)."""
         HW = H * Wd
-        if self.prefetch_convs and "next" in r:
-            nx = r["next"]
-            self._prefetch([nx["c1"][0], nx["c2"][0]] + ([nx["sc"][0]] if "sc" in nx else []))
         if x2 is not None:
             cat = torch.empty((B * HW, r["cin"]), dtype=self.dtype, device=self.device)
             ops.concat_channels(x, C1, x2, r["cin"] - C1, cat, B * HW)
@@ -415,7 +403,6 @@ class HipUNet:
         C, heads, HW = t["c"], t["heads"], H * Wd
         M = B * HW
         st = torch.empty((M, C // 160, 2), dtype=torch.float32, device=self.device)
-        self._prefetch(self._block_weights(t["blocks"][0]))  # block 0's weights under proj_in
         h = ops.gemm(hn, t["pin"][0], bias=t["pin"][1], ln_out=st)
         # the two-GEMM cross-attention needs its matrices (Lk <= 80) and whole 256-row groups per image
         xa = self.xattn and self.Lk <= self.XSLOT and HW % 256 == 0 and t["blocks"][0].get("xm") is not None
@@ -423,8 +410,6 @@ class HipUNet:
         att = torch.empty((M, C), dtype=self.dtype, device=self.device)
         nb = len(t["blocks"])
         for i, b in enumerate(t["blocks"]):
-            # the next block's weights (or proj_out's after the last) into the Infinity Cache under this block
-            self._prefetch(self._block_weights(t["blocks"][i + 1]) if i + 1 < nb else [t["pout"][0]])
             w, c, d = b["qkv_f"]
             ops.gemm(h, w, bias=d, out=qkv, ln_in=st, ln_c=c)
             ops.flash_attn(qkv, qkv[:, C:], qkv[:, 2 * C:], att, B, heads, HW, HW, 3 * C, 3 * C, 3 * C, C,
@@ -446,25 +431,6 @@ class HipUNet:
             ff = ops.gemm(h, w, bias=d, act="geglu", ln_in=st, ln_c=c)
             ops.gemm(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h, ln_out=st if i + 1 < nb else None)
         return self._proj_out(t, h, x, B, HW)
-
-    def _block_weights(self, b):
-        if "qkv_f" not in b:
-            return []
-        att2 = [b["xm"].b1, b["xm"].b2] if self.xattn and b.get("xm") is not None else [b["q2_f"][0], b["o2"][0]]
-        return [b["qkv_f"][0], b["o1"][0]] + att2 + [b["ff1_f"][0], b["ff2"][0]]
-
-    def _prefetch(self, tensors):
-        """Issue fd_prefetch of these weights on the side stream, ordered after everything enqueued so far on the
-        current stream; _forward joins the side stream at its end (inside the captured graph)."""
-        if not self.prefetch or not tensors:
-            return
-        cur = torch.cuda.current_stream(self.device)
-        if self._pf_stream is None:
-            self._pf_stream = torch.cuda.Stream(self.device)
-        self._pf_stream.wait_stream(cur)
-        with torch.cuda.stream(self._pf_stream):
-            ops.prefetch(tensors)
-        self._pf_used = True
 
     def _pbuf_get(self, M, KP):
         """The probability buffer of the two-GEMM cross-attention [M, KP]: persistent per shape (hipGraph replays
@@ -565,7 +531,6 @@ class HipUNet:
         # no split-K, so the streams never share the GEMM workspace).  Opt-in (FD_SIDE_STREAM=1): measured
         # 0.39 ms/step SLOWER at C2 when it also carried the prompt K/V GEMM (now in set_context).
         self._gn_src = None
-        self._pf_used = False
         cur = torch.cuda.current_stream(self.device)
         side = self._side_stream()
         if side is not None:
@@ -611,7 +576,4 @@ class HipUNet:
                 h = ops.conv3x3(h, *blk["us"], B, hh, ww, upsample=True, upsample_size=(th, tw))
                 hh, ww = th, tw
         h = ops.group_norm(h, *self.norm_out, B, hh * ww, 320, 32, 1e-5, silu=True, stats=self._gn_stats_of(h))
-        out = ops.conv3x3(h, *self.conv_out, B, hh, ww)
-        if self._pf_used:  # join the prefetch stream (required inside graph capture)
-            cur.wait_stream(self._pf_stream)
-        return out
+        return ops.conv3x3(h, *self.conv_out, B, hh, ww)

@@ -299,9 +299,6 @@ int fd_add_strided(const void* x, long long ldx, const void* a, long long lda, v
                    int dtype, int out_dtype, void* stream);
 /* y[m][n] = alpha * x[m][n] + beta * z[m][n] (bf16/f16, N % 8 == 0, 16-B aligned rows; y may alias z).
  * Replaces the RRDB residual `out * 0.2 + x` of the BSRNet pre-pass (bsrnet_arch.py:72-76). */
-/* Read `bytes` at p once (16-B aligned) with nwg workgroups so the lines are in the Infinity Cache when a later
- * kernel reads them (weight prefetch one transformer block ahead, on a side stream of the UNet graph). */
-int fd_prefetch(const void* p, long long bytes, int nwg, void* stream);
 int fd_axpby(const void* x, long long ldx, const void* z, long long ldz, void* y, long long ldy, int M, int N,
              float alpha, float beta, int dtype, void* stream);
 /* NCHW <-> NHWC transposes (dtype in, out_dtype out; scale applied). */

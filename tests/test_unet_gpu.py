@@ -102,34 +102,6 @@ def test_unet_forward_matches_reference_golden(name):
     assert rel < 1.5e-2 and cos > 0.9999
 
 
-def test_unet_prefetch_changes_no_bit():
-    """The weight prefetch (FD_PREFETCH 1 / 2: fd_prefetch on a side stream, joined at the end of the forward) only
-    reads weights: the forward is bitwise the same with and without it, eager and as a captured graph."""
-    from fdhip import knobs
-    _, hip = unet_pair()
-    h = w = 64
-    B, x, cond, ctx, text, tids = make_inputs(h, w, 1, seed=9)
-    base = run_hip(hip, B, x, cond, ctx, text, tids, 951.0, h, w)
-    for mode in (1, 2):
-        old = (hip.prefetch, hip.prefetch_convs)
-        hip.prefetch, hip.prefetch_convs = True, mode >= 2
-        try:
-            got = run_hip(hip, B, x, cond, ctx, text, tids, 951.0, h, w)
-            dev = "cuda"
-            xn = x.permute(0, 2, 3, 1).reshape(B * h * w, 4).to(dev, torch.bfloat16).contiguous()
-            cn = cond.permute(0, 2, 3, 1).reshape(B * h * w, 512).to(dev, torch.bfloat16).contiguous()
-            args = [xn, torch.full((B,), 951.0, device=dev), tids.to(dev), text.to(dev), cn]
-            for _ in range(3):  # eager, capture, replay
-                g = hip.run(*args, B, h, w).float().reshape(B, h, w, 4).permute(0, 3, 1, 2).cpu()
-            torch.cuda.synchronize()
-        finally:
-            hip.prefetch, hip.prefetch_convs = old
-            hip.graphs.clear()
-        assert torch.equal(got, base), mode
-        assert torch.equal(g, base), mode
-    assert knobs.get("FD_PREFETCH") == knobs.default("FD_PREFETCH")
-
-
 def test_unet_cfg_rows_and_tile_batching_consistent():
     """Batching two tiles in one forward == two single-tile forwards (rows independent, bitwise)."""
     _, hip = unet_pair()
