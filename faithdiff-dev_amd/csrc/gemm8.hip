@@ -1046,14 +1046,17 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
   Plan8 q;
   if (p->act == FD_ACT_SOFTMAX) {
     // the attention-score GEMM: 160-column tiles (two 80-column head groups): the tile with the fewest operand bytes
-    // per CU, rounds on 256 CUs x (BM + BN), counted from m_ref (batching never changes the plan); FD_XATTN_SPLIT:
-    // the 128 x 160 form with K split in two (pairwise combine, softmax after it) -- 320 half-K workgroups instead of
-    // 160 full ones at M = 2048
+    // per CU, rounds on 256 CUs x (BM + BN); FD_XATTN_SPLIT: the 128 x 160 form with K split in two (pairwise
+    // combine, softmax after it) -- 320 half-K workgroups instead of 160 full ones at M = 2048 (measured slower)
     if (p->N % 160) return 0;
+    // one K pass: every tile shape gives the same bits, so the batched M may choose (C3's 13 tiles: 256 x 160);
+    // with the split the plan must come from m_ref (the split changes the summation order)
+    const int xsplit = fd_knob(FDK_XATTN_SPLIT);
+    const int m_plan = xsplit ? m_ref : p->M;
     int best = 0;
     long long bc = 0;
     for (int bm = 256; bm >= 64; bm /= 2) {
-      const long long tiles = (long long)((m_ref + bm - 1) / bm) * (p->N / 160);
+      const long long tiles = (long long)((m_plan + bm - 1) / bm) * (p->N / 160);
       const long long c = (tiles + 255) / 256 * (bm + 160);
       if (!best || c < bc) {
         best = bm;
@@ -1066,7 +1069,7 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     q.nw = (best == 256 || (best == 128 && w8)) ? 8 : 4;
     q.waves_m = best == 256 ? 8 : (best == 128 && w8) ? 4 : 2;
     q.ns = 3;
-    q.S = (best == 128 && fd_knob(FDK_XATTN_SPLIT) && p->K >= 1024) ? 2 : 1;
+    q.S = (best == 128 && xsplit && p->K >= 1024) ? 2 : 1;
     goto planned;
   }
   if (p->ln_out) {
