@@ -37,7 +37,16 @@ constexpr int PW = 18;  // patch width: 16 output columns + halo
 constexpr int TR = 4;   // tap of chunk c at which chunk c + 1's patch is waited for
 constexpr int NPART = 8 - TR;  // ... and transformed in NPART pieces at taps TR .. 7 (published by tap 8's barrier)
 
-template <typename T, int TH, int BN, bool GNI, bool SK, int NS>
+// LDS-only workgroup barrier: this wave's LDS operations retired, then s_barrier.  Unlike __syncthreads() it does
+// not drain vector memory, so LDS-DMA and stores issued before it stay in flight (the PT epilogue relies on that).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// PT (persistent tiles): one workgroup per CU walks a strided list of tiles inside its XCD's contiguous share; the
+// epilogue stages 32-row passes in an LDS region of its own past the ring, so the next tile's weight stages and
+// patches are DMA'd while this tile's outputs are written (the non-PT form waits for its patches at the start of
+// every tile and stores at the end with nothing to overlap either: at the VAE's 1024^2 level that was ~1/3 of the
+// conv).  The per-element K order, the stored values and the GroupNorm partials are bit for bit the non-PT ones.
+template <typename T, int TH, int BN, bool GNI, bool SK, int NS, bool PT>
 __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, float* __restrict__ slabs,
                                                           unsigned* __restrict__ counters) {
   typedef typename VecT<T>::v8 V8;
@@ -60,7 +69,12 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   constexpr int EROWS = 128, LDE = BN + 4, EPB = EROWS * LDE * 4, VPR = BN / 8;
   constexpr int SLOT = EPB, RED = SLOT + EROWS * VPR * 16;
   constexpr int SMEM_EPI = RED + 512 * 8;
-  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  constexpr int PER = 32;  // PT epilogue pass: 32 rows x BN fp32 + their GroupNorm slots, past the ring
+  constexpr int PT_EP = SMEM_MAIN, PT_SLOT = PT_EP + PER * LDE * 4, PT_END = PT_SLOT + PER * VPR * 16;
+  static_assert(!PT || (!SK && BN == 128 && TH == 16 && PER * VPR == 512 && PT_END <= 163840 &&
+                        PER * LDE * 4 >= 512 * 8),
+                "PT layout: one 8-column vector per thread per pass, red[] in the pass buffer");
+  constexpr int SMEM = PT ? PT_END : (SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI);
   static_assert(SMEM <= 163840, "LDS");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[SMEM];
 
@@ -75,10 +89,17 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   // runs at once share one weight panel in its L2; SK: the two channel halves of a tile adjacent (same XCD)
   const int pid = xcd_remap(blockIdx.x, gridDim.x);
   const int split = SK ? (pid & 1) : 0, tlin = SK ? (pid >> 1) : pid;
-  const int nt = tlin / nsp, sp = tlin - nt * nsp;
-  const int img = sp / (tiles_y * tiles_x), spi = sp - img * (tiles_y * tiles_x);
-  const int tyt = spi / tiles_x, txt = spi - tyt * tiles_x;
-  const int y0 = tyt * TH, x0 = txt * 16, n0 = nt * BN;
+  // this workgroup's tiles: tl, tl + tl_step, ... < tl_hi (non-PT: the one tile tlin).  PT: workgroups b and b + 8
+  // share an XCD (blocks are dealt round-robin), so XCD b % 8 takes the contiguous eighth [lo, hi) of the tile
+  // order and its gx workgroups stride it -- the ~32 tiles an XCD holds at once are neighbours sharing halo rows
+  int tl = tlin, tl_hi = tlin + 1, tl_step = 1;
+  if constexpr (PT) {
+    const int total = (N / BN) * nsp, xcd = blockIdx.x & 7;
+    tl = (int)((long long)xcd * total / 8) + (blockIdx.x >> 3);
+    tl_hi = (int)((long long)(xcd + 1) * total / 8);
+    tl_step = gridDim.x >> 3;
+    if (tl >= tl_hi) return;
+  }
   // input-channel chunks of this workgroup: all, or (SK) one half of them, combined pairwise after the K loop
   const int nch_all = Cin / 64;
   const int cb = SK && split ? nch_all / 2 : 0, ce = SK && !split ? nch_all / 2 : nch_all;
@@ -87,53 +108,80 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   const T* __restrict__ Bw = (const T*)p.B;
   const bool up2 = p.upsample && Ho == 2 * p.Hin && Wo == 2 * p.Win;
 
-  // ---- weight stages (waves 0-3): rows n0 + (w + 4 i) * 8 + lane / 8, source-side XOR swizzle of 128-B rows
-  const T* b_row[PER_B];
-  const T* p_src[P_I];  // patch pixels (waves 4-7): this lane's source 16-B chunk at channel 0, nullptr = outside
-  if (w < 4) {
-#pragma unroll
-    for (int i = 0; i < PER_B; ++i) {
-      const int row = (w + 4 * i) * 8 + (lane >> 3);
-      b_row[i] = Bw + (long long)(n0 + row) * p.ldb + (((lane & 7) ^ ((row >> 1) & 7)) * 8);
+  // ---- per-tile coordinates and DMA sources.  Weight stages (waves 0-3): rows n0 + (w + 4 i) * 8 + lane / 8,
+  // source-side XOR swizzle of 128-B rows; patch pixels (waves 4-7): this lane's source 16-B chunk at channel 0,
+  // nullptr = outside the image.  Non-PT: computed once into registers.  PT: recomputed at each DMA issue from the
+  // (wave-uniform) tile coordinates, which keeps ~30 VGPRs of pointers out of the epilogue, and rows past the patch
+  // (j >= P_TOT) re-load row P_TOT - 1 (the same bytes to the same LDS address), so every patch wave issues exactly
+  // P_I loads per chunk and the epilogue's counted waits hold
+  int img = 0, spi = 0, y0 = 0, x0 = 0, n0 = 0;
+  const T* b_row[PT ? 1 : PER_B];
+  const T* p_src[PT ? 1 : P_I];
+  const float* __restrict__ aff = nullptr;
+  auto b_src = [&] __attribute__((always_inline)) (int i) {
+    int row = (w + 4 * i) * 8 + (lane >> 3);
+    if constexpr (PT) asm volatile("" : "+v"(row));
+    return Bw + (long long)(n0 + row) * p.ldb + (((lane & 7) ^ ((row >> 1) & 7)) * 8);
+  };
+  auto p_row = [&] __attribute__((always_inline)) (int i) { return PT ? min((w - 4) + 4 * i, P_TOT - 1) : (w - 4) + 4 * i; };
+  auto p_src_of = [&] __attribute__((always_inline)) (int i) -> const T* {
+    const int j = p_row(i);
+    int pix = j * 8 + (lane >> 3);
+    if constexpr (PT) asm volatile("" : "+v"(pix));  // PT: recomputed at each issue, never hoisted out of the loops
+    const int py = pix / PW, px = pix - (pix / PW) * PW;
+    const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+    const bool ok = j < P_TOT && pix < PIX && iy >= 0 && iy < Ho && ix >= 0 && ix < Wo;
+    int sy = iy, sx = ix;
+    if (p.upsample) {
+      sy = up2 ? (iy >> 1) : (iy * p.Hin) / Ho;
+      sx = up2 ? (ix >> 1) : (ix * p.Win) / Wo;
     }
-  } else {
+    return ok ? A + ((long long)(img * p.Hin + sy) * p.Win + sx) * p.lda + (((lane & 7) ^ ((pix >> 1) & 7)) * 8)
+              : nullptr;
+  };
+  auto setup = [&] __attribute__((always_inline)) (int tile) {
+    const int nt = tile / nsp, sp = tile - nt * nsp;
+    img = sp / (tiles_y * tiles_x);
+    spi = sp - img * (tiles_y * tiles_x);
+    const int tyt = spi / tiles_x, txt = spi - tyt * tiles_x;
+    y0 = tyt * TH;
+    x0 = txt * 16;
+    n0 = nt * BN;
+    if constexpr (!PT) {
+      if (w < 4) {
 #pragma unroll
-    for (int i = 0; i < P_I; ++i) {
-      const int j = (w - 4) + 4 * i;
-      const int pix = j * 8 + (lane >> 3);
-      const int py = pix / PW, px = pix - (pix / PW) * PW;
-      const int iy = y0 - 1 + py, ix = x0 - 1 + px;
-      const bool ok = j < P_TOT && pix < PIX && iy >= 0 && iy < Ho && ix >= 0 && ix < Wo;
-      int sy = iy, sx = ix;
-      if (p.upsample) {
-        sy = up2 ? (iy >> 1) : (iy * p.Hin) / Ho;
-        sx = up2 ? (ix >> 1) : (ix * p.Win) / Wo;
+        for (int i = 0; i < PER_B; ++i) b_row[i] = b_src(i);
+      } else {
+#pragma unroll
+        for (int i = 0; i < P_I; ++i) p_src[i] = p_src_of(i);
       }
-      p_src[i] = ok ? A + ((long long)(img * p.Hin + sy) * p.Win + sx) * p.lda + (((lane & 7) ^ ((pix >> 1) & 7)) * 8)
-                    : nullptr;
     }
-  }
-  const float* __restrict__ aff = GNI ? (const float*)p.gi_affine + (long long)img * Cin * 2 : nullptr;
+    if (GNI) aff = (const float*)p.gi_affine + (long long)img * Cin * 2;
+  };
 
-  auto stage_b = [&](int s, int rb) {  // s: this workgroup's step (chunk cb + s / 9, tap s % 9)
+  auto stage_b = [&] __attribute__((always_inline)) (int s, int rb) {  // s: this workgroup's step (chunk cb + s / 9, tap s % 9)
     const int c = cb + s / 9, t = s - (s / 9) * 9;
     const int off = t * Cin + c * 64;
     unsigned char* dst = smem + RING + rb * STAGE;
 #pragma unroll
     for (int i = 0; i < PER_B; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + off), LDS_PTR(dst + (w + 4 * i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)((PT ? b_src(i) : b_row[PT ? 0 : i]) + off),
+                                       LDS_PTR(dst + (w + 4 * i) * 1024), 16, 0, 0);
   };
-  auto stage_p = [&](int c) {  // patch of chunk c into buffer c & 1 (+ its affine table)
+  auto stage_p = [&] __attribute__((always_inline)) (int c) {  // patch of chunk c into buffer c & 1 (+ its affine table)
     unsigned char* dst = smem + (c & 1) * PBUF;
 #pragma unroll
     for (int i = 0; i < P_I; ++i) {
-      const int j = (w - 4) + 4 * i;
-      if (j < P_TOT) {
-        const void* s = p_src[i] ? (const void*)(p_src[i] + c * 64) : (const void*)g_zero_halo;
+      const int j = p_row(i);
+      if (PT || j < P_TOT) {
+        const T* src = PT ? p_src_of(i) : p_src[PT ? 0 : i];
+        const void* s = src ? (const void*)(src + c * 64) : (const void*)g_zero_halo;
         __builtin_amdgcn_global_load_lds(s, LDS_PTR(dst + j * 1024), 16, 0, 0);
       }
     }
-    if (GNI && w == 4)  // 64 channels x (scale, shift) = 512 B; the upper half of the 1 KB is never read
+    // 64 channels x (scale, shift) = 512 B; the upper half of the 1 KB is never read.  PT: every patch wave loads it
+    // (identical bytes), for the uniform DMA count
+    if (GNI && (PT || w == 4))
       __builtin_amdgcn_global_load_lds((const void*)(aff + (long long)c * 128 + lane * 4), LDS_PTR(dst + PATCH), 16, 0,
                                        0);
   };
@@ -141,7 +189,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   // bits), zero outside the image.  Each thread keeps one logical 8-channel slot (tid % 8) for every pixel.  Piece
   // `part` of `nparts` covers pixels [part * PIX / nparts, (part + 1) * PIX / nparts): the main loop transforms the
   // next chunk's patch a piece per tap, issued behind that tap's MFMAs so the VALU work runs under them.
-  auto transform = [&](int c, int part, auto npc) {
+  auto transform = [&] __attribute__((always_inline)) (int c, int part, auto npc) {
     constexpr int NP = decltype(npc)::value;
     unsigned char* buf = smem + (c & 1) * PBUF;
     const int lc = tid & 7;
@@ -181,7 +229,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       }
     }
   };
-  auto read_frags = [&](int c, int t, int rb, int h, V8 (&af)[MT], V8 (&bf)[NT]) {
+  auto read_frags = [&] __attribute__((always_inline)) (int c, int t, int rb, int h, V8 (&af)[MT], V8 (&bf)[NT]) {
     const unsigned char* pa = smem + (c & 1) * PBUF;
     const unsigned char* sb = smem + RING + rb * STAGE;
     const int ky = t / 3, kx = t - (t / 3) * 3;
@@ -198,18 +246,14 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     }
   };
   f32x4 acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const V8 (&af)[MT], const V8 (&bf)[NT]) {
+  auto mma =[&](const V8 (&af)[MT], const V8 (&bf)[NT]) {
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = mfma16x16x32(af[mi], bf[ni], acc[mi][ni]);
   };
   // B-waves: all but the youngest `ahead` weight stages landed (ahead <= NS - 1)
-  auto wait_b = [&](int ahead) {
+  auto wait_b = [&] __attribute__((always_inline)) (int ahead) {
     if (NS >= 5 && ahead >= 4) hvm<(NS >= 5 ? 4 : 0) * PER_B>();
     else if (NS >= 4 && ahead >= 3) hvm<(NS >= 4 ? 3 : 0) * PER_B>();
     else if (ahead >= 2) hvm<2 * PER_B>();
@@ -217,17 +261,29 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     else hvm<0>();
   };
 
-  // ---- prologue: weight stages 0..NS-1, patches of chunks 0 and 1
-  if (w < 4) {
+  // ---- prologue DMA: weight stages 0..NS-1, patches of chunks 0 and 1
+  auto prologue_dma = [&] __attribute__((always_inline)) () {
+    if (w < 4) {
 #pragma unroll
-    for (int s0 = 0; s0 < NS; ++s0)
-      if (s0 < nsteps) stage_b(s0, s0);
-    wait_b(min(nsteps, NS) - 1);
-  } else {
-    stage_p(cb);
-    if (cb + 1 < ce) stage_p(cb + 1);
-    hvm<0>();
-  }
+      for (int s0 = 0; s0 < NS; ++s0)
+        if (s0 < nsteps) stage_b(s0, s0);
+    } else {
+      stage_p(cb);
+      if (cb + 1 < ce) stage_p(cb + 1);
+    }
+  };
+  setup(tl);
+  prologue_dma();
+  for (bool first = true;; first = false) {
+  // PT after the first tile: the DMA went out under the previous tile's epilogue, whose 8 output stores (one per
+  // pass; wave 0 also the GroupNorm partial) are the only younger vector-memory operations
+  if (PT && !first) hvm<8>();
+  else if (w < 4) wait_b(min(nsteps, NS) - 1);
+  else hvm<0>();
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   __builtin_amdgcn_s_barrier();
   if (GNI) {
     transform(cb, 0, std::integral_constant<int, 1>());
@@ -271,6 +327,129 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   read_frags(c, t, rb, 1, a1, b1);
   mma(a0, b0);
   mma(a1, b1);
+
+  if constexpr (PT) {
+    // ---- PT epilogue: thread tid owns the 8-column vector cv of row rr of each 32-row pass.  This tile's bias and
+    // residual go into registers first (older than the next tile's DMA, so the compiler's counted waits on them do
+    // not wait for it), then -- every wave past its last ring / patch read -- the next tile's DMA is issued, then
+    // the passes run on the PT region only.  Stores, GroupNorm slots and the fixed-order fold as in the 128-row
+    // epilogue below (the fold visits rows gj, gj + TPG, ... in the same order, so the partials are the same bits).
+    constexpr int NPASS = BM / PER;
+    const int rr = tid >> 4, cv = tid & 15, n = n0 + cv * 8;
+    const T* __restrict__ R = (const T*)p.residual;
+    float bv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) bv[i] = 0.f;
+    if (p.bias) {
+      *(f32x4*)&bv[0] = *(const f32x4*)(p.bias + n);
+      *(f32x4*)&bv[4] = *(const f32x4*)(p.bias + n + 4);
+    }
+    const long long m0 = ((long long)img * Ho + y0) * Wo + x0;  // output row of the tile's pixel (0, 0)
+    TO8 res[NPASS];
+    if (R) {
+#pragma unroll
+      for (int k = 0; k < NPASS; ++k) {
+        const int rt = k * PER + rr;
+        res[k] = *(const TO8*)(R + (m0 + (long long)(rt >> 4) * Wo + (rt & 15)) * p.ldr + n);
+      }
+    }
+    const int cimg = img, cspi = spi, cn0 = n0;
+    lds_barrier();
+    const int tl_next = tl + tl_step;
+    if (tl_next < tl_hi) {
+      setup(tl_next);
+      prologue_dma();
+    }
+    T* __restrict__ C = (T*)p.C;
+    float* ep = (float*)(smem + PT_EP);
+    f32x4* const slots = (f32x4*)(smem + PT_SLOT);
+    const bool gn = p.gn_part != nullptr;
+    const int cpg = gn ? N / p.gn_groups : 8;
+    const int G = BN / cpg, TPG = gn ? 512 / G : 512;
+    const int gg = tid / TPG, gj = tid - (tid / TPG) * TPG;
+    float gs = 0.f, gq = 0.f;
+#pragma unroll 1
+    for (int k = 0; k < NPASS; ++k) {
+      if (k) lds_barrier();  // the previous pass's ep / slot reads done
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        if (wm * WM + mi * 16 >= k * PER && wm * WM + mi * 16 < (k + 1) * PER) {
+          const int rl = wm * WM + mi * 16 + fg * 4 - k * PER;
+#pragma unroll
+          for (int ni = 0; ni < NT; ++ni) {
+            const int col = wn * WN + ni * 16 + fr;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ep[(rl + j) * LDE + col] = acc[mi][ni][j] * p.alpha;
+          }
+        }
+      }
+      lds_barrier();
+      float v[8];
+      *(f32x4*)&v[0] = *(const f32x4*)(ep + rr * LDE + cv * 8);
+      *(f32x4*)&v[4] = *(const f32x4*)(ep + rr * LDE + cv * 8 + 4);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] += bv[i];
+      if (p.act != FD_ACT_NONE) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = act_f(v[i], p.act);
+      }
+      if (R) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += (float)res[k][i];
+      }
+      TO8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (T)v[i];
+      const int rt = k * PER + rr;
+      *(TO8*)(C + (m0 + (long long)(rt >> 4) * Wo + (rt & 15)) * p.ldc + n) = o;
+      if (gn) {
+        const int sp8 = ((cv * 8) / cpg + 1) * cpg - cv * 8;
+        float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float f = (float)o[i];
+          if (i < sp8) {
+            s0 += f;
+            q0 += f * f;
+          } else {
+            s1 += f;
+            q1 += f * f;
+          }
+        }
+        slots[tid] = (f32x4){s0, q0, s1, q1};
+        lds_barrier();
+        const int cc0 = (gg * cpg) / 8, cc1 = ((gg + 1) * cpg - 1) / 8;
+        const int r0 = ((gj - (k * PER) % TPG) % TPG + TPG) % TPG;  // first row of this pass that is = gj mod TPG
+        for (int r = r0; r < PER; r += TPG)
+          for (int cc = cc0; cc <= cc1; ++cc) {
+            const f32x4 v4 = slots[r * VPR + cc];
+            const bool fst = (cc * 8) / cpg == gg;
+            gs += fst ? v4[0] : v4[2];
+            gq += fst ? v4[1] : v4[3];
+          }
+      }
+    }
+    if (gn) {  // red[] in the pass buffer: its last readers passed the fold barrier above
+      float2* red = (float2*)ep;
+      red[tid] = make_float2(gs, gq);
+      lds_barrier();
+      if (tid < G) {
+        float S = 0.f, Q = 0.f;
+        for (int k = 0; k < TPG; ++k) {
+          const float2 v2 = red[tid * TPG + k];
+          S += v2.x;
+          Q += v2.y;
+        }
+        const long long blk = (long long)cimg * (tiles_y * tiles_x) + cspi;
+        ((float2*)p.gn_part)[blk * p.gn_groups + cn0 / cpg + tid] = make_float2(S, Q);
+      }
+    }
+    tl = tl_next;
+    if (tl >= tl_hi) return;
+    continue;
+  }
+  break;
+  }  // tile loop (one pass unless PT)
 
   // ---- SK: pairwise combine (gemm8's S = 2 form): the first half to finish publishes its fp32 accumulators with
   // write-through (sc1) stores and an sc1 flag; the second waits for the flag, adds them to its own (a + b: the
@@ -444,7 +623,32 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
 
 struct HaloPlan {
   int th, bn, tiles, sk, ns;  // tiles: output tiles (workgroups = tiles * (1 + sk)); ns: weight ring depth
+  int pt;                     // persistent workgroups (PT form), 0 = one workgroup per tile
 };
+
+// Compute units of the current device (cached per device id).
+int cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cache[dev] = v;
+  }
+  return cache[dev];
+}
+
+// The PT form: 256-row x 128-column tiles over whole images (every tile full: one store per thread and pass), at
+// least two chunks of input channels (the prologue DMA count the epilogue waits rely on), no per-image row bias,
+// and at least two tiles per CU (below that there is no next tile to overlap).  Returns its workgroup count.
+int halo_pt_grid(const fd_gemm_params* p, int th, int bn, int sk, long long tiles) {
+  if (!fd_knob(FDK_CONV_HALO_PT) || th != 16 || bn != 128 || sk || p->Cin < 128 || p->rowbias) return 0;
+  if (p->Hout % 16 || p->Wout % 16) return 0;
+  const int cus = cu_count();
+  if (tiles < 2LL * cus || cus < 8) return 0;
+  return cus & ~7;
+}
 
 // Eligibility and tile plan, from per-image quantities only (m_ref: rows of one TLC tile's forward), so batching
 // tiles never moves a launch between this kernel and the implicit GEMM (bitwise batch invariance).
@@ -453,7 +657,9 @@ int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
   // 256^2 - 512^2 and the upsample convs: its intake beats the 128 / 160-column halo tile there even with the
   // GroupNorm pass, probes/conv_ab.py); 2 on wherever eligible
   const int mode = fd_knob(FDK_CONV_HALO);
-  if (!mode || (mode == 1 && gemm256_takes(p))) return 0;
+  if (!mode) return 0;
+  const bool g256 = mode == 1 && gemm256_takes(p);
+  if (g256 && fd_knob(FDK_CONV_HALO_PT) != 2) return 0;
   if (!p->conv || p->batch > 1 || p->stride != 1 || p->pad != 1 || p->A2 || p->K != 9 * p->Cin) return 0;
   if (p->Cin % 64 || p->lda < p->Cin || p->lda % 8 || p->ldb % 8 || p->ldc % 8) return 0;
   if (p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out || p->dtype != p->out_dtype || p->dtype == FD_F32) return 0;
@@ -481,11 +687,13 @@ int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
   pl->th = th;
   pl->bn = bn;
   pl->sk = sk;
-  // a 128-row tile's K step is half the MFMA work of a 256-row one: its weight stages need a deeper ring to cover
-  // the L2 latency (the 256-row tile's LDS holds only 3 stages)
-  pl->ns = th == 8 ? fd_knob(FDK_CONV_HALO_NS8) : 3;
   pl->tiles = (int)(p->nimg * ((p->Hout + th - 1) / th) * ((p->Wout + 15) / 16) * (p->N / bn));
   if (sk && pl->tiles > 32768) return 0;  // one split-K counter / flag per tile
+  pl->pt = halo_pt_grid(p, th, bn, sk, pl->tiles);
+  // a 128-row tile's K step is half the MFMA work of a 256-row one: its weight stages need a deeper ring to cover
+  // the L2 latency (the 256-row tile's LDS holds 3 stages at 160 columns, 4 at 128)
+  pl->ns = th == 8 ? fd_knob(FDK_CONV_HALO_NS8) : (bn == 128 && !pl->pt ? fd_knob(FDK_CONV_HALO_NS16) : 3);
+  if (g256 && !pl->pt) return 0;  // FD_CONV_HALO_PT = 2 takes a gemm256 conv only in the PT form
   return 1;
 }
 
@@ -496,18 +704,30 @@ int launch_halo(const fd_gemm_params* p, const HaloPlan& pl, hipStream_t s) {
   const bool gi = p->gi_affine != nullptr;
   float* slabs = pl.sk ? (float*)((char*)p->ws + 65536 * sizeof(unsigned)) : nullptr;
   unsigned* cnt = pl.sk ? (unsigned*)p->ws : nullptr;
-  const dim3 grid(pl.tiles * (1 + pl.sk));
+  const dim3 grid(pl.pt ? pl.pt : pl.tiles * (1 + pl.sk));
+  if (pl.pt) {
+    if (pl.th != 16 || pl.bn != 128 || pl.sk || pl.ns != 3) return FD_ERR_ARG;
+    if (gi)
+      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, true, false, 3, true>), grid, dim3(512), 0, s, *p, slabs, cnt);
+    else
+      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, false, false, 3, true>), grid, dim3(512), 0, s, *p, slabs, cnt);
+    FD_LAUNCH_CHECK();
+    return FD_OK;
+  }
 #define FD_HALO(TH_, BN_, SK_, NS_)                                                                                  \
   if (pl.th == TH_ && pl.bn == BN_ && pl.sk == SK_ && pl.ns == NS_) {                                                \
     if (gi)                                                                                                          \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true, SK_, NS_>), grid, dim3(512), 0, s, *p, slabs, cnt);   \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true, SK_, NS_, false>), grid, dim3(512), 0, s, *p, slabs,   \
+                         cnt);                                                                                       \
     else                                                                                                             \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, SK_, NS_>), grid, dim3(512), 0, s, *p, slabs, cnt);  \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, SK_, NS_, false>), grid, dim3(512), 0, s, *p, slabs,  \
+                         cnt);                                                                                       \
     FD_LAUNCH_CHECK();                                                                                               \
     return FD_OK;                                                                                                    \
   }
   FD_HALO(16, 160, 0, 3)
   FD_HALO(16, 128, 0, 3)
+  FD_HALO(16, 128, 0, 4)
   FD_HALO(8, 160, 0, 3)
   FD_HALO(8, 128, 0, 3)
   FD_HALO(8, 160, 1, 3)
@@ -527,6 +747,13 @@ extern "C" int fd_conv_halo_plan(const fd_gemm_params* p) {
   HaloPlan pl;
   if (!halo_plan(p, &pl)) return 0;
   return pl.th * 16;
+}
+
+// Workgroups of the PT form for this conv, 0 = one workgroup per tile (or not the halo kernel).
+extern "C" int fd_conv_halo_pt(const fd_gemm_params* p) {
+  HaloPlan pl;
+  if (!p || !halo_plan(p, &pl)) return 0;
+  return pl.pt;
 }
 
 // Split-K workspace of the halo kernel for this conv: -1 = the halo kernel does not take it, else bytes (0 = none).

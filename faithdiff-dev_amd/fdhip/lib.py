@@ -48,6 +48,7 @@ _SIGS = {
     "fd_gemm": (c_int, [ctypes.POINTER(GemmParams), c_vp]),
     "fd_gemm_ws_bytes": (c_ll, [ctypes.POINTER(GemmParams)]),
     "fd_conv_halo_plan": (c_int, [ctypes.POINTER(GemmParams)]),
+    "fd_conv_halo_pt": (c_int, [ctypes.POINTER(GemmParams)]),
     "fd_group_norm_affine": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_f, c_vp, c_vp, c_int,
                                      c_vp]),
     "fd_conv2d_direct": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_f,

@@ -545,6 +545,20 @@ def halo_conv_rows(x, wp, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, 
     return int(L.load().fd_conv_halo_plan(ctypes.byref(p)))
 
 
+def halo_conv_pt(x, wp, nimg, H, W, upsample=False, upsample_size=None, residual=False, rowbias=False):
+    """Workgroups of the halo kernel's persistent form for this conv (0: one workgroup per tile, or not the halo
+    kernel).  Shapes only."""
+    dummy = torch.empty((1, wp.shape[0]), dtype=x.dtype, device=x.device)
+    p, _ = _conv_params(x, wp, None, nimg, H, W, 1, 1, upsample, None, None, dummy, None, None, "none", None,
+                        upsample_size, None, 1.0)
+    p.C, p.ldc = x.data_ptr(), wp.shape[0]
+    if residual:
+        p.residual, p.ldr = x.data_ptr(), wp.shape[0]
+    if rowbias:
+        p.rowbias, p.rowbias_ld = x.data_ptr(), wp.shape[0]
+    return int(L.load().fd_conv_halo_pt(ctypes.byref(p)))
+
+
 def conv3x3_narrow(x, w32, bias, nimg, H, W, out_dtype=None, out=None):
     """3x3 conv (stride 1, pad 1) with Cout <= 4 on NHWC x [nimg*H*W, Cin]: w32 fp32 [Cout, 9*Cin] (tap-major, the
     pack_conv3x3 layout).  The VAE decoder's conv_out."""

@@ -135,6 +135,10 @@ int fd_gemm(fd_gemm_params* p, void* stream);  /* writes only p->gn_done */
  * tiles; the choice reads m_ref, never the batched M.  Returns the rows per GroupNorm-statistics block it writes
  * (256 or 128), 0 when fd_gemm would use the implicit GEMM for this conv. */
 int fd_conv_halo_plan(const fd_gemm_params* p);
+/* Workgroups of the halo kernel's persistent form for this conv (one per CU, each walking a strided list of 256-row
+ * tiles with the next tile's DMA under the current tile's epilogue; bitwise equal to the one-tile-per-workgroup
+ * form), 0 when the conv runs one workgroup per tile or not on the halo kernel.  Knob FD_CONV_HALO_PT. */
+int fd_conv_halo_pt(const fd_gemm_params* p);
 /* Workspace fd_gemm needs for this launch (0 = none). */
 long long fd_gemm_ws_bytes(const fd_gemm_params* p);
 

@@ -33,7 +33,9 @@ SHAPES = [("unet128_320", 2, 128, 128, 320, 320, torch.bfloat16, False),
           ("vae256_512", 1, 256, 256, 512, 512, torch.float16, False),
           ("vae512_256", 1, 512, 512, 256, 256, torch.float16, False),
           ("vae1024_128", 1, 1024, 1024, 128, 128, torch.float16, False),
-          ("vae_up512_512", 1, 256, 256, 512, 512, torch.float16, True)]
+          ("vae_up512_512", 1, 256, 256, 512, 512, torch.float16, True),
+          ("vae_up1024_256", 1, 1024, 1024, 256, 256, torch.float16, True),
+          ("vae1024_256to128", 1, 1024, 1024, 256, 128, torch.float16, False)]
 
 
 def graph_us(fn, reps=20, inner=10):

@@ -195,3 +195,48 @@ def _channel_split(Cin, Cout):
     assert torch.equal(fused, plain)
     if one is not None:
         assert torch.equal(y, one)
+
+
+@pytest.mark.parametrize("case", ["vae1024_like", "cin256_gn_res", "n256_upsample"])
+def test_halo_conv_persistent_form_is_bitwise_the_per_tile_form(case):
+    """The persistent form (FD_CONV_HALO_PT: one workgroup per CU walking 256 x 128 tiles, the next tile's DMA under
+    this tile's epilogue, 32-row epilogue passes) against the one-workgroup-per-tile form: outputs and the epilogue's
+    GroupNorm statistics bitwise equal, with the GroupNorm + SiLU folded into the staging, a residual and fp16 (the
+    VAE decoder's 1024^2 level at a quarter of its pixels), 4 input-channel chunks (a patch DMA issued inside the
+    K loop), and a nearest x2 upsample with 2 output-channel tiles (FD_CONV_HALO_PT = 2 takes it from gemm256).
+    One case against torch fp32 as well."""
+    from fdhip import ops
+    nimg, H, W, Cin, Cout, up, dt = {"vae1024_like": (1, 512, 256, 128, 128, None, torch.float16),
+                                     "cin256_gn_res": (2, 256, 256, 256, 128, None, torch.bfloat16),
+                                     "n256_upsample": (1, 512, 256, 256, 256, (256, 128), torch.float16)}[case]
+    x, w, b = _inputs(nimg, H, W, Cin, Cout, dt, seed=21, up=up)
+    Hi, Wi = up if up else (H, W)
+    g = torch.Generator().manual_seed(22)
+    gamma = (1 + 0.1 * torch.randn(Cin, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(Cin, generator=g)).to(DEV)
+    res = _nhwc(torch.randn(nimg, Cout, H, W, generator=g).to(dt)).to(DEV)
+    wp = ops.pack_conv3x3(w.float()).to(DEV, dt)
+    xs = _nhwc(x).to(DEV)
+    bd = b.float().to(DEV)
+    kw = dict(upsample=True) if up else dict(residual=res)
+    outs = {}
+    for pt in (0, 2):
+        with _knobs(FD_CONV_HALO_PT=pt, FD_CONV_HALO=2):
+            npt = ops.halo_conv_pt(xs, wp, nimg, Hi, Wi, upsample=bool(up), residual=not up)
+            assert (npt > 0) == (pt > 0), npt
+            st = ops.GnStats(nimg, H * W, 32, DEV)
+            if up:
+                y = ops.conv3x3(xs, wp, bd, nimg, Hi, Wi, gn=st, **kw)
+            else:
+                aff = ops.group_norm_affine(xs, gamma, beta, nimg, H * W, Cin, 32, 1e-5)
+                y = ops.conv3x3(xs, wp, bd, nimg, H, W, gn_in=(aff, True), gn=st, **kw)
+            assert st.done and st.rows == 256
+            torch.cuda.synchronize()
+            outs[pt] = (y.clone(), st.part[:nimg * (H * W // 256) * 32 * 2].clone())  # 256-row blocks written
+    assert torch.equal(outs[0][0], outs[2][0])
+    assert torch.equal(outs[0][1], outs[2][1])
+    if case == "vae1024_like":
+        xr = F.silu(F.group_norm(x.float(), 32, gamma.cpu(), beta.cpu(), 1e-5)).to(dt).float()
+        ref = F.conv2d(xr, w.float(), b, padding=1) + _nchw(res.float().cpu(), nimg, H, W)
+        rel = rel_l2(_nchw(outs[2][0].float().cpu(), nimg, H, W), ref)
+        assert rel < 6e-3, rel
