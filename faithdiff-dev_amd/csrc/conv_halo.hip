@@ -46,7 +46,15 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // patches are DMA'd while this tile's outputs are written (the non-PT form waits for its patches at the start of
 // every tile and stores at the end with nothing to overlap either: at the VAE's 1024^2 level that was ~1/3 of the
 // conv).  The per-element K order, the stored values and the GroupNorm partials are bit for bit the non-PT ones.
-template <typename T, int TH, int BN, bool GNI, bool SK, int NS, bool PT>
+//
+// PH (the nearest x2 upsample conv, Upsample2D, in four phases): output pixel (2i + a, 2j + b) of conv3x3(up2(x))
+// reads only source rows i + a - 1 + {0, 1} and columns j + b - 1 + {0, 1}, so each phase (a, b) is a 2 x 2 conv
+// of the LOW-resolution x with weights summed over the taps that land on the same source pixel
+// (pack_conv3x3_up2: [4 * Cout][4 * Cin]) -- 16 taps per 2 x 2 output pixels instead of 36.  The tiles cover the
+// low-resolution grid; the combined N = 4 * Cout is phase-major (an N tile never straddles two phases); a tile's
+// 4 taps read the window at rows a + {0, 1}, columns b + {0, 1} of its (TH + 2) x 18 patch, and its epilogue writes
+// the strided output pixels.  GroupNorm partials: one block per (image, phase, tile) -- 256 output pixels each.
+template <typename T, int TH, int BN, bool GNI, bool SK, int NS, bool PT, bool PH>
 __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, float* __restrict__ slabs,
                                                           unsigned* __restrict__ counters) {
   typedef typename VecT<T>::v8 V8;
@@ -71,6 +79,8 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   constexpr int SMEM_EPI = RED + 512 * 8;
   constexpr int PER = 32;  // PT epilogue pass: 32 rows x BN fp32 + their GroupNorm slots, past the ring
   constexpr int PT_EP = SMEM_MAIN, PT_SLOT = PT_EP + PER * LDE * 4, PT_END = PT_SLOT + PER * VPR * 16;
+  static_assert(!PH || (!GNI && !SK && !PT), "phase form: plain tiles only");
+  constexpr int NTAP = PH ? 4 : 9;
   static_assert(!PT || (!SK && BN == 128 && TH == 16 && PER * VPR == 512 && PT_END <= 163840 &&
                         PER * LDE * 4 >= 512 * 8),
                 "PT layout: one 8-column vector per thread per pass, red[] in the pass buffer");
@@ -83,7 +93,8 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   const int wm = w >> 1, wn = w & 1;
   const int fr = lane & 15, fg = lane >> 4;
   const int Ho = p.Hout, Wo = p.Wout, Cin = p.Cin, N = p.N;
-  const int tiles_x = (Wo + 15) / 16, tiles_y = (Ho + TH - 1) / TH;
+  const int Hg = PH ? p.Hin : Ho, Wg = PH ? p.Win : Wo;  // the tiled (and patch) grid
+  const int tiles_x = (Wg + 15) / 16, tiles_y = (Hg + TH - 1) / TH;
   const int nsp = p.nimg * tiles_y * tiles_x;
   // tile order: XCD-contiguous chunks (bijective remap), output-channel tiles outer, so the ~32 workgroups an XCD
   // runs at once share one weight panel in its L2; SK: the two channel halves of a tile adjacent (same XCD)
@@ -94,7 +105,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   // order and its gx workgroups stride it -- the ~32 tiles an XCD holds at once are neighbours sharing halo rows
   int tl = tlin, tl_hi = tlin + 1, tl_step = 1;
   if constexpr (PT) {
-    const int total = (N / BN) * nsp, xcd = blockIdx.x & 7;
+    const int total = ((PH ? 4 : 1) * N / BN) * nsp, xcd = blockIdx.x & 7;
     tl = (int)((long long)xcd * total / 8) + (blockIdx.x >> 3);
     tl_hi = (int)((long long)(xcd + 1) * total / 8);
     tl_step = gridDim.x >> 3;
@@ -103,10 +114,11 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   // input-channel chunks of this workgroup: all, or (SK) one half of them, combined pairwise after the K loop
   const int nch_all = Cin / 64;
   const int cb = SK && split ? nch_all / 2 : 0, ce = SK && !split ? nch_all / 2 : nch_all;
-  const int nsteps = 9 * (ce - cb);
+  const int nsteps = NTAP * (ce - cb);
   const T* __restrict__ A = (const T*)p.A;
   const T* __restrict__ Bw = (const T*)p.B;
   const bool up2 = p.upsample && Ho == 2 * p.Hin && Wo == 2 * p.Win;
+  const bool ups = !PH && p.upsample;  // nearest resize folded into the patch gather (PH: the patch is low-res)
 
   // ---- per-tile coordinates and DMA sources.  Weight stages (waves 0-3): rows n0 + (w + 4 i) * 8 + lane / 8,
   // source-side XOR swizzle of 128-B rows; patch pixels (waves 4-7): this lane's source 16-B chunk at channel 0,
@@ -114,14 +126,14 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   // (wave-uniform) tile coordinates, which keeps ~30 VGPRs of pointers out of the epilogue, and rows past the patch
   // (j >= P_TOT) re-load row P_TOT - 1 (the same bytes to the same LDS address), so every patch wave issues exactly
   // P_I loads per chunk and the epilogue's counted waits hold
-  int img = 0, spi = 0, y0 = 0, x0 = 0, n0 = 0;
+  int img = 0, spi = 0, y0 = 0, x0 = 0, n0 = 0, nb = 0, pha = 0, phb = 0;  // nb: B row base (PH: phase-major)
   const T* b_row[PT ? 1 : PER_B];
   const T* p_src[PT ? 1 : P_I];
   const float* __restrict__ aff = nullptr;
   auto b_src = [&] __attribute__((always_inline)) (int i) {
     int row = (w + 4 * i) * 8 + (lane >> 3);
     if constexpr (PT) asm volatile("" : "+v"(row));
-    return Bw + (long long)(n0 + row) * p.ldb + (((lane & 7) ^ ((row >> 1) & 7)) * 8);
+    return Bw + (long long)(nb + row) * p.ldb + (((lane & 7) ^ ((row >> 1) & 7)) * 8);
   };
   auto p_row = [&] __attribute__((always_inline)) (int i) { return PT ? min((w - 4) + 4 * i, P_TOT - 1) : (w - 4) + 4 * i; };
   auto p_src_of = [&] __attribute__((always_inline)) (int i) -> const T* {
@@ -130,9 +142,9 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     if constexpr (PT) asm volatile("" : "+v"(pix));  // PT: recomputed at each issue, never hoisted out of the loops
     const int py = pix / PW, px = pix - (pix / PW) * PW;
     const int iy = y0 - 1 + py, ix = x0 - 1 + px;
-    const bool ok = j < P_TOT && pix < PIX && iy >= 0 && iy < Ho && ix >= 0 && ix < Wo;
+    const bool ok = j < P_TOT && pix < PIX && iy >= 0 && iy < Hg && ix >= 0 && ix < Wg;
     int sy = iy, sx = ix;
-    if (p.upsample) {
+    if (ups) {
       sy = up2 ? (iy >> 1) : (iy * p.Hin) / Ho;
       sx = up2 ? (ix >> 1) : (ix * p.Win) / Wo;
     }
@@ -146,7 +158,11 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     const int tyt = spi / tiles_x, txt = spi - tyt * tiles_x;
     y0 = tyt * TH;
     x0 = txt * 16;
-    n0 = nt * BN;
+    nb = nt * BN;
+    const int ph = PH ? nb / N : 0;
+    pha = ph >> 1;
+    phb = ph & 1;
+    n0 = nb - ph * N;
     if constexpr (!PT) {
       if (w < 4) {
 #pragma unroll
@@ -160,7 +176,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   };
 
   auto stage_b = [&] __attribute__((always_inline)) (int s, int rb) {  // s: this workgroup's step (chunk cb + s / 9, tap s % 9)
-    const int c = cb + s / 9, t = s - (s / 9) * 9;
+    const int c = cb + s / NTAP, t = s - (s / NTAP) * NTAP;
     const int off = t * Cin + c * 64;
     unsigned char* dst = smem + RING + rb * STAGE;
 #pragma unroll
@@ -232,7 +248,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   auto read_frags = [&] __attribute__((always_inline)) (int c, int t, int rb, int h, V8 (&af)[MT], V8 (&bf)[NT]) {
     const unsigned char* pa = smem + (c & 1) * PBUF;
     const unsigned char* sb = smem + RING + rb * STAGE;
-    const int ky = t / 3, kx = t - (t / 3) * 3;
+    const int ky = PH ? pha + (t >> 1) : t / 3, kx = PH ? phb + (t & 1) : t - (t / 3) * 3;
     const int ch = h * 4 + fg;
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
@@ -299,19 +315,19 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     mma(a0, b0);
     __builtin_amdgcn_sched_barrier(0);
     if (w < 4) wait_b(min(NS - 2, nsteps - 2 - s));  // stage s + 1 landed
-    else if (t == TR) hvm<0>();                       // chunk c + 1's patch landed
+    else if (t == (PH ? NTAP - 1 : TR)) hvm<0>();     // chunk c + 1's patch landed
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_s_barrier();
     if (w < 4) {
       if (s + NS < nsteps) stage_b(s + NS, rb);
-    } else if (t == 8 && c + 2 < ce) {
+    } else if (t == NTAP - 1 && c + 2 < ce) {
       stage_p(c + 2);  // buffer c & 1: its last reads (this step's half 1) are behind the barrier
     }
     // chunk c + 1's patch: a piece per tap TR .. 7 behind this step's half-1 MFMAs (below); visible to the readers
     // after step (c, 8)'s barrier
-    const int tc = (GNI && t >= TR && t < 8 && c + 1 < ce) ? c + 1 : -1, tp = t - TR;
+    const int tc = (GNI && t >= TR && t < NTAP - 1 && c + 1 < ce) ? c + 1 : -1, tp = t - TR;
     rb = rb == NS - 1 ? 0 : rb + 1;
-    if (t == 8) {
+    if (t == NTAP - 1) {
       ++c;
       t = 0;
     } else {
@@ -538,8 +554,8 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       const int r = e / VPR, cv = e - (e / VPR) * VPR;
       const int rt = half * EROWS + r;
       const int oy = y0 + (rt >> 4), ox = x0 + (rt & 15);
-      const bool ok = oy < Ho && ox < Wo;
-      const long long m = ((long long)img * Ho + oy) * Wo + ox;
+      const bool ok = oy < Hg && ox < Wg;
+      const long long m = PH ? ((long long)img * Ho + 2 * oy + pha) * Wo + 2 * ox + phb : ((long long)img * Ho + oy) * Wo + ox;
       const int n = n0 + cv * 8;
       float v[8], bv[8], rv[8];
       TO8 res;
@@ -615,7 +631,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
         S += v2.x;
         Q += v2.y;
       }
-      const long long blk = (long long)img * (tiles_y * tiles_x) + spi;
+      const long long blk = ((long long)img * (PH ? 4 : 1) + (PH ? pha * 2 + phb : 0)) * (tiles_y * tiles_x) + spi;
       ((float2*)p.gn_part)[blk * p.gn_groups + n0 / cpg + tid] = make_float2(S, Q);
     }
   }
@@ -624,6 +640,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
 struct HaloPlan {
   int th, bn, tiles, sk, ns;  // tiles: output tiles (workgroups = tiles * (1 + sk)); ns: weight ring depth
   int pt;                     // persistent workgroups (PT form), 0 = one workgroup per tile
+  int ph;                     // the phase form of a nearest x2 upsample conv (fd_gemm_params.up_phase)
 };
 
 // Compute units of the current device (cached per device id).
@@ -652,7 +669,39 @@ int halo_pt_grid(const fd_gemm_params* p, int th, int bn, int sk, long long tile
 
 // Eligibility and tile plan, from per-image quantities only (m_ref: rows of one TLC tile's forward), so batching
 // tiles never moves a launch between this kernel and the implicit GEMM (bitwise batch invariance).
+// The phase form (up_phase): always this kernel (no other takes the [4 Cout][4 Cin] weights); tiles over the
+// low-resolution grid, 256-row tiles while there are enough of them, else 128-row.
+int halo_plan_phase(const fd_gemm_params* p, HaloPlan* pl) {
+  if (!p->conv || !p->upsample || p->batch > 1 || p->stride != 1 || p->pad != 1 || p->A2 || p->gi_affine) return 0;
+  if (p->Hout != 2 * p->Hin || p->Wout != 2 * p->Win || p->K != 4 * p->Cin || p->Cin % 64) return 0;
+  if (p->lda < p->Cin || p->lda % 8 || p->ldb % 8 || p->ldc % 8 || p->ldb < 4 * p->Cin) return 0;
+  if (p->act == FD_ACT_GEGLU || p->ln_in || p->ln_out || p->dtype != p->out_dtype || p->dtype == FD_F32) return 0;
+  if ((p->residual && p->ldr % 8) || (p->rowbias && p->rowbias_ld % 4)) return 0;
+  const unsigned long long al = (unsigned long long)p->A | (unsigned long long)p->B | (unsigned long long)p->C |
+                                (unsigned long long)(p->residual ? p->residual : nullptr) |
+                                (unsigned long long)(p->bias ? p->bias : nullptr) |
+                                (unsigned long long)(p->rowbias ? p->rowbias : nullptr);
+  if (al & 15) return 0;
+  const int bn = p->N % 160 == 0 ? 160 : (p->N % 128 == 0 ? 128 : 0);
+  if (!bn || p->Win < 16 || p->Hin < 8) return 0;
+  const long long hw = (long long)p->Hout * p->Wout;
+  const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
+  const long long nimg_ref = m_ref / hw > 0 ? m_ref / hw : 1;
+  const long long t16 = nimg_ref * ((p->Hin + 15) / 16) * ((p->Win + 15) / 16) * (4 * p->N / bn);
+  const int th = (t16 >= fd_knob(FDK_CONV_HALO_MIN_TILES) && p->Hin >= 16) ? 16 : 8;
+  pl->th = th;
+  pl->bn = bn;
+  pl->sk = 0;
+  pl->pt = 0;
+  pl->ns = 3;
+  pl->ph = 1;
+  pl->tiles = (int)(p->nimg * ((p->Hin + th - 1) / th) * ((p->Win + 15) / 16) * (4 * p->N / bn));
+  return 1;
+}
+
 int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
+  if (p->up_phase) return halo_plan_phase(p, pl);
+  pl->ph = 0;
   // FD_CONV_HALO: 0 off; 1 on, except the convs the 256 x 256 kernel takes (the VAE's 256 / 512-channel levels at
   // 256^2 - 512^2 and the upsample convs: its intake beats the 128 / 160-column halo tile there even with the
   // GroupNorm pass, probes/conv_ab.py); 2 on wherever eligible
@@ -705,22 +754,38 @@ int launch_halo(const fd_gemm_params* p, const HaloPlan& pl, hipStream_t s) {
   float* slabs = pl.sk ? (float*)((char*)p->ws + 65536 * sizeof(unsigned)) : nullptr;
   unsigned* cnt = pl.sk ? (unsigned*)p->ws : nullptr;
   const dim3 grid(pl.pt ? pl.pt : pl.tiles * (1 + pl.sk));
+  if (pl.ph) {
+    if (gi || pl.sk || pl.pt || pl.ns != 3) return FD_ERR_ARG;
+#define FD_HALO_PH(TH_, BN_)                                                                                          \
+    if (pl.th == TH_ && pl.bn == BN_) {                                                                              \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, false, 3, false, true>), grid, dim3(512), 0, s, *p,   \
+                         slabs, cnt);                                                                                \
+      FD_LAUNCH_CHECK();                                                                                             \
+      return FD_OK;                                                                                                  \
+    }
+    FD_HALO_PH(16, 160)
+    FD_HALO_PH(16, 128)
+    FD_HALO_PH(8, 160)
+    FD_HALO_PH(8, 128)
+#undef FD_HALO_PH
+    return FD_ERR_ARG;
+  }
   if (pl.pt) {
     if (pl.th != 16 || pl.bn != 128 || pl.sk || pl.ns != 3) return FD_ERR_ARG;
     if (gi)
-      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, true, false, 3, true>), grid, dim3(512), 0, s, *p, slabs, cnt);
+      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, true, false, 3, true, false>), grid, dim3(512), 0, s, *p, slabs, cnt);
     else
-      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, false, false, 3, true>), grid, dim3(512), 0, s, *p, slabs, cnt);
+      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, false, false, 3, true, false>), grid, dim3(512), 0, s, *p, slabs, cnt);
     FD_LAUNCH_CHECK();
     return FD_OK;
   }
 #define FD_HALO(TH_, BN_, SK_, NS_)                                                                                  \
   if (pl.th == TH_ && pl.bn == BN_ && pl.sk == SK_ && pl.ns == NS_) {                                                \
     if (gi)                                                                                                          \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true, SK_, NS_, false>), grid, dim3(512), 0, s, *p, slabs,   \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true, SK_, NS_, false, false>), grid, dim3(512), 0, s, *p, slabs,   \
                          cnt);                                                                                       \
     else                                                                                                             \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, SK_, NS_, false>), grid, dim3(512), 0, s, *p, slabs,  \
+      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, SK_, NS_, false, false>), grid, dim3(512), 0, s, *p, slabs,  \
                          cnt);                                                                                       \
     FD_LAUNCH_CHECK();                                                                                               \
     return FD_OK;                                                                                                    \
@@ -770,7 +835,7 @@ extern "C" long long fd_conv_halo_ws_bytes(const fd_gemm_params* p) {
 // conv with gi_affine set is FD_ERR_SHAPE (callers ask fd_conv_halo_plan first).
 extern "C" int fd_conv_halo_try(fd_gemm_params* p, void* stream) {
   HaloPlan pl;
-  if (!halo_plan(p, &pl)) return p->gi_affine ? FD_ERR_SHAPE : 0;
+  if (!halo_plan(p, &pl)) return (p->gi_affine || p->up_phase) ? FD_ERR_SHAPE : 0;
   if (pl.sk && (!p->ws || p->ws_bytes < 65536LL * (long long)sizeof(unsigned) +
                                           (long long)pl.tiles * slab_bytes(pl.th, pl.bn)))
     return FD_ERR_ARG;
@@ -779,7 +844,8 @@ extern "C" int fd_conv_halo_try(fd_gemm_params* p, void* stream) {
   if (q.gn_part) {
     const int cpg = q.gn_groups > 0 ? q.N / q.gn_groups : 0;
     const bool ok = q.gn_groups > 0 && q.N % q.gn_groups == 0 && cpg >= 4 && pl.bn % cpg == 0 &&
-                    512 % (pl.bn / cpg) == 0 && q.Hout % pl.th == 0 && q.Wout % 16 == 0 &&
+                    512 % (pl.bn / cpg) == 0 && (pl.ph ? q.Hin : q.Hout) % pl.th == 0 &&
+                    (pl.ph ? q.Win : q.Wout) % 16 == 0 &&
                     q.gn_hw == q.Hout * q.Wout && q.M == q.nimg * q.gn_hw;
     if (!ok) q.gn_part = nullptr;
   }

@@ -740,7 +740,8 @@ extern "C" int fd_gemm(fd_gemm_params* p, void* stream) {
   if (p->act == FD_ACT_GEGLU && (p->N % 32) != 0) return FD_ERR_SHAPE;
   if (p->rowbias && p->rows_per_group <= 0) return FD_ERR_ARG;
   if (p->conv) {
-    if (p->Cin % 64 || (p->C1 > 0 && (p->C1 % 64 || !p->A2)) || p->K != 9 * p->Cin) return FD_ERR_SHAPE;
+    if (p->Cin % 64 || (p->C1 > 0 && (p->C1 % 64 || !p->A2)) || p->K != (p->up_phase ? 4 : 9) * p->Cin)
+      return FD_ERR_SHAPE;
     if (p->M != p->nimg * p->Hout * p->Wout) return FD_ERR_SHAPE;
     if (p->stride != 1 && p->stride != 2) return FD_ERR_SHAPE;
     if (p->upsample && (p->stride != 1 || p->pad != 1 || p->Hout < p->Hin || p->Wout < p->Win)) return FD_ERR_SHAPE;

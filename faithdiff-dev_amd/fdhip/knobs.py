@@ -22,6 +22,7 @@ HOST_DEFAULTS = {
     "FD_FP8_MX_ATTN": 1,    # fp8 model: MX e4m3 attention outputs only (the measured-fastest form)
     "FD_FP8_MX_GEGLU": 0,   # fp8 model: MX output straight from the GEGLU epilogue
     "FD_VAE_NARROW": 0,     # VAE conv_out on the direct narrow kernel (measured no faster)
+    "FD_UP2_PHASE": 1,      # Upsample2D convs (VAE decoder, UNet up blocks) as four 2x2 phase convs of the low-res input
     "FD_GRAPHS": 1,         # hipGraph capture / replay of the UNet, VAE and text encoders
     "FD_TILE_BATCH": 13,    # TLC tiles per UNet forward
     "FD_CFG_STREAMS": 0,    # UNet forward split into two concurrent row halves after the extras

@@ -40,6 +40,7 @@ class GemmParams(ctypes.Structure):
         ("batch_inner", c_int), ("strideA_o", c_ll), ("strideB_o", c_ll), ("strideC_o", c_ll),
         ("bsel_rows", c_int), ("bsel_mod", c_int), ("bsel_strideB", c_ll), ("bsel_strideN", c_ll),
         ("sm_group", c_int), ("sm_len", c_int),
+        ("up_phase", c_int),
     ]
 
 

@@ -99,6 +99,31 @@ def pack_conv3x3(w):
     return w.permute(0, 2, 3, 1).reshape(co, kh * kw * ci).contiguous()
 
 
+# taps of a 3x3 kernel on the nearest-x2 upsampled grid that land on source row (col) offset r in {0, 1} of phase a:
+# phase 0 (even output rows): r = 0 <- ky 0, r = 1 <- ky 1, 2; phase 1 (odd): r = 0 <- ky 0, 1, r = 1 <- ky 2
+_UP2_TAPS = (((0,), (1, 2)), ((0, 1), (2,)))
+
+
+def pack_conv3x3_up2(w):
+    """Upsample2D's conv (nearest x2, then 3x3 pad 1) as four 2x2 phase convs of the low-resolution input:
+    [Cout, Cin, 3, 3] -> [4 * Cout, 4 * Cin], row ph * Cout + o (ph = 2a + b: output pixel (2i + a, 2j + b)),
+    column (2 ry + rx) * Cin + c: the sum in fp32 of the taps landing on source pixel (i + a - 1 + ry, j + b - 1 + rx)
+    (fd_gemm_params.up_phase).  Cast to the conv dtype by the caller (one rounding of each summed weight)."""
+    co, ci, _, _ = w.shape
+    w = w.float()
+    out = torch.zeros(4, co, 2, 2, ci, dtype=torch.float32)
+    for a in range(2):
+        for b in range(2):
+            for ry in range(2):
+                for rx in range(2):
+                    acc = torch.zeros(co, ci, dtype=torch.float32)
+                    for ky in _UP2_TAPS[a][ry]:
+                        for kx in _UP2_TAPS[b][rx]:
+                            acc += w[:, :, ky, kx].cpu()
+                    out[2 * a + b, :, ry, rx, :] = acc
+    return out.reshape(4 * co, 4 * ci).contiguous()
+
+
 def pack_geglu(w, b):
     """GEGLU proj [2F, K] -> rows interleaved in groups of 32 = [16 hidden | 16 gate] (fd_gemm GEGLU)."""
     F2, K = w.shape
@@ -516,6 +541,45 @@ def conv3x3(x, wp, bias, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, C
     if gn is not None:
         gn.collect(p)
     return out
+
+
+class _WShape:  # a [Cout, 9 Cin] stand-in for _conv_params (the phase weights are [4 Cout, 4 Cin])
+    def __init__(self, w, cout, cin):
+        self.shape, self._p = (cout, 9 * cin), w.data_ptr()
+
+    def data_ptr(self):
+        return self._p
+
+
+def conv3x3_up2_params(x, wph, bias, nimg, H, W, out=None, residual=None, act="none", gn=None):
+    Cout, Cin = wph.shape[0] // 4, wph.shape[1] // 4
+    p, out = _conv_params(x, _WShape(wph, Cout, Cin), bias, nimg, H, W, 1, 1, True, None, None, out, None, residual,
+                          act, None, None, None, 1.0)
+    p.K, p.ldb, p.up_phase = 4 * Cin, wph.stride(0), 1
+    return p, out
+
+
+def conv3x3_up2(x, wph, bias, nimg, H, W, out=None, residual=None, act="none", gn=None):
+    """Upsample2D (nearest x2 + 3x3 conv) on NHWC x [nimg*H*W, Cin] in four 2x2 phases with the
+    pack_conv3x3_up2 weights wph [4*Cout, 4*Cin] -> [nimg*2H*2W, Cout] (fd_gemm_params.up_phase; the halo-staged
+    kernel; up2_phase_ok() says whether it takes the shape)."""
+    p, out = conv3x3_up2_params(x, wph, bias, nimg, H, W, out, residual, act)
+    if gn is not None:
+        gn.attach(p)
+    _attach_ws(p, x.device)
+    _launch_gemm(p, "fd_gemm(conv up2 phases)")
+    if gn is not None:
+        gn.collect(p)
+    return out
+
+
+def up2_phase_ok(x, wph, nimg, H, W):
+    """True when fd_gemm runs this x2 upsample conv in the phase form (shapes only)."""
+    dummy = torch.empty((1, wph.shape[0] // 4), dtype=x.dtype, device=x.device)
+    p, _ = conv3x3_up2_params(x, wph, None, nimg, H, W, out=dummy)
+    p.C, p.ldc = x.data_ptr(), wph.shape[0] // 4
+    p.M = nimg * 4 * H * W
+    return int(L.load().fd_conv_halo_plan(ctypes.byref(p))) > 0
 
 
 def gn_conv3x3(x, gamma, beta, wp, bias, nimg, H, W, eps, silu=True, groups=32, stats=None, **kw):

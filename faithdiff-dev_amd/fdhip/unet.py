@@ -173,7 +173,8 @@ class HipUNet:
                     blk["attns"].append(t2d(f"up_blocks.{i}.attentions.{j}", co, Lr[lvl]))
             if i < 2:
                 p = f"up_blocks.{i}.upsamplers.0.conv"
-                blk["us"] = (_dev(ops.pack_conv3x3(sd[p + ".weight"]), self.device, dtype), Fp(p + ".bias"))
+                blk["us"] = (_dev(ops.pack_conv3x3(sd[p + ".weight"]), self.device, dtype), Fp(p + ".bias"),
+                             _dev(ops.pack_conv3x3_up2(sd[p + ".weight"]), self.device, dtype))
             self.up.append(blk)
             prev = co
         self.norm_out = (Fp("conv_norm_out.weight"), Fp("conv_norm_out.bias"))
@@ -573,7 +574,11 @@ class HipUNet:
             if blk["us"] is not None:
                 # Upsample2D to the next skip's size (x2, or diffusers' forward_upsample_size path, ext:665-666)
                 th, tw = skips[-1][2], skips[-1][3]
-                h = ops.conv3x3(h, *blk["us"], B, hh, ww, upsample=True, upsample_size=(th, tw))
+                us = blk["us"]
+                if (th, tw) == (2 * hh, 2 * ww) and knobs.get("FD_UP2_PHASE") and ops.up2_phase_ok(h, us[2], B, hh, ww):
+                    h = ops.conv3x3_up2(h, us[2], us[1], B, hh, ww)  # the four 2x2 phase convs (pack_conv3x3_up2)
+                else:
+                    h = ops.conv3x3(h, us[0], us[1], B, hh, ww, upsample=True, upsample_size=(th, tw))
                 hh, ww = th, tw
         h = ops.group_norm(h, *self.norm_out, B, hh * ww, 320, 32, 1e-5, silu=True, stats=self._gn_stats_of(h))
         return ops.conv3x3(h, *self.conv_out, B, hh, ww)

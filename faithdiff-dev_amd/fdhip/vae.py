@@ -169,7 +169,10 @@ class HipDecoder:
         prev = rch[0]
         for i, c in enumerate(rch):
             rs = [t.resnet(f"decoder.up_blocks.{i}.resnets.{j}", prev if j == 0 else c, c) for j in range(3)]
-            us = t.conv(f"decoder.up_blocks.{i}.upsamplers.0.conv") if i < 3 else None
+            us = None
+            if i < 3:  # Upsample2D: the 3x3 form and the four-phase form (ops.pack_conv3x3_up2)
+                k = f"decoder.up_blocks.{i}.upsamplers.0.conv"
+                us = t.conv(k) + (_dev(ops.pack_conv3x3_up2(t.sd[t.prefix + k + ".weight"]), self.device, dtype),)
             self.blocks.append((rs, us))
             prev = c
         self.norm_out = (t.f32("decoder.conv_norm_out.weight"), t.f32("decoder.conv_norm_out.bias"))
@@ -200,7 +203,10 @@ class HipDecoder:
                 x, st = run_resnet(r, x, n, hh, ww, self.dtype, self.device, st)
             if us is not None:
                 st = ops.GnStats(n, 4 * hh * ww, 32, x.device)
-                x = ops.conv3x3(x, *us, n, hh, ww, upsample=True, gn=st)
+                if knobs.get("FD_UP2_PHASE") and ops.up2_phase_ok(x, us[2], n, hh, ww):
+                    x = ops.conv3x3_up2(x, us[2], us[1], n, hh, ww, gn=st)
+                else:
+                    x = ops.conv3x3(x, us[0], us[1], n, hh, ww, upsample=True, gn=st)
                 hh, ww = hh * 2, ww * 2
         x = ops.group_norm(x, *self.norm_out, n, hh * ww, 128, 32, 1e-6, silu=True, stats=st)
         if self.narrow:

@@ -127,6 +127,13 @@ typedef struct fd_gemm_params {
    * become softmax over those values of the epilogue before the activation (LayerNorm fold, bias, alpha), the rest
    * are written as 0.  N % 160 == 0, no residual / row bias / GEGLU, 16-bit output. */
   int sm_group, sm_len;
+  /* up_phase = 1: a nearest x2 upsample conv (upsample = 1, Hout = 2 Hin, Wout = 2 Win) with its weights in the
+   * four-phase form of pack_conv3x3_up2 ([4 * Cout][4 * Cin], B = those, ldb >= 4 Cin, K = 4 Cin): output pixel
+   * (2i + a, 2j + b) = sum over the 2 x 2 source pixels (i + a - 1 + {0, 1}, j + b - 1 + {0, 1}) -- 16 taps per
+   * 2 x 2 output pixels instead of 36, the same function up to the rounding of the summed weights.  Only the
+   * halo-staged kernel runs it (FD_ERR_SHAPE when it cannot: Win < 16, Hin < 8, Cout not a multiple of 128 / 160);
+   * no concat source, no gi_affine; gn_part blocks are (image, phase, 256- or 128-pixel tile). */
+  int up_phase;
 } fd_gemm_params;
 
 int fd_gemm(fd_gemm_params* p, void* stream);  /* writes only p->gn_done */

@@ -240,3 +240,49 @@ def test_halo_conv_persistent_form_is_bitwise_the_per_tile_form(case):
         ref = F.conv2d(xr, w.float(), b, padding=1) + _nchw(res.float().cpu(), nimg, H, W)
         rel = rel_l2(_nchw(outs[2][0].float().cpu(), nimg, H, W), ref)
         assert rel < 6e-3, rel
+
+
+@pytest.mark.parametrize("nimg,H,W,C,Cout,dt", [(1, 64, 64, 512, 512, torch.float16), (1, 32, 48, 256, 256, torch.float16),
+                                                (2, 32, 32, 1280, 1280, torch.bfloat16),
+                                                (2, 64, 64, 640, 640, torch.bfloat16),
+                                                (1, 8, 32, 128, 128, torch.float16),
+                                                (1, 23, 17 + 16, 320, 320, torch.bfloat16)])
+def test_upsample_conv_in_four_phases(nimg, H, W, C, Cout, dt):
+    """Upsample2D in the phase form (fd_gemm_params.up_phase, pack_conv3x3_up2): against torch fp32 nearest x2 +
+    conv3x3 on the same inputs and the original weights (rel-L2 < 6e-3: the summed weights are rounded once to
+    the conv dtype), against the one-workgroup-per-tap upsample conv, bitwise batch invariant (two images in one
+    launch == one launch per image), and its epilogue GroupNorm statistics equal to a pass over the output
+    (fp32 summation order).  VAE decoder levels (fp16, 256 / 512 ch), the UNet's (bf16, 1280 / 640 ch, 2 images),
+    a 128-row tile case (H = 8) and a ragged one (23 x 33)."""
+    from fdhip import ops
+    x, w, b = _inputs(nimg, 2 * H, 2 * W, C, Cout, dt, seed=31, up=(H, W))
+    xs = _nhwc(x).to(DEV)
+    bd = b.float().to(DEV)
+    wph = ops.pack_conv3x3_up2(w.float()).to(DEV, dt)
+    assert ops.up2_phase_ok(xs, wph, nimg, H, W)
+    st = ops.GnStats(nimg, 4 * H * W, 32, DEV)
+    y = ops.conv3x3_up2(xs, wph, bd, nimg, H, W, gn=st)
+    with _knobs(FD_CONV_HALO_MIN_TILES=1):
+        wp = ops.pack_conv3x3(w.float()).to(DEV, dt)
+        y9 = ops.conv3x3(xs, wp, bd, nimg, H, W, upsample=True)
+    one = None
+    if nimg == 2:
+        one = torch.cat([ops.conv3x3_up2(xs[i * H * W:(i + 1) * H * W].contiguous(), wph, bd, 1, H, W)
+                         for i in range(2)])
+    torch.cuda.synchronize()
+    ref = F.conv2d(F.interpolate(x.float(), scale_factor=2, mode="nearest"), w.float(), b, padding=1)
+    rel = rel_l2(_nchw(y.float().cpu(), nimg, 2 * H, 2 * W), ref)
+    assert rel < 6e-3, rel
+    assert rel_l2(y.float().cpu(), y9.float().cpu()) < 6e-3
+    if one is not None:
+        assert torch.equal(y, one)
+    if st.done:
+        g = torch.Generator().manual_seed(32)
+        gamma = (1 + 0.1 * torch.randn(Cout, generator=g)).to(DEV)
+        beta = (0.1 * torch.randn(Cout, generator=g)).to(DEV)
+        a1 = ops.group_norm_affine(y, gamma, beta, nimg, 4 * H * W, Cout, 32, 1e-5, stats=st)
+        a2 = ops.group_norm_affine(y, gamma, beta, nimg, 4 * H * W, Cout, 32, 1e-5)
+        torch.cuda.synchronize()
+        assert rel_l2(a1[:nimg * Cout].cpu(), a2[:nimg * Cout].cpu()) < 1e-5
+    else:
+        assert H % 16 or W % 16  # statistics are written for whole tiles

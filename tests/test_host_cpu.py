@@ -210,3 +210,24 @@ def test_quantize_e4m3_semantics():
     u = UNet2DConditionModel({})
     u.quantize_8bit()
     assert u._fp8
+
+
+def test_upsample_conv_phase_packing_is_the_same_function():
+    """pack_conv3x3_up2: Upsample2D (nearest x2, then conv3x3 pad 1; diffusers Upsample2D, called by the VAE decoder
+    and the UNet up blocks, unet_2d_condition_vae_extension.py:665-666) as four 2x2 convs of the low-resolution
+    input, each phase's weights the fp32 sums of the taps that land on one source pixel -- equal in fp64 to the
+    upsample-then-conv, borders included (odd sizes too)."""
+    import torch.nn.functional as F
+    from fdhip import ops
+    g = torch.Generator().manual_seed(5)
+    for (n, ci, co, H, W) in [(2, 8, 6, 5, 7), (1, 4, 4, 1, 1), (1, 3, 5, 6, 4)]:
+        x = torch.randn(n, ci, H, W, generator=g, dtype=torch.float64)
+        w = torch.randn(co, ci, 3, 3, generator=g, dtype=torch.float64)
+        ref = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), w, padding=1)
+        wph = ops.pack_conv3x3_up2(w).double().reshape(4, co, 2, 2, ci).permute(0, 1, 4, 2, 3)
+        xp = F.pad(x, (1, 1, 1, 1))
+        out = torch.empty_like(ref)
+        for a in range(2):
+            for b in range(2):
+                out[:, :, a::2, b::2] = F.conv2d(xp[:, :, a:a + H + 1, b:b + W + 1], wph[2 * a + b])
+        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
