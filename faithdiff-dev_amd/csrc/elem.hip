@@ -1,6 +1,8 @@
 // Elementwise, layout, direct-conv and denoise-loop kernels (all HBM- or latency-bound).
 #include <math.h>
 
+#include <type_traits>
+
 #include "fd_common.h"
 
 static inline dim3 grid1d(long long n, int per_thread = 1) {
@@ -288,86 +290,172 @@ extern "C" int fd_conv2d_direct(const void* x, const float* w, const float* bias
 }
 
 // ------------------------------------------------------------------------------------------------
-// Narrow 3x3 conv (Cout <= 4, stride 1, pad 1, Cin % 32 == 0): the VAE decoder's conv_out (128 -> 3 at 1024^2),
+// Narrow 3x3 conv (Cout <= 4, stride 1, pad 1, Cin 32 / 64 / 128): the VAE decoder's conv_out (128 -> 3 at 1024^2),
 // which the implicit-GEMM tiles run at 3 of 64 columns while gathering every input element 9 times (285 us,
-// profiles/r03_vae_pmc_kernel_stats.csv).  One workgroup = 64 consecutive output pixels of one row: the 3 x 66-pixel
-// x Cin input halo is staged once in LDS (pixel pitch Cin + 8 elements: lane-consecutive pixels fall on
-// consecutive 16-B bank groups, conflict-free ds_read_b128); wave w sums channels [w Cin/4, (w+1) Cin/4) of the 9
-// taps for the 64 pixels (lane = pixel) against wave-uniform fp32 weights (scalar loads), and the 4 partial sums
-// are added in wave order.  fp32 accumulation; a different summation order than the GEMM path.
-template <typename T, typename TO, int CIN, int NOUT>
-__global__ void __launch_bounds__(256) conv3x3_narrow_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                             const float* __restrict__ bias, TO* __restrict__ y,
-                                                             int nimg, int H, int W) {
-  typedef typename VecT<T>::v8 V8;
-  constexpr int PP = CIN + 8, VPP = CIN / 8, CPW = CIN / 4;  // halo pixel pitch (elements), channels per wave
-  __shared__ __attribute__((aligned(16))) T halo[3 * 66 * PP];
-  __shared__ float red[256 * 4];
-  const int tpr = (W + 63) / 64;
-  const long long rowid = blockIdx.x / tpr;  // img * H + oy
-  const int x0 = (blockIdx.x - (int)(rowid * tpr)) * 64;
-  const int oy = (int)(rowid % H);
-  const long long img = rowid / H;
-  for (int e = threadIdx.x; e < 3 * 66 * VPP; e += 256) {
-    const int v = e % VPP, pp = e / VPP, col = pp % 66, r = pp / 66;
-    const int iy = oy - 1 + r, ix = x0 - 1 + col;
-    V8 val;
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-      val = *(const V8*)(x + ((img * H + iy) * W + ix) * CIN + v * 8);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) val[i] = (T)0.f;
-    }
-    *(V8*)(halo + pp * PP + v * 8) = val;
-  }
-  __syncthreads();
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  // the wave's weights: a wave-uniform base + compile-time offsets -> scalar loads (SGPR operands of the FMAs)
-  const float* __restrict__ wb = w + wv * CPW;
-  float acc[NOUT];
-#pragma unroll
-  for (int n = 0; n < NOUT; ++n) acc[n] = 0.f;
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    const T* hp = halo + ((tap / 3) * 66 + lane + tap % 3) * PP + wv * CPW;
-#pragma unroll
-    for (int cv = 0; cv < CPW; cv += 8) {
-      const V8 xv = *(const V8*)(hp + cv);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float f = (float)xv[i];
-#pragma unroll
-        for (int n = 0; n < NOUT; ++n) acc[n] = __builtin_fmaf(f, wb[n * 9 * CIN + tap * CIN + cv + i], acc[n]);
-      }
-    }
-  }
-#pragma unroll
-  for (int n = 0; n < NOUT; ++n) red[(wv * 64 + lane) * 4 + n] = acc[n];
-  __syncthreads();
-  if (wv == 0 && x0 + lane < W) {
-    TO* yp = y + (rowid * W + x0 + lane) * NOUT;
-#pragma unroll
-    for (int n = 0; n < NOUT; ++n) {
-      const float sum = ((red[lane * 4 + n] + red[(64 + lane) * 4 + n]) + red[(128 + lane) * 4 + n]) +
-                        red[(192 + lane) * 4 + n];
-      yp[n] = (TO)(sum + (bias ? bias[n] : 0.f));
-    }
+// profiles/r03_vae_pmc_kernel_stats.csv), with the decoder's conv_norm_out GroupNorm + SiLU optionally folded in
+// (gi_affine: the (scale, shift) per (image, channel) of fd_group_norm_affine, applied to every staged element
+// exactly as fd_group_norm stores it, zero padding after the transform).
+// One workgroup = a strip of TH output rows x 64 pixels.  Input rows pass through a 4-slot LDS ring (66 pixels x Cin,
+// pixel pitch Cin + 8 elements: lane-consecutive pixels on consecutive 16-B bank groups, conflict-free
+// ds_read_b128): each input row is loaded, transformed and staged once per strip (TH + 2 rows for TH outputs), and
+// row r + 2's global loads are in flight while row r is computed.  Wave w sums channels [w Cin/4, (w+1) Cin/4) of the
+// 9 taps for the 64 pixels (lane = pixel) against wave-uniform fp32 weights (scalar loads); the 4 partial sums are
+// added in wave order.  fp32 accumulation; a different summation order than the GEMM path.  (The round-3 form staged
+// 3 rows per output row in 64-pixel workgroups: every input row loaded 3 times, no overlap, ~0.3 ms at 1024^2.)
+template <typename T>
+__device__ __forceinline__ float dot2_acc(unsigned a, unsigned b, float c) {
+  if constexpr (std::is_same<T, f16>::value) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, a), __builtin_bit_cast(h2, b), c, false);
+  } else {
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2, a), __builtin_bit_cast(b2, b), c, false);
   }
 }
 
-extern "C" int fd_conv3x3_narrow(const void* x, const float* w, const float* bias, void* y, int nimg, int H, int W,
-                                 int Cin, int Cout, int dtype, int out_dtype, void* stream) {
+template <typename T, typename TO, int CIN, int NOUT, int TH>
+__global__ void __launch_bounds__(256, 2) conv3x3_narrow_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                                const float* __restrict__ bias,
+                                                                const float* __restrict__ aff, int silu,
+                                                                TO* __restrict__ y, int nimg, int H, int W) {
+  typedef typename VecT<T>::v8 V8;
+  typedef __attribute__((ext_vector_type(4))) unsigned U4;
+  constexpr int PP = CIN + 8, VPP = CIN / 8, CPW = CIN / 4;  // pixel pitch (elements), vectors per pixel, ch per wave
+  constexpr int RW = 66, ROW = RW * PP, NV = RW * VPP, VPT = (NV + 255) / 256;
+  // weights as 16-bit pairs, [tap][8-channel vector][out][4 pairs]: one broadcast ds_read_b128 per (vector, out)
+  constexpr int WV = 9 * VPP * NOUT;  // 16-B weight vectors
+  __shared__ __attribute__((aligned(16))) T ring[3 * ROW];
+  __shared__ __attribute__((aligned(16))) U4 wsh[WV];
+  __shared__ float red[256 * 4];
+  __shared__ __attribute__((aligned(16))) float aff_s[CIN * 2];
+  const int tid = threadIdx.x;
+  const int tpr = (W + 63) / 64, tpc = (H + TH - 1) / TH;
+  int bid = blockIdx.x;
+  const int tx = bid % tpr;
+  bid /= tpr;
+  const int ty = bid % tpc;
+  const long long img = bid / tpc;
+  const int x0 = tx * 64, y0 = ty * TH, y1 = min(y0 + TH, H);
+  if (aff && tid < CIN * 2 / 4) *(f32x4*)(aff_s + tid * 4) = *(const f32x4*)(aff + img * CIN * 2 + tid * 4);
+  for (int e = tid; e < WV; e += 256) {  // e = (tap * VPP + v) * NOUT + n
+    const int n = e % NOUT, tv = e / NOUT, v = tv % VPP, tap = tv / VPP;
+    const float* src = w + (long long)n * 9 * CIN + tap * CIN + v * 8;
+    V8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (T)src[i];
+    wsh[e] = __builtin_bit_cast(U4, h);
+  }
+  // two register sets of staged-row loads: row oy + 3's global loads go out while row oy + 2's (issued one row
+  // earlier, so they had a row of compute to land) are transformed into the ring
+  V8 ldA[VPT], ldB[VPT];
+  unsigned okA = 0, okB = 0;  // bit k: vector k of this thread lies inside the image
+  auto load_row = [&] __attribute__((always_inline)) (int iy, V8 (&ld)[VPT], unsigned& okm) {
+    okm = 0;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int e = tid + k * 256;
+      const int v = e % VPP, col = e / VPP, ix = x0 - 1 + col;
+      if (e < NV && iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        ld[k] = *(const V8*)(x + ((img * H + iy) * W + ix) * CIN + v * 8);
+        okm |= 1u << k;
+      }
+    }
+  };
+  auto store_row = [&] __attribute__((always_inline)) (int slot, const V8 (&ld)[VPT], unsigned okm) {
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int e = tid + k * 256;
+      if (e < NV) {
+        const int v = e % VPP, col = e / VPP;
+        const bool ok = (okm >> k) & 1;
+        typedef __attribute__((ext_vector_type(4))) unsigned U4;
+        U4 bits = ok ? __builtin_bit_cast(U4, ld[k]) : (U4){0u, 0u, 0u, 0u};  // zero padding: raw bits, no fp round trip
+        if (aff) {
+          V8 val;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            float f = __builtin_fmaf((float)ld[k][i], aff_s[(v * 8 + i) * 2], aff_s[(v * 8 + i) * 2 + 1]);
+            if (silu) f = silu_f(f);
+            val[i] = (T)f;
+          }
+          bits = ok ? __builtin_bit_cast(U4, val) : (U4){0u, 0u, 0u, 0u};
+        }
+        *(U4*)(ring + slot * ROW + col * PP + v * 8) = bits;
+      }
+    }
+  };
+  __syncthreads();  // aff_s, wsh
+  for (int r = 0; r < 3; ++r) {
+    load_row(y0 - 1 + r, ldA, okA);
+    store_row(r, ldA, okA);
+  }
+  if (y0 + 1 < y1) load_row(y0 + 2, ldA, okA);  // input row of output row y0 + 1
+  __syncthreads();
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const U4* wq = wsh + wv * (CPW / 8) * NOUT;  // this wave's channel vectors start at v = wv * CPW / 8
+  auto row = [&] __attribute__((always_inline)) (int oy, V8 (&cur)[VPT], unsigned& okc, V8 (&nxt)[VPT],
+                                                   unsigned& okn) {
+    const int r = oy - y0;
+    const bool more = oy + 1 < y1;  // output row oy + 1 needs input row oy + 2 (in cur since one row ago)
+    if (oy + 2 < y1) load_row(oy + 3, nxt, okn);
+    float acc[NOUT];
+#pragma unroll
+    for (int n = 0; n < NOUT; ++n) acc[n] = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int sl = r + ky >= 3 ? (r + ky) % 3 : r + ky;
+      const T* rp = ring + sl * ROW + lane * PP + wv * CPW;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+#pragma unroll
+        for (int cv = 0; cv < CPW / 8; ++cv) {
+          const U4 xv = __builtin_bit_cast(U4, *(const V8*)(rp + kx * PP + cv * 8));
+#pragma unroll
+          for (int n = 0; n < NOUT; ++n) {
+            const U4 wn = wq[((ky * 3 + kx) * VPP + cv) * NOUT + n];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[n] = dot2_acc<T>(xv[j], wn[j], acc[n]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NOUT; ++n) red[(wv * 64 + lane) * 4 + n] = acc[n];
+    __syncthreads();  // red[] written; every wave done reading the slot of input row oy - 1
+    if (more) store_row(r % 3, cur, okc);  // input row oy + 2 = (y0 - 1) + r + 3: the slot of row oy - 1
+    if (wv == 0 && x0 + lane < W) {
+      TO* yp = y + ((img * H + oy) * W + x0 + lane) * NOUT;
+#pragma unroll
+      for (int n = 0; n < NOUT; ++n) {
+        const float sum = ((red[lane * 4 + n] + red[(64 + lane) * 4 + n]) + red[(128 + lane) * 4 + n]) +
+                          red[(192 + lane) * 4 + n];
+        yp[n] = (TO)(sum + (bias ? bias[n] : 0.f));
+      }
+    }
+    __syncthreads();  // red[] read; the new slot visible
+  };
+  for (int oy = y0; oy < y1; oy += 2) {
+    row(oy, ldA, okA, ldB, okB);
+    if (oy + 1 < y1) row(oy + 1, ldB, okB, ldA, okA);
+  }
+}
+
+static int conv3x3_narrow(const void* x, const float* w, const float* bias, const float* aff, int silu, void* y,
+                          int nimg, int H, int W, int Cin, int Cout, int dtype, int out_dtype, void* stream) {
   if (!x || !w || !y) return FD_ERR_ARG;
   if (nimg <= 0 || H <= 0 || W <= 0) return FD_ERR_SHAPE;
   if (((unsigned long long)x) & 15) return FD_ERR_ARG;  // 16-B vector loads of the input rows
-  const long long nblk = (long long)nimg * H * ((W + 63) / 64);
+  if (aff && (((unsigned long long)aff) & 15)) return FD_ERR_ARG;
+  constexpr int TH = 16;
+  const long long nblk = (long long)nimg * ((H + TH - 1) / TH) * ((W + 63) / 64);
   if (nblk > 0x7fffffff) return FD_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   dim3 g((unsigned)nblk), b(256);
   // instances: Cin 32 / 64 / 128 (the decoder's conv_out is 128 -> 3), Cout 1..4
-#define FD_NARROW(CI, NO)                                                                                          \
-  FD_DISPATCH_T(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv3x3_narrow_kernel<T, TO, CI, NO>), g, b, 0, s, \
-                                                                   (const T*)x, w, bias, (TO*)y, nimg, H, W)))
+#define FD_NARROW(CI, NO)                                                                                         \
+  FD_DISPATCH_T(dtype, FD_DISPATCH_O(out_dtype, hipLaunchKernelGGL((conv3x3_narrow_kernel<T, TO, CI, NO, TH>), g, b, \
+                                                                   0, s, (const T*)x, w, bias, aff, silu, (TO*)y,    \
+                                                                   nimg, H, W)))
 #define FD_NARROW_N(CI)                  \
   switch (Cout) {                        \
     case 1: FD_NARROW(CI, 1); break;     \
@@ -389,6 +477,18 @@ extern "C" int fd_conv3x3_narrow(const void* x, const float* w, const float* bia
 #undef FD_NARROW
   FD_LAUNCH_CHECK();
   return FD_OK;
+}
+
+extern "C" int fd_conv3x3_narrow(const void* x, const float* w, const float* bias, void* y, int nimg, int H, int W,
+                                 int Cin, int Cout, int dtype, int out_dtype, void* stream) {
+  return conv3x3_narrow(x, w, bias, nullptr, 0, y, nimg, H, W, Cin, Cout, dtype, out_dtype, stream);
+}
+
+extern "C" int fd_conv3x3_narrow_gn(const void* x, const float* w, const float* bias, const float* gi_affine,
+                                    int gi_silu, void* y, int nimg, int H, int W, int Cin, int Cout, int dtype,
+                                    int out_dtype, void* stream) {
+  if (!gi_affine) return FD_ERR_ARG;
+  return conv3x3_narrow(x, w, bias, gi_affine, gi_silu, y, nimg, H, W, Cin, Cout, dtype, out_dtype, stream);
 }
 
 // ------------------------------------------------------------------------------------------------

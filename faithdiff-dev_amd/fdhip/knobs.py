@@ -21,7 +21,7 @@ HOST_DEFAULTS = {
     "FD_FP8_MX": 0,         # fp8 model: MX e4m3 activations everywhere
     "FD_FP8_MX_ATTN": 1,    # fp8 model: MX e4m3 attention outputs only (the measured-fastest form)
     "FD_FP8_MX_GEGLU": 0,   # fp8 model: MX output straight from the GEGLU epilogue
-    "FD_VAE_NARROW": 0,     # VAE conv_out on the direct narrow kernel (measured no faster)
+    "FD_VAE_NARROW": 1,     # VAE conv_norm_out + SiLU + conv_out in the narrow strip kernel (fd_conv3x3_narrow_gn)
     "FD_UP2_PHASE": 1,      # Upsample2D convs (VAE decoder, UNet up blocks) as four 2x2 phase convs of the low-res input
     "FD_GRAPHS": 1,         # hipGraph capture / replay of the UNet, VAE and text encoders
     "FD_TILE_BATCH": 13,    # TLC tiles per UNet forward

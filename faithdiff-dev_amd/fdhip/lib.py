@@ -73,6 +73,8 @@ _SIGS = {
                               c_int, c_int, c_int, c_int, c_f, c_int, c_vp]),
     "fd_embed_tokens": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "fd_conv3x3_narrow": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
+    "fd_conv3x3_narrow_gn": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_int, c_vp]),
     "fd_flash_attn_d512": (c_int, [c_vp, c_vp, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_int, c_int, c_f, c_int, c_vp]),
     "fd_mha_seq_axis": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "fd_softmax_rows": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_f, c_int, c_vp]),

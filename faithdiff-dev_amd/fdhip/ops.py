@@ -623,18 +623,26 @@ def halo_conv_pt(x, wp, nimg, H, W, upsample=False, upsample_size=None, residual
     return int(L.load().fd_conv_halo_pt(ctypes.byref(p)))
 
 
-def conv3x3_narrow(x, w32, bias, nimg, H, W, out_dtype=None, out=None):
+def conv3x3_narrow(x, w32, bias, nimg, H, W, out_dtype=None, out=None, gn_in=None):
     """3x3 conv (stride 1, pad 1) with Cout <= 4 on NHWC x [nimg*H*W, Cin]: w32 fp32 [Cout, 9*Cin] (tap-major, the
-    pack_conv3x3 layout).  The VAE decoder's conv_out."""
+    pack_conv3x3 layout).  The VAE decoder's conv_out.  gn_in = (affine, silu): the GroupNorm (+ SiLU) in front of
+    it applied to the staged input (affine from group_norm_affine; fd_conv3x3_narrow_gn)."""
     Cout, K = w32.shape
     Cin = K // 9
     odt = out_dtype or x.dtype
     if out is None:
         out = torch.empty((nimg * H * W, Cout), dtype=odt, device=x.device)
+    if gn_in is None:
+        fn = lambda: L.check(L.load().fd_conv3x3_narrow(L.ptr(x), L.ptr(w32), L.ptr(bias), L.ptr(out), nimg, H, W, Cin,
+                                                        Cout, L.dtype_code(x.dtype), L.dtype_code(odt), L.stream()),
+                             "fd_conv3x3_narrow")
+    else:
+        aff, silu = gn_in
+        fn = lambda: L.check(L.load().fd_conv3x3_narrow_gn(L.ptr(x), L.ptr(w32), L.ptr(bias), L.ptr(aff), int(silu),
+                                                           L.ptr(out), nimg, H, W, Cin, Cout, L.dtype_code(x.dtype),
+                                                           L.dtype_code(odt), L.stream()), "fd_conv3x3_narrow_gn")
     _timed("conv_narrow", 2.0 * nimg * H * W * Cout * K, 0.0, label=f"conv3x3_narrow M={nimg * H * W} N={Cout} K={K}",
-           launch=lambda: L.check(L.load().fd_conv3x3_narrow(L.ptr(x), L.ptr(w32), L.ptr(bias), L.ptr(out), nimg, H,
-                                                             W, Cin, Cout, L.dtype_code(x.dtype), L.dtype_code(odt),
-                                                             L.stream()), "fd_conv3x3_narrow"))
+           launch=fn)
     return out
 
 

@@ -177,11 +177,8 @@ class HipDecoder:
             prev = c
         self.norm_out = (t.f32("decoder.conv_norm_out.weight"), t.f32("decoder.conv_norm_out.bias"))
         self.conv_out = t.conv("decoder.conv_out")
-        # conv_out (128 -> 3) on the direct narrow-N kernel (fd_conv3x3_narrow, fp32 weights) with FD_VAE_NARROW=1;
-        # by default the implicit-GEMM path: on one box the decode measured 15.28 / 15.30 ms narrow vs 15.24 / 15.26 ms
-        # GEMM (profiles/r03_vae_narrow_ab.txt) -- the direct kernel reads the input once but at two workgroups per
-        # CU it is latency-bound at the same ~0.3 ms
-        self.narrow = knobs.get("FD_VAE_NARROW") == 1
+        # conv_out (128 -> 3): FD_VAE_NARROW=1 runs it on the direct narrow-N kernel (fd_conv3x3_narrow_gn, fp32
+        # weights, 16-row strips) with conv_norm_out + SiLU applied in its staging; 0: GroupNorm pass + implicit GEMM
         self.conv_out32 = (ops.pack_conv3x3(t.sd[t.prefix + "decoder.conv_out.weight"]).float().to(self.device),
                            self.conv_out[1])
         self.graphs = GraphCache()
@@ -208,7 +205,8 @@ class HipDecoder:
                 else:
                     x = ops.conv3x3(x, us[0], us[1], n, hh, ww, upsample=True, gn=st)
                 hh, ww = hh * 2, ww * 2
+        if knobs.get("FD_VAE_NARROW"):  # conv_norm_out + SiLU folded into the narrow conv_out's staging
+            aff = ops.group_norm_affine(x, *self.norm_out, n, hh * ww, 128, 32, 1e-6, stats=st)
+            return ops.conv3x3_narrow(x, *self.conv_out32, n, hh, ww, gn_in=(aff, True))
         x = ops.group_norm(x, *self.norm_out, n, hh * ww, 128, 32, 1e-6, silu=True, stats=st)
-        if self.narrow:
-            return ops.conv3x3_narrow(x, *self.conv_out32, n, hh, ww)
         return ops.conv3x3(x, *self.conv_out, n, hh, ww)

@@ -164,6 +164,12 @@ int fd_conv2d_direct(const void* x, const float* w, const float* bias, void* y, 
  * Replaces: cuDNN conv2d of decoder.conv_out (diffusers Decoder; pipeline_FaithDiff_tlc.py:1438). */
 int fd_conv3x3_narrow(const void* x, const float* w, const float* bias, void* y, int nimg, int H, int W, int Cin,
                       int Cout, int dtype, int out_dtype, void* stream);
+/* The same conv of GroupNorm(+SiLU)(x): gi_affine fp32 (scale, shift) per (image, channel) [nimg][Cin][2] from
+ * fd_group_norm_affine (16-B aligned), applied to every staged input element exactly as fd_group_norm would store it
+ * (zero padding after the transform) -- the decoder's conv_norm_out + SiLU + conv_out without the normalised
+ * tensor.  Replaces: GroupNorm, SiLU and conv_out of the diffusers Decoder (pipeline_FaithDiff_tlc.py:1438). */
+int fd_conv3x3_narrow_gn(const void* x, const float* w, const float* bias, const float* gi_affine, int gi_silu,
+                         void* y, int nimg, int H, int W, int Cin, int Cout, int dtype, int out_dtype, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * GroupNorm over NHWC x[nimg][HW][C] (32 groups typical), fp32 statistics, optional fused SiLU.

@@ -167,6 +167,17 @@ def test_conv3x3_narrow(dtype, nimg, H, W, Cin, Cout):
     if Cin % 64 == 0:  # the implicit-GEMM conv needs Cin % 64 == 0
         gemm = ops.conv3x3(x, ops.pack_conv3x3(w.to(dtype)), b, nimg, H, W)
         assert rel_l2(out, gemm) < 2 * TOL[dtype]
+    # the decoder's conv_norm_out + SiLU folded into the staging (fd_conv3x3_narrow_gn): bitwise the same conv of
+    # fd_group_norm's stored output (the staged values are those bits, the summation order is unchanged)
+    if Cin >= 32:
+        gamma = 1 + 0.1 * torch.randn(Cin, device=DEV)
+        beta = 0.1 * torch.randn(Cin, device=DEV)
+        aff = ops.group_norm_affine(x, gamma, beta, nimg, H * W, Cin, 32, 1e-6)
+        fused = ops.conv3x3_narrow(x, ops.pack_conv3x3(w).float(), b, nimg, H, W, gn_in=(aff, True))
+        hn = ops.group_norm(x, gamma, beta, nimg, H * W, Cin, 32, 1e-6, silu=True)
+        plain = ops.conv3x3_narrow(hn, ops.pack_conv3x3(w).float(), b, nimg, H, W)
+        torch.cuda.synchronize()
+        assert torch.equal(fused, plain)
 
 
 def test_conv3x3_concat_temb_residual():
