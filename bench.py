@@ -477,7 +477,8 @@ def roofline_leg(loop, fp8):
         a_tf = fl_a / (ms_a / 1e3) / 1e12
         res["attention"] = {"bound": "mfma", "achieved": round(a_tf, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                             "frac": round(a_tf / PEAK_BF16_TFLOPS, 4), "launches": n_a, "ms_per_forward": round(ms_a, 3),
-                            "kernel": "flash_attn_d64_kernel (140 self/cross attentions per forward)"}
+                            "kernel": f"flash_attn_d64_kernel ({n_a} attentions per forward; with the default two-GEMM "
+                                      "cross-attention (GEMM family) these are the self-attentions)"}
     if "gemm_e4m3" in fam:
         n_f, fl_f, _, ms_f = fam["gemm_e4m3"]
         f8_tf = fl_f / (ms_f / 1e3) / 1e12
