@@ -54,7 +54,6 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_CONV_HALO_PT", 0},        // halo conv persistent over tiles (next tile's DMA under the epilogue) for launches of
                                    // >= 2 tiles per CU; 2: also the gemm256-eligible ones; 0: off
     {"FD_CONV_HALO_NS16", 3},      // weight-ring depth of its 256 x 128 tiles (3 or 4)
-    {"FD_GN_FIN", 0},              // GroupNorm finalize folded into the apply blocks (<= 64 chunks; +0.1 ms/step, r04y)
 };
 int g_knobs[FDK_COUNT];
 bool g_init = false;

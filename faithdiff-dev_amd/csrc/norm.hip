@@ -267,24 +267,15 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
 // (t % VPR, the block's first (256 / VPR) * VPR threads): its 8 scales and shifts live in registers, built straight
 // from the group statistics -- no LDS tables, no barrier, no per-vector 64-bit modulo -- and U rows' vectors are
 // in flight per thread.  Same arithmetic per element as gn_apply_kernel (bitwise equal output).
-//
-// FIN (nchunks <= 64 partials, the UNet's GroupNorms): gn_finalize_kernel folded into every block -- wave w folds groups
-// w, w + 4, ... of its image, lane j holding chunk j (all of the wave's loads in flight at once), the same fp64
-// butterfly and (mean, rstd) formula, so the statistics are the same bits; block 0 of each image also stores them to
-// `stats`.  One ~5 us latency-bound launch per GroupNorm fewer.
-template <typename T, int U, bool FIN = false>
+template <typename T, int U>
 __global__ void __launch_bounds__(256) gn_apply2_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                         const float2* __restrict__ stats, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int HW, int C, int groups,
-                                                        int rows_per_block, int silu,
-                                                        const float2* __restrict__ part = nullptr, int nchunks = 0,
-                                                        float eps = 0.f) {
+                                                        int rows_per_block, int silu) {
   typedef typename VecT<T>::v8 V8;
-  __shared__ float2 st_s[FIN ? 64 : 1];
   const int img = blockIdx.y, t = threadIdx.x;
   const int VPR = C / 8, RPP = 256 / VPR;  // chunks per row, rows per pass
-  const bool active = t < RPP * VPR;
-  if (!FIN && !active) return;
+  if (t >= RPP * VPR) return;
   const int v = t % VPR, r0 = t / VPR;
   const int cpg = C / groups;
   const int rb = blockIdx.x * rows_per_block, re = min(rb + rows_per_block, HW);
@@ -295,45 +286,13 @@ __global__ void __launch_bounds__(256) gn_apply2_kernel(const T* __restrict__ x,
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int r = rb + r0 + u * RPP;
-    if (active && r < re) val[u] = *(const V8*)(xb + (long long)r * C);
-  }
-  if constexpr (FIN) {
-    const int wv = t >> 6, lane = t & 63;
-    const float2* pimg = part + (long long)img * nchunks * groups;
-    constexpr int GPW = 16;  // groups <= 64 over 4 waves
-    float2 pv[GPW];
-#pragma unroll
-    for (int k = 0; k < GPW; ++k) {
-      const int g = wv + 4 * k;
-      pv[k] = (g < groups && lane < nchunks) ? pimg[(long long)lane * groups + g] : make_float2(0.f, 0.f);
-    }
-#pragma unroll
-    for (int k = 0; k < GPW; ++k) {
-      const int g = wv + 4 * k;
-      if (g >= groups) break;
-      double sd = (double)pv[k].x, qd = (double)pv[k].y;
-      for (int o = 32; o > 0; o >>= 1) {
-        sd += __shfl_xor(sd, o, 64);
-        qd += __shfl_xor(qd, o, 64);
-      }
-      if (lane == 0) {
-        const double n = (double)HW * cpg;
-        const double mean = sd / n;
-        double var = qd / n - mean * mean;
-        if (var < 0) var = 0;
-        const float2 r = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
-        st_s[g] = r;
-        if (blockIdx.x == 0) ((float2*)stats)[img * groups + g] = r;
-      }
-    }
-    __syncthreads();
-    if (!active) return;
+    if (r < re) val[u] = *(const V8*)(xb + (long long)r * C);
   }
   float sc[8], sh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int c = v * 8 + i, g = c / cpg;
-    const float2 st = FIN ? st_s[g] : stats[img * groups + g];
+    const float2 st = stats[img * groups + g];
     const float a = st.y * (gamma ? gamma[c] : 1.f);
     sc[i] = a;
     sh[i] = __builtin_fmaf(-st.x, a, beta ? beta[c] : 0.f);
@@ -368,32 +327,14 @@ static int gn_apply_version() {
   return v;
 }
 
-// the apply launch shared by fd_group_norm and fd_group_norm_partials (grid: ~1024 blocks of whole rows).
-// part != nullptr: the finalize of those nchunks partials runs inside the apply blocks (gn_apply2 FIN form) when
-// it can (nchunks <= 64, the register-scale kernel); returns 0 when it cannot (the caller finalizes first).
+// the apply launch shared by fd_group_norm and fd_group_norm_partials (grid: ~1024 blocks of whole rows)
 static int gn_apply_launch(const void* x, void* y, const float2* stats, const float* gamma, const float* beta, int nimg,
-                           int HW, int C, int groups, int silu, int dtype, hipStream_t s,
-                           const float2* part = nullptr, int nchunks = 0, float eps = 0.f) {
+                           int HW, int C, int groups, int silu, int dtype, hipStream_t s) {
   const int apply_blocks = fd_knob(FDK_GN_APPLY_BLOCKS);
   const int apply_u = fd_knob(FDK_GN_APPLY_U);  // vectors in flight per thread (4 or 8)
   int rpb = 1;
   while ((long long)nimg * ((HW + rpb - 1) / rpb) > apply_blocks) rpb *= 2;
   const int nblk = (HW + rpb - 1) / rpb;
-  if (part) {
-    if (!(gn_apply_version() == 2 && C / 8 <= 256 && nchunks <= 64 && groups <= 64 && fd_knob(FDK_GN_FIN)))
-      return 0;
-    if (apply_u == 8) {
-      FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply2_kernel<T, 8, true>), dim3(nblk, nimg), dim3(256), 0, s,
-                                              (const T*)x, (T*)y, stats, gamma, beta, HW, C, groups, rpb, silu, part,
-                                              nchunks, eps));
-    } else {
-      FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply2_kernel<T, 4, true>), dim3(nblk, nimg), dim3(256), 0, s,
-                                              (const T*)x, (T*)y, stats, gamma, beta, HW, C, groups, rpb, silu, part,
-                                              nchunks, eps));
-    }
-    FD_LAUNCH_CHECK();
-    return 1;
-  }
   if (gn_apply_version() == 2 && C / 8 <= 256) {
     if (apply_u == 8) {
       FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_apply2_kernel<T, 8>), dim3(nblk, nimg), dim3(256), 0, s,
@@ -439,10 +380,6 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
   }
   FD_LAUNCH_CHECK();
   float2* stats = (float2*)ws + (long long)nimg * nch * groups;
-  const int fin = gn_apply_launch(x, y, stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s, (const float2*)ws, nch,
-                                  eps);
-  if (fin < 0) return fin;
-  if (fin == 1) return FD_OK;
   gn_finalize_launch((const float2*)ws, stats, nimg, HW, C, groups, nch, eps, s);
   FD_LAUNCH_CHECK();
   return gn_apply_launch(x, y, stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s);
@@ -460,10 +397,6 @@ extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma
       C > GN_MAXC)
     return FD_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
-  const int fin = gn_apply_launch(x, y, (const float2*)stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s,
-                                  (const float2*)part, HW / part_rows, eps);
-  if (fin < 0) return fin;
-  if (fin == 1) return FD_OK;
   gn_finalize_launch((const float2*)part, (float2*)stats, nimg, HW, C, groups, HW / part_rows, eps, s);
   FD_LAUNCH_CHECK();
   return gn_apply_launch(x, y, (const float2*)stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s);

@@ -233,31 +233,6 @@ def test_group_norm_deterministic():
     assert torch.equal(a1, a2)
 
 
-@pytest.mark.parametrize("nimg,HW,C,part_rows", [(2, 16384, 320, 256), (2, 4096, 640, 256), (2, 1024, 1280, 128),
-                                                 (2, 1024, 2560, 0), (1, 100, 256, 0), (2, 4096, 960, 0)])
-def test_group_norm_finalize_in_apply_is_bitwise(nimg, HW, C, part_rows):
-    """FD_GN_FIN: the GroupNorm finalize folded into the apply blocks (<= 64 partial chunks) gives the same bits as
-    the separate finalize launch -- from its own statistics pass (part_rows 0) and from producer partials
-    (fd_group_norm_partials; partials made by a statistics pass over row blocks of part_rows)."""
-    from fdhip import knobs, ops
-    x = (torch.randn(nimg * HW, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
-    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
-    outs = []
-    for fin in (0, 1):
-        with knobs.override(FD_GN_FIN=fin):
-            if part_rows:
-                st = ops.GnStats(nimg, HW, 32, DEV)
-                xr = x.float().view(nimg, HW // part_rows, part_rows, 32, C // 32)
-                ps = torch.stack([xr.sum((2, 4)), (xr * xr).sum((2, 4))], -1)  # [nimg, blocks, groups, 2]
-                st.part[:ps.numel()] = ps.reshape(-1)
-                st.done, st.rows = True, part_rows
-                outs.append(ops.group_norm(x, g, b, nimg, HW, C, 32, 1e-5, silu=True, stats=st))
-            else:
-                outs.append(ops.group_norm(x, g, b, nimg, HW, C, 32, 1e-5, silu=True))
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
-
-
 @pytest.mark.parametrize("C", [640, 1280])
 def test_layer_norm(C):
     from fdhip import ops
