@@ -565,7 +565,10 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
         *(f32x4*)&bv[0] = *(const f32x4*)(bias + n);
         *(f32x4*)&bv[4] = *(const f32x4*)(bias + n + 4);
       }
-      if (rbias) {
+      // rows outside the image (ragged tiles) are never stored and must not read either: past the last image
+      // m / rows_per_group indexes a row-bias row that does not exist (an out-of-bounds read that faulted when the
+      // allocator placed the time-embedding buffer at the end of a mapping)
+      if (rbias && ok) {
         const float* rr = rbias + (long long)(m / p.rows_per_group) * p.rowbias_ld + n;
         *(f32x4*)&rv[0] = *(const f32x4*)rr;
         *(f32x4*)&rv[4] = *(const f32x4*)(rr + 4);
@@ -575,7 +578,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] += bv[i];
       }
-      if (rbias) {
+      if (rbias && ok) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] += rv[i];
       }

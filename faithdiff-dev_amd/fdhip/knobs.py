@@ -15,6 +15,7 @@ from . import lib as L
 # host-side path switches (fdhip / FaithDiff modules), name -> default
 HOST_DEFAULTS = {
     "FD_LN_FOLD": 1,        # LayerNorms folded into the transformer GEMM pairs (0: separate LayerNorm launches)
+    "FD_ITL_FOLD": 1,       # ... and into the information transformer's in_proj / c_fc (with FD_LN_FOLD)
     "FD_UNET_GN_EPI": 1,    # UNet GroupNorm statistics from the producing GEMM / conv epilogue
     "FD_SIDE_STREAM": 0,    # time / add embeddings on a second stream inside the UNet graph (measured slower)
     "FD_FP8_MFMA": 0,       # use_fp8 model on the e4m3 MFMA (quantize_8bit(fp8_mfma=...) / FaithDiff_pipeline arg)

@@ -201,6 +201,9 @@ class HipUNet:
                     ln2=(Fp(p + ".ln_2.weight"), Fp(p + ".ln_2.bias")),
                     fc=(W(p + ".mlp.c_fc.weight"), Fp(p + ".mlp.c_fc.bias")),
                     proj=(W(p + ".mlp.c_proj.weight"), Fp(p + ".mlp.c_proj.bias"))))
+                if self.ln_fold:  # ln_1 / ln_2 folded into in_proj / c_fc (partials from out_proj / c_proj epilogues)
+                    self.itl[-1]["inp_f"] = fold(sd[p + ".attn.in_proj_weight"], p + ".ln_1", sd[p + ".attn.in_proj_bias"])
+                    self.itl[-1]["fc_f"] = fold(sd[p + ".mlp.c_fc.weight"], p + ".ln_2", sd[p + ".mlp.c_fc.bias"])
             self.scp = (W("spatial_ch_projs.weight"), Fp("spatial_ch_projs.bias"))
         # all 70 attn2 K/V projections of the prompt as ONE [sum 2C, 2048] weight: one GEMM per forward
         kv_ws, off = [], 0
@@ -468,14 +471,28 @@ class HipUNet:
         ops.concat_channels(x0, 320, ie, 320, feat, M)
         n = torch.empty_like(feat)
         att = torch.empty_like(feat)
-        for lay in self.itl:
-            ops.layer_norm(feat, *lay["ln1"], 1e-5, out=n)
-            qkv = ops.gemm(n, lay["inp"][0], bias=lay["inp"][1])
+        # FD_ITL_FOLD (with FD_LN_FOLD): ln_2 of each layer and ln_1 of the second folded into the next GEMM
+        # (fd_gemm_params.ln_in), the per-row partials written by the out_proj / c_proj epilogues (ln_out); ln_1 of
+        # the first layer (input: the concat) stays a pass
+        fold = self.ln_fold and knobs.get("FD_ITL_FOLD") != 0 and "fc_f" in self.itl[0]
+        st = torch.empty((M, 640 // 160, 2), dtype=torch.float32, device=self.device) if fold else None
+        for li, lay in enumerate(self.itl):
+            if fold and li > 0:
+                w, c, d = lay["inp_f"]
+                qkv = ops.gemm(feat, w, bias=d, ln_in=st, ln_c=c)
+            else:
+                ops.layer_norm(feat, *lay["ln1"], 1e-5, out=n)
+                qkv = ops.gemm(n, lay["inp"][0], bias=lay["inp"][1])
             ops.mha_seq_axis(qkv, att, self.ncfg, B // self.ncfg, HW, 640, 8)
-            ops.gemm(att, lay["outp"][0], bias=lay["outp"][1], residual=feat, out=feat)
-            ops.layer_norm(feat, *lay["ln2"], 1e-5, out=n)
-            m = ops.gemm(n, lay["fc"][0], bias=lay["fc"][1], act="quickgelu")
-            ops.gemm(m, lay["proj"][0], bias=lay["proj"][1], residual=feat, out=feat)
+            ops.gemm(att, lay["outp"][0], bias=lay["outp"][1], residual=feat, out=feat, ln_out=st)
+            if fold:
+                w, c, d = lay["fc_f"]
+                m = ops.gemm(feat, w, bias=d, act="quickgelu", ln_in=st, ln_c=c)
+            else:
+                ops.layer_norm(feat, *lay["ln2"], 1e-5, out=n)
+                m = ops.gemm(n, lay["fc"][0], bias=lay["fc"][1], act="quickgelu")
+            ops.gemm(m, lay["proj"][0], bias=lay["proj"][1], residual=feat, out=feat,
+                     ln_out=st if fold and li + 1 < len(self.itl) else None)
         return feat
 
     # ------------------------------------------------------------------------------------------ forward
