@@ -152,7 +152,23 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
               : nullptr;
   };
   auto setup = [&] __attribute__((always_inline)) (int tile) {
-    const int nt = tile / nsp, sp = tile - nt * nsp;
+    // tile order: output-channel tiles outer (the ~32 workgroups an XCD holds share one weight panel in its L2).
+    // PH: the 4 x Cout / BN column tiles come in groups of G whose weight panels fit together in ~2 MB of L2, the
+    // G tiles of one group and spatial tile adjacent -- the low-resolution patch is then fetched once per group
+    // instead of once per column tile (the 1024^2 upsample conv: 8 column tiles, all in one group)
+    int nt, sp;
+    if constexpr (PH) {
+      const int ntn = 4 * N / BN;
+      const long long panel = (long long)BN * p.K * 2;
+      int g = (int)min((long long)ntn, max(1LL, (2LL << 20) / panel));
+      while (ntn % g) --g;
+      const int ntg = tile / (nsp * g), rem = tile - ntg * (nsp * g);
+      sp = rem / g;
+      nt = ntg * g + (rem - sp * g);
+    } else {
+      nt = tile / nsp;
+      sp = tile - nt * nsp;
+    }
     img = sp / (tiles_y * tiles_x);
     spi = sp - img * (tiles_y * tiles_x);
     const int tyt = spi / tiles_x, txt = spi - tyt * tiles_x;
