@@ -739,6 +739,15 @@ extern "C" int fd_gemm(fd_gemm_params* p, void* stream) {
   if (p->M <= 0 || p->N <= 0 || p->K <= 0 || (p->K % 64) != 0) return FD_ERR_SHAPE;
   if (p->act == FD_ACT_GEGLU && (p->N % 32) != 0) return FD_ERR_SHAPE;
   if (p->rowbias && p->rows_per_group <= 0) return FD_ERR_ARG;
+  if (p->rowbias && p->rowbias_rows < ((long long)p->M + p->rows_per_group - 1) / p->rows_per_group)
+    return FD_ERR_SHAPE;  // the table must cover every row group of the launch (include/faithdiff_hip.h)
+  if (p->residual) {
+    if (p->ldr <= 0) return FD_ERR_SHAPE;
+    const long long need = (long long)p->M + (p->batch > 1 ? (long long)(p->batch - 1) * ((p->strideR + p->ldr - 1) /
+                                                                                            p->ldr) : 0);
+    if (p->residual_rows < need) return FD_ERR_SHAPE;
+  }
+  if (p->batch_inner > 1 && (p->residual || p->rowbias || p->ln_out || p->ln_in || p->gn_part)) return FD_ERR_SHAPE;
   if (p->conv) {
     if (p->Cin % 64 || (p->C1 > 0 && (p->C1 % 64 || !p->A2)) || p->K != (p->up_phase ? 4 : 9) * p->Cin)
       return FD_ERR_SHAPE;

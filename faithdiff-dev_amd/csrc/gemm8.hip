@@ -562,15 +562,22 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
       return;
     }
     if (tid == 0) {
-      // bounded: a lost flag would give a wrong tile, never a hung GPU
-      for (int it = 0; it < (1 << 24); ++it) {
-        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
-        __builtin_amdgcn_s_sleep(2);
+      // bounded: a lost flag poisons the tile (NaN, so the forward's finiteness checks see it) instead of hanging
+      // the GPU; the flag and the counter are reset only after the partner's flag was seen, never on the timeout
+      // path (a late partner's flag must not be taken for a later launch's)
+      unsigned got = 0u;
+      for (int it = 0; it < (1 << 24) && !got; ++it) {
+        got = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!got) __builtin_amdgcn_s_sleep(2);
       }
-      __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (got) {
+        __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ((volatile unsigned*)smem)[1] = got;
     }
     __syncthreads();
+    const bool partner_ok = ((volatile unsigned*)smem)[1] != 0u;
     f32x4 part[MT][NT];
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi)
@@ -582,6 +589,12 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
     for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
       for (int ni = 0; ni < NT; ++ni) acc[mi][ni] += part[mi][ni];
+    if (!partner_ok) {
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) acc[mi][ni] = f32x4{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+    }
   } else if (S > 1) {
     constexpr int SLAB = MT * NT * NTHR * 16;  // bytes per split of one tile
     const __amdgpu_buffer_rsrc_t rs =

@@ -26,7 +26,6 @@ HOST_DEFAULTS = {
     "FD_UP2_PHASE": 1,      # Upsample2D convs (VAE decoder, UNet up blocks) as four 2x2 phase convs of the low-res input
     "FD_GRAPHS": 1,         # hipGraph capture / replay of the UNet, VAE and text encoders
     "FD_TILE_BATCH": 13,    # TLC tiles per UNet forward
-    "FD_CFG_STREAMS": 0,    # UNet forward split into two concurrent row halves after the extras
     "FD_XATTN_GEMM": 1,     # attn2 as two GEMMs (scores + softmax epilogue, P . V W_o) against per-prompt products
     "FD_HALO_GN_CIN_MAX": 640,  # GroupNorm folded into the halo conv's staging pass up to this many input channels
 }

@@ -41,6 +41,7 @@ class GemmParams(ctypes.Structure):
         ("bsel_rows", c_int), ("bsel_mod", c_int), ("bsel_strideB", c_ll), ("bsel_strideN", c_ll),
         ("sm_group", c_int), ("sm_len", c_int),
         ("up_phase", c_int),
+        ("rowbias_rows", c_ll), ("residual_rows", c_ll),
     ]
 
 

@@ -206,6 +206,12 @@ class GnStats:
         self.done = self.rows > 0
 
 
+def _rows(t, ld):
+    """Rows of ``ld`` elements readable from t.data_ptr() within t's own extent (fd_gemm_params.*_rows)."""
+    span = 1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride()) if n > 0)
+    return 0 if t.numel() == 0 or ld <= 0 else (span - 1) // ld + 1
+
+
 def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=1, alpha=1.0, act="none",
          out_dtype=None, batch=1, M=None, N=None, K=None, lda=None, ldw=None, ldc=None, ldr=None,
          stride_a=0, stride_w=0, stride_c=0, stride_r=0, ln_out=None, ln_in=None, ln_c=None, ln_eps=1e-5, gn=None,
@@ -240,8 +246,10 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
         p.residual = residual.data_ptr()
         p.ldr = residual.stride(-2) if ldr is None else ldr
         p.strideR = stride_r
+        p.residual_rows = _rows(residual, p.ldr)
     if rowbias is not None:
         p.rowbias, p.rowbias_ld = rowbias.data_ptr(), rowbias.stride(0)
+        p.rowbias_rows = _rows(rowbias, p.rowbias_ld)
     p.rows_per_group = rows_per_group
     p.alpha = alpha
     p.act = L.ACT[act]
@@ -508,8 +516,10 @@ def _conv_params(x, wp, bias, nimg, H, W, stride, pad, upsample, x2, C1, out, ro
     p.bias = bias.data_ptr() if bias is not None else None
     if residual is not None:
         p.residual, p.ldr = residual.data_ptr(), residual.stride(-2)
+        p.residual_rows = _rows(residual, p.ldr)
     if rowbias is not None:
         p.rowbias, p.rowbias_ld, p.rows_per_group = rowbias.data_ptr(), rowbias.stride(0), Hout * Wout
+        p.rowbias_rows = _rows(rowbias, p.rowbias_ld)
     else:
         p.rows_per_group = 1
     p.alpha, p.act = alpha, L.ACT[act]
@@ -591,21 +601,28 @@ def gn_conv3x3(x, gamma, beta, wp, bias, nimg, H, W, eps, silu=True, groups=32, 
     # the in-staging transform costs ~1.2-1.5 us per 64-channel chunk, a GroupNorm apply pass ~10-14 us at the UNet's
     # sizes: folding pays up to ~10 chunks (probes/conv_ab.py, profiles/r04d_conv_ab.jsonl, r04e_conv_ab.jsonl);
     # wider inputs take the apply pass and the plain halo conv
-    if C <= knobs.get("FD_HALO_GN_CIN_MAX") and halo_conv_rows(x, wp, nimg, H, W, upsample=kw.get("upsample", False),
-                                                            upsample_size=kw.get("upsample_size")) > 0:
+    if C <= knobs.get("FD_HALO_GN_CIN_MAX") and halo_conv_rows(
+            x, wp, nimg, H, W, upsample=kw.get("upsample", False), upsample_size=kw.get("upsample_size"),
+            residual=kw.get("residual"), rowbias=kw.get("rowbias"), out=kw.get("out"),
+            out_dtype=kw.get("out_dtype")) > 0:
         aff = group_norm_affine(x, gamma, beta, nimg, H * W, C, groups, eps, stats=stats)
         return conv3x3(x, wp, bias, nimg, H, W, gn_in=(aff, silu), **kw)
     h = group_norm(x, gamma, beta, nimg, H * W, C, groups, eps, silu=silu, stats=stats)
     return conv3x3(h, wp, bias, nimg, H, W, **kw)
 
 
-def halo_conv_rows(x, wp, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, upsample_size=None, lda=None):
+def halo_conv_rows(x, wp, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, upsample_size=None, lda=None,
+                   residual=None, rowbias=None, out=None, out_dtype=None):
     """Rows per GroupNorm-statistics block the halo-staged conv kernel would write for this conv (256 / 128), 0 when
-    fd_gemm takes it on the implicit GEMM (then a consumer GroupNorm must run as its own pass).  Shapes only."""
-    dummy = torch.empty((1, wp.shape[0]), dtype=x.dtype, device=x.device)
-    p, _ = _conv_params(x, wp, None, nimg, H, W, stride, pad, upsample, x2, None if x2 is None else 0, dummy, None,
-                        None, "none", None, upsample_size, lda, 1.0)
-    p.C, p.ldc = x.data_ptr(), wp.shape[0]  # alignment / stride stand-ins for the real output (fresh allocations)
+    fd_gemm takes it on the implicit GEMM (then a consumer GroupNorm must run as its own pass).  Shapes only; the
+    residual / row bias / output the real call passes (their pointers and pitches) enter the plan's alignment rules."""
+    dummy = torch.empty((1, wp.shape[0]), dtype=out_dtype or x.dtype, device=x.device)
+    p, _ = _conv_params(x, wp, None, nimg, H, W, stride, pad, upsample, x2, None if x2 is None else 0, dummy, rowbias,
+                        residual, "none", out_dtype, upsample_size, lda, 1.0)
+    if out is not None:
+        p.C, p.ldc = out.data_ptr(), out.stride(-2)
+    else:
+        p.C, p.ldc = x.data_ptr(), wp.shape[0]  # alignment / stride stand-ins for a fresh output allocation
     return int(L.load().fd_conv_halo_plan(ctypes.byref(p)))
 
 
@@ -617,9 +634,9 @@ def halo_conv_pt(x, wp, nimg, H, W, upsample=False, upsample_size=None, residual
                         upsample_size, None, 1.0)
     p.C, p.ldc = x.data_ptr(), wp.shape[0]
     if residual:
-        p.residual, p.ldr = x.data_ptr(), wp.shape[0]
+        p.residual, p.ldr, p.residual_rows = x.data_ptr(), wp.shape[0], p.M
     if rowbias:
-        p.rowbias, p.rowbias_ld = x.data_ptr(), wp.shape[0]
+        p.rowbias, p.rowbias_ld, p.rowbias_rows = x.data_ptr(), wp.shape[0], nimg
     return int(L.load().fd_conv_halo_pt(ctypes.byref(p)))
 
 

@@ -112,8 +112,9 @@ typedef struct fd_gemm_params {
    * in front of every ResnetBlock2D conv (diffusers; UNet and VAE). */
   const void* gi_affine;
   int gi_silu;
-  /* Two-level batch (the 4-wave kernel, batch > 1): z -> (zo, zi) = (z / batch_inner, z % batch_inner); the
-   * operands sit at zi * strideX + zo * strideX_o.  batch_inner <= 1: one level (z * strideX). */
+  /* Two-level batch (the 4-wave kernel, batch > 1): z -> (zo, zi) = (z / batch_inner, z % batch_inner); A, B and C
+   * sit at zi * strideX + zo * strideX_o.  batch_inner <= 1: one level (z * strideX).  batch_inner > 1 takes no
+   * residual, row bias, LayerNorm partials or GroupNorm statistics (FD_ERR_SHAPE). */
   int batch_inner;
   long long strideA_o, strideB_o, strideC_o;
   /* Per-row-group B operand (cross-attention as two GEMMs: each image row of a batched forward multiplies its own
@@ -134,6 +135,12 @@ typedef struct fd_gemm_params {
    * halo-staged kernel runs it (FD_ERR_SHAPE when it cannot: Win < 16, Hin < 8, Cout not a multiple of 128 / 160);
    * no concat source, no gi_affine; gn_part blocks are (image, phase, 256- or 128-pixel tile). */
   int up_phase;
+  /* Extents fd_gemm checks on the host before any launch (FD_ERR_SHAPE when short, also for 0 with the pointer set):
+   * rowbias_rows = row groups the rowbias table holds, >= ceil(M / rows_per_group); residual_rows = rows of ldr
+   * elements readable from residual, >= M + (batch - 1) * ceil(strideR / ldr).  A ragged tile's rows past the last
+   * image are masked in every epilogue; these make an undersized table a returned error instead of a silent
+   * over-read (the r04 halo-conv row-bias fault, profiles/r04zc_serialized_fault.log). */
+  long long rowbias_rows, residual_rows;
 } fd_gemm_params;
 
 int fd_gemm(fd_gemm_params* p, void* stream);  /* writes only p->gn_done */

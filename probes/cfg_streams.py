@@ -1,7 +1,11 @@
 """Probe: does running the two CFG halves of a C2 UNet forward as two B = 1 graphs on two streams beat one B = 2
 graph?  (After the FaithDiff extras every row of the UNet is independent; two concurrent launch chains let one
 half's kernel prologue / epilogue / launch ramp overlap the other half's main loop.)  Timing only: the extras run
-per half here (MHA over one row), so the numbers are not a parity result.  Workspaces are made per stream."""
+per half here (MHA over one row), so the numbers are not a parity result.  The two concurrent forwards also share
+one HipUNet's persistent two-GEMM cross-attention P buffer (ops._pbuf, keyed by (M, KP)) and the GEMM split-K
+workspace, so they RACE: the outputs of this probe are meaningless and only its timings stand.  Concurrent forwards
+in the product would need a P buffer and workspace per stream; the product has no such mode (the FD_CFG_STREAMS
+knob was removed)."""
 import os
 import sys
 import time

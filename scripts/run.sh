@@ -10,7 +10,7 @@
 #     trace                     rocprofv3 kernel trace of the C2 bench: step window, GEMM instances, roofline check
 #     pmc=<unet|unet_fp8|vae|attn>   counter passes (scripts/prof.sh)
 #     probe=<script>[,args]     a python probe / measurement script
-#     ab=<reps>;<envA>;<envB>   alternating bench A/B (knob env per arm, e.g. ab=2;X=0;FD_CFG_STREAMS=1)
+#     ab=<reps>;<envA>;<envB>   alternating bench A/B (knob env per arm, e.g. ab=2;X=0;FD_GEMM8_W128=0)
 # Knob overrides (FD_*) reach bench.py / probes through fdhip.knobs.apply_env(); the product never reads them.
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out

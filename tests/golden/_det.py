@@ -1,4 +1,6 @@
 """Deterministic tensors shared by the golden generator and the tests (CPU torch RNG)."""
+import os
+
 import torch
 
 
@@ -65,6 +67,32 @@ def c2_inputs():
     post = det_tensor((1, 4, H // 8, W // 8), 9106)
     return dict(H=H, W=W, img=img, pe=pe, npe=npe, ppe=ppe, nppe=nppe, noise=noise, post=post, steps=20,
                 guidance=5.0, overlap=0.5, target=(1024, 1024), seed=0)
+
+
+BAND_PNG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "band", "band.png")
+
+
+def band_inputs(upscale=1, steps=4):
+    """The reference's one in-tree input (examples/band.png, 1079x778 RGBA) prepared exactly as
+    test_wo_llava.py:65,78-82 does: convert('RGB'), resize by ``upscale`` with LANCZOS, check_image_size
+    (bottom/right edge replication to a multiple of 8).  x1: 1080x784 -> a 135x98 latent, two ragged 128x98 TLC
+    tiles (target 1024: 128-latent tiles clamped to the 98-row height), both on the UNet's forward_upsample_size
+    path (98 = 2 * 49).  x4: 4316x3112 -> 4320x3112, a 540x389 latent.  The caption (LLaVA, OUT of scope) is
+    replaced by seeded prompt embeddings; noise and the VAE posterior draw are explicit seeded tensors."""
+    from PIL import Image
+    from utils.image_process import check_image_size
+    image = Image.open(BAND_PNG).convert("RGB")
+    w, h = image.size
+    image = image.resize((w * upscale, h * upscale), Image.LANCZOS)
+    padded, w0, h0, W, H = check_image_size(image)
+    pe = det_tensor((1, 77, 2048), 9201)
+    npe = det_tensor((1, 77, 2048), 9202)
+    ppe = det_tensor((1, 1280), 9203)
+    nppe = det_tensor((1, 1280), 9204)
+    noise = det_tensor((1, 4, H // 8, W // 8), 9205)
+    post = det_tensor((1, 4, H // 8, W // 8), 9206)
+    return dict(H=H, W=W, w0=w0, h0=h0, image=image, img=padded, pe=pe, npe=npe, ppe=ppe, nppe=nppe, noise=noise,
+                post=post, steps=steps, guidance=5.0, overlap=0.5, target=(1024, 1024), seed=0)
 
 
 # ----------------------------------------------------------------------------------------------------------------

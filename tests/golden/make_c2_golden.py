@@ -6,7 +6,10 @@ embeddings, initial noise and VAE posterior draw (tests/golden/_det.py:c2_inputs
 Follows pipeline_FaithDiff_tlc.py:1187-1459 through oracle/pipeline.py:run_pipeline.  Writes
 tests/golden/c2/{c2_golden.npz, c2_image.png}: the latent after steps 1, 5, 10, 15 and 20 (fp32), the
 final decoded uint8 image, and the sha256 of the uint8 input image (the GPU test re-creates the input
-from the same seed and checks the hash first).  Run here (CPU, ~10 min on 8 cores):
+from the same seed and checks the hash first).  Also writes tests/golden/c2/c2_eps_golden.npz: the oracle's step
+input latent and guided noise prediction (after CFG, the eps the Euler step consumes) at steps 1, 10, 19 and 20 --
+the teacher-forced per-step eps pins of SURVEY 8(d) (tests/test_pipeline_gpu.py::test_c2_teacher_forced_eps).
+Run here (CPU, ~12 min on 8 cores):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_c2_golden.py
 """
@@ -27,6 +30,7 @@ for p in (ROOT, os.path.join(ROOT, "faithdiff-dev_amd"), HERE):
 from _det import c2_inputs  # noqa: E402
 
 KEEP_STEPS = (0, 4, 9, 14, 19)
+EPS_STEPS = (0, 9, 18, 19)  # steps 1, 10, 19, 20: t = 951, 501, 51, 1 (sigma 11.03, 1.62, 0.23, 0.04)
 
 
 def oracle_models(seed=0):
@@ -61,16 +65,24 @@ def main():
         if i in KEEP_STEPS:
             kept[f"lat_step{i + 1}"] = lat.float().numpy().copy()
 
+    eps_kept = {}
+
+    def ecb(i, n, x, eps):
+        if i in EPS_STEPS:
+            eps_kept[f"x_step{i + 1}"] = x.float().numpy().copy()
+            eps_kept[f"eps_step{i + 1}"] = eps.float().numpy().copy()
+
     t0 = time.time()
     ref = run_pipeline(ru, rv, re_, x, c["pe"], c["npe"], c["ppe"], c["nppe"], c["noise"], c["post"],
                        num_inference_steps=c["steps"], guidance_scale=c["guidance"], overlap=c["overlap"],
                        target_size=c["target"], original_size=(c["H"], c["W"]), start_point="lr",
-                       step_callback=cb)
+                       step_callback=cb, eps_callback=ecb)
     img = ((ref["image"][0].permute(1, 2, 0) / 2 + 0.5).clamp(0, 1) * 255).round().to(torch.uint8).numpy()
     out = os.path.join(HERE, "c2")
     os.makedirs(out, exist_ok=True)
     np.savez_compressed(os.path.join(out, "c2_golden.npz"), final=ref["latents"].numpy(), input_sha256=np.array(sha),
                         **kept)
+    np.savez_compressed(os.path.join(out, "c2_eps_golden.npz"), input_sha256=np.array(sha), **eps_kept)
     from PIL import Image
     Image.fromarray(img).save(os.path.join(out, "c2_image.png"))
     print(f"done in {time.time() - t0:.0f} s; input sha256 {sha}")

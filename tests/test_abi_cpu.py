@@ -80,3 +80,56 @@ def test_knob_table_defaults_and_no_environment_reads():
             if f.endswith(".py") and f != "knobs.py":
                 txt = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"environ(\.get)?[\[(]\s*[\"']FD_(?!LIB_PATH)", txt), f
+
+
+def test_gemm_rejects_short_rowbias_and_residual_before_any_launch():
+    """fd_gemm_params.rowbias_rows / residual_rows: an undersized per-image row-bias table or
+    residual is FD_ERR_SHAPE from the host-side checks, before anything touches a device -- here on a machine with
+    no GPU at all.  The shape is the r04 fault's: a ResnetBlock2D conv1 on a 62x46 latent (the forward_upsample_size
+    path), two CFG images, time-embedding row bias one row per image."""
+    import ctypes
+    from fdhip import lib
+    FD_ERR_SHAPE, FD_ERR_ARG = -1, -5
+
+    def conv_params():
+        p = lib.GemmParams()
+        p.A, p.B, p.C = 0x10000, 0x20000, 0x30000  # never dereferenced: the checks return first
+        nimg, H, W, C = 2, 62, 46, 320
+        p.M, p.N, p.K, p.batch = nimg * H * W, C, 9 * C, 1
+        p.lda, p.ldb, p.ldc = C, 9 * C, C
+        p.conv, p.nimg, p.Hin, p.Win, p.Cin, p.Hout, p.Wout, p.stride, p.pad = 1, nimg, H, W, C, H, W, 1, 1
+        p.alpha, p.dtype, p.out_dtype, p.rows_per_group = 1.0, 0, 0, H * W
+        return p
+
+    so = lib.load()
+    p = conv_params()
+    p.rowbias, p.rowbias_ld, p.rowbias_rows = 0x40000, 1280, 1  # one image's row, two images in the launch
+    assert so.fd_gemm(ctypes.byref(p), None) == FD_ERR_SHAPE
+    p.rowbias_rows = 0  # pointer set, extent not given
+    assert so.fd_gemm(ctypes.byref(p), None) == FD_ERR_SHAPE
+    p = conv_params()
+    p.residual, p.ldr, p.residual_rows = 0x40000, 320, p.M - 1  # one row short
+    assert so.fd_gemm(ctypes.byref(p), None) == FD_ERR_SHAPE
+    p = conv_params()
+    p.rowbias, p.rowbias_ld, p.rowbias_rows, p.rows_per_group = 0x40000, 320, 2, 0
+    assert so.fd_gemm(ctypes.byref(p), None) == FD_ERR_ARG
+    # batched residual: (batch - 1) * strideR / ldr + M rows needed
+    q = lib.GemmParams()
+    q.A, q.B, q.C = 0x10000, 0x20000, 0x30000
+    q.M, q.N, q.K, q.batch, q.lda, q.ldb, q.ldc = 64, 128, 64, 3, 64, 64, 128
+    q.alpha, q.rows_per_group = 1.0, 1
+    q.residual, q.ldr, q.strideR, q.residual_rows = 0x40000, 128, 64 * 128, 64 * 3 - 1
+    assert so.fd_gemm(ctypes.byref(q), None) == FD_ERR_SHAPE
+    # the two-level batch offsets only A, B, C: a residual (or row bias) with batch_inner > 1 is refused (ADVICE r04)
+    q.residual_rows, q.batch_inner = 64 * 3, 3
+    assert so.fd_gemm(ctypes.byref(q), None) == FD_ERR_SHAPE
+
+
+def test_rows_helper_counts_reachable_rows():
+    import torch
+    from fdhip import ops
+    t = torch.empty(7, 320)
+    assert ops._rows(t, 320) == 7
+    assert ops._rows(torch.empty(5, 1280)[:, 640:960], 1280) == 5  # a column slice of the time-embedding table
+    assert ops._rows(torch.empty(3, 4, 160), 160) == 12
+    assert ops._rows(torch.empty(0, 8), 8) == 0

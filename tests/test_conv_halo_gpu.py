@@ -161,6 +161,41 @@ def test_halo_conv_epilogue_residual_rowbias_act_and_groupnorm_statistics():
     assert rel_l2(a1[:nimg * C].cpu(), a2[:nimg * C].cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("fold_gn", [False, True])
+def test_halo_conv_ragged_rowbias_residual_silu(fold_gn):
+    """The r04 fault's class (profiles/r04zc_serialized_fault.log): rows of a ragged tile past the last image must not
+    read the per-image row bias or the residual.  23 x 33 images (neither a multiple of the 8 / 16 tile rows nor of
+    the 16 tile columns), two images, a time-embedding table of EXACTLY nimg rows and a residual of exactly M rows in
+    their own allocations, SiLU, with and without the consumer GroupNorm folded into the staging pass -- against
+    torch.  The halo kernel must be the one that runs (fd_conv_halo_plan > 0)."""
+    from fdhip import ops
+    nimg, H, W, C = 2, 23, 33, 320
+    x, w, b = _inputs(nimg, H, W, C, C, torch.bfloat16, seed=21)
+    g = torch.Generator().manual_seed(22)
+    temb = torch.randn(nimg, C, generator=g)
+    res = torch.randn(nimg, C, H, W, generator=g).to(torch.bfloat16)
+    gamma = 1 + 0.1 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    with _knobs(FD_CONV_HALO_MIN_TILES=1):
+        wp = ops.pack_conv3x3(w.float()).to(DEV, torch.bfloat16)
+        xs, tb, rs = _nhwc(x).to(DEV), temb.to(DEV).contiguous(), _nhwc(res).to(DEV)
+        assert tb.shape == (nimg, C) and rs.shape == (nimg * H * W, C)
+        assert ops.halo_conv_rows(xs, wp, nimg, H, W, residual=rs, rowbias=tb) > 0
+        kw = dict(rowbias=tb, residual=rs, act="silu")
+        if fold_gn:
+            aff = ops.group_norm_affine(xs, gamma.to(DEV), beta.to(DEV), nimg, H * W, C, 32, 1e-5)
+            y = ops.conv3x3(xs, wp, b.float().to(DEV), nimg, H, W, gn_in=(aff, True), **kw)
+        else:
+            y = ops.conv3x3(xs, wp, b.float().to(DEV), nimg, H, W, **kw)
+    torch.cuda.synchronize()
+    xin = x.float()
+    if fold_gn:
+        xin = F.silu(F.group_norm(xin, 32, gamma, beta, 1e-5)).to(torch.bfloat16).float()
+    ref = F.silu(F.conv2d(xin, w.float(), b, padding=1) + temb[:, :, None, None]) + res.float()
+    rel = rel_l2(_nchw(y.float().cpu(), nimg, H, W), ref)
+    assert torch.isfinite(y).all() and rel < 6e-3, rel
+
+
 @pytest.mark.parametrize("Cin,Cout", [(1280, 1280), (2560, 1280), (640, 640)])
 def test_halo_conv_channel_split(Cin, Cout):
     """The 32^2 level (C2: 2 x 32 x 32): too few tiles, so the input channels are split over two workgroups combined
