@@ -539,11 +539,16 @@ class FaithDiffStableDiffusionXLPipeline:
             for c0 in range(0, count, tb):
                 n = min(tb, count - c0)
                 rows = n * cfg
-                ops.tlc_scale_input(state["canvas"], rows_t, cols_t, h, w, kh, kw, begin + c0, n, cfg, s, xin)
                 cond = cond_tiles[c0 * cfg:(c0 + n) * cfg].reshape(rows * kh * kw, cond_tiles.shape[-1])
                 tid = tids_all[(begin + c0) * cfg:(begin + c0 + n) * cfg]
+                # once run()'s graph for this batch shape is captured, the latent tiles and the step's timesteps go
+                # straight into its static inputs (one launch, fd_tlc_scale_input_t; no input copies for them)
+                st = unet.graph_inputs(rows, kh, kw, add_sample=add_sample, cond_embedded=cond_emb)
+                x_in, t_in = (st[0], st[1]) if st is not None else (xin[:rows * kh * kw], t_rows[i, :rows])
+                ops.tlc_scale_input(state["canvas"], rows_t, cols_t, h, w, kh, kw, begin + c0, n, cfg, s, x_in,
+                                    t_out=t_in if st is not None else None, timestep=float(ts[i]))
                 # one hipGraph replay per tile batch after the first two steps (HipUNet.run, fdhip/graphs.py)
-                eps = unet.run(xin[:rows * kh * kw], t_rows[i, :rows], tid, text_rows[:rows], cond, rows, kh, kw,
+                eps = unet.run(x_in, t_in, tid, text_rows[:rows], cond, rows, kh, kw,
                                add_sample=add_sample, cond_embedded=cond_emb)
                 ops.tlc_cfg_euler_step(eps, state["canvas"], rows_t, cols_t, h, w, kh, kw, begin + c0, n, cfg,
                                        guidance_scale, guidance_rescale, s, s_next, out[c0:c0 + n])

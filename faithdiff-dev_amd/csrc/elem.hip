@@ -537,7 +537,9 @@ extern "C" int fd_time_features(const float* t, const float* time_ids, const flo
 template <typename TO>
 __global__ void tlc_scale_input_kernel(const float* __restrict__ canvas, const int* __restrict__ row_org,
                                        const int* __restrict__ col_org, int nc, int H, int W, int kh, int kw,
-                                       int tile_begin, int ntiles, int cfg, float s, TO* __restrict__ out) {
+                                       int tile_begin, int ntiles, int cfg, float s, TO* __restrict__ out,
+                                       float* __restrict__ t_out, int t_n, float t_val) {
+  if (t_out && blockIdx.x == 0 && (int)threadIdx.x < t_n) t_out[threadIdx.x] = t_val;  // the step's UNet timesteps
   const long long per = (long long)kh * kw;
   const long long total = (long long)ntiles * per;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
@@ -557,10 +559,11 @@ __global__ void tlc_scale_input_kernel(const float* __restrict__ canvas, const i
   }
 }
 
-extern "C" int fd_tlc_scale_input(const float* canvas, const int* row_org, int nr, const int* col_org, int nc, int H,
-                                  int W, int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma, void* out,
-                                  int dtype, void* stream) {
+extern "C" int fd_tlc_scale_input_t(const float* canvas, const int* row_org, int nr, const int* col_org, int nc,
+                                    int H, int W, int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma,
+                                    void* out, int dtype, float* t_out, int t_n, float timestep, void* stream) {
   if (!canvas || !row_org || !col_org || !out) return FD_ERR_ARG;
+  if (t_n < 0 || t_n > 256 || (t_n > 0 && !t_out)) return FD_ERR_SHAPE;
   if (ntiles <= 0 || tile_begin < 0 || tile_begin + ntiles > nr * nc || kh > H || kw > W || cfg <= 0)
     return FD_ERR_SHAPE;
   // scale_model_input divides by (sigma^2 + 1)^0.5 (diffusers EulerDiscreteScheduler; pipeline:1336): `sigma`
@@ -569,9 +572,16 @@ extern "C" int fd_tlc_scale_input(const float* canvas, const int* row_org, int n
   hipStream_t st = (hipStream_t)stream;
   FD_DISPATCH_O(dtype, hipLaunchKernelGGL(tlc_scale_input_kernel<TO>, grid1d((long long)ntiles * kh * kw), dim3(256), 0,
                                           st, canvas, row_org, col_org, nc, H, W, kh, kw, tile_begin, ntiles, cfg, sigma,
-                                          (TO*)out));
+                                          (TO*)out, t_n > 0 ? t_out : nullptr, t_n, timestep));
   FD_LAUNCH_CHECK();
   return FD_OK;
+}
+
+extern "C" int fd_tlc_scale_input(const float* canvas, const int* row_org, int nr, const int* col_org, int nc, int H,
+                                  int W, int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma, void* out,
+                                  int dtype, void* stream) {
+  return fd_tlc_scale_input_t(canvas, row_org, nr, col_org, nc, H, W, kh, kw, tile_begin, ntiles, cfg, sigma, out,
+                              dtype, nullptr, 0, 0.f, stream);
 }
 
 // CFG combine + Euler step for each tile; x taken from the canvas at the tile origin.

@@ -62,6 +62,12 @@ class GraphCache:
         g.replay()
         return out
 
+    def static_inputs(self, key):
+        """The captured graph's static input buffers for ``key`` (None before capture).  A caller that writes its
+        inputs straight into them makes run() skip the copies (it compares data pointers)."""
+        ent = self._graphs.get(key) if self.enabled else None
+        return None if ent is None else ent[1]
+
     def _capture(self, key, fn, inputs):
         from . import ops
         static = [None if x is None else x.clone() for x in inputs]

@@ -91,6 +91,8 @@ _SIGS = {
     "fd_time_features": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "fd_tlc_scale_input": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                    c_f, c_vp, c_int, c_vp]),
+    "fd_tlc_scale_input_t": (c_int, [c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_f, c_vp, c_int, c_vp, c_int, c_f, c_vp]),
     "fd_tlc_cfg_euler_step": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                       c_int, c_f, c_f, c_f, c_f, c_vp, c_int, c_vp]),
     "fd_tlc_blend": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),

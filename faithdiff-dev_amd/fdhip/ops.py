@@ -831,12 +831,23 @@ def euler_scale_divisor(sigma):
     return float((sg ** 2 + 1) ** 0.5)
 
 
-def tlc_scale_input(canvas, row_org, col_org, H, W, kh, kw, tile_begin, ntiles, cfg, sigma, out):
-    """Tiles of the canvas / (sigma^2 + 1)^0.5 (correctly rounded fp32 division), CFG-duplicated, NHWC."""
-    L.check(L.load().fd_tlc_scale_input(L.ptr(canvas), L.ptr(row_org), row_org.numel(), L.ptr(col_org),
-                                        col_org.numel(), H, W, kh, kw, tile_begin, ntiles, cfg,
-                                        euler_scale_divisor(sigma), L.ptr(out),
-                                        L.dtype_code(out.dtype), L.stream()), "fd_tlc_scale_input")
+def tlc_scale_input(canvas, row_org, col_org, H, W, kh, kw, tile_begin, ntiles, cfg, sigma, out, t_out=None,
+                    timestep=None):
+    """Tiles of the canvas / (sigma^2 + 1)^0.5 (correctly rounded fp32 division), CFG-duplicated, NHWC.  t_out (fp32,
+    contiguous): also filled with ``timestep`` by the same launch (fd_tlc_scale_input_t)."""
+    if t_out is None:
+        L.check(L.load().fd_tlc_scale_input(L.ptr(canvas), L.ptr(row_org), row_org.numel(), L.ptr(col_org),
+                                            col_org.numel(), H, W, kh, kw, tile_begin, ntiles, cfg,
+                                            euler_scale_divisor(sigma), L.ptr(out),
+                                            L.dtype_code(out.dtype), L.stream()), "fd_tlc_scale_input")
+        return out
+    if t_out.dtype != torch.float32 or not t_out.is_contiguous():
+        raise ValueError("tlc_scale_input: t_out must be a contiguous fp32 tensor")
+    L.check(L.load().fd_tlc_scale_input_t(L.ptr(canvas), L.ptr(row_org), row_org.numel(), L.ptr(col_org),
+                                          col_org.numel(), H, W, kh, kw, tile_begin, ntiles, cfg,
+                                          euler_scale_divisor(sigma), L.ptr(out), L.dtype_code(out.dtype),
+                                          L.ptr(t_out), t_out.numel(), float(timestep), L.stream()),
+            "fd_tlc_scale_input_t")
     return out
 
 

@@ -519,11 +519,21 @@ class HipUNet:
         """forward() through the graph cache (fdhip/graphs.py): eager on the first call of a shape, captured on
         the second, one hipGraph replay after that.  The result is the graph's static output buffer (valid
         until the next run() of the same shape).  This is what the pipeline's denoise loop and bench.py call."""
-        key = ("unet", B, H, Wd, bool(add_sample), cond is None, bool(cond_embedded), x.dtype, self.npairs > 1,
-               kv_pair0)
+        key = self._graph_key(B, H, Wd, add_sample, cond is None, cond_embedded, x.dtype, kv_pair0)
         return self.graphs.run(key, lambda *a: self.forward(*a, B, H, Wd, add_sample=add_sample,
                                                             cond_embedded=cond_embedded, kv_pair0=kv_pair0),
                                [x, t, time_ids, text_embeds, cond])
+
+    def _graph_key(self, B, H, Wd, add_sample, no_cond, cond_embedded, dtype, kv_pair0):
+        return ("unet", B, H, Wd, bool(add_sample), bool(no_cond), bool(cond_embedded), dtype, self.npairs > 1,
+                kv_pair0)
+
+    def graph_inputs(self, B, H, Wd, add_sample=True, cond_embedded=False, kv_pair0=0, has_cond=True):
+        """The static input buffers [x, t, time_ids, text_embeds, cond] of run()'s captured graph for this call
+        shape, or None before the capture.  The denoise loop writes the step's latent tile and timestep straight
+        into them (fd_tlc_scale_input_t), so a replay needs no input copies."""
+        return self.graphs.static_inputs(self._graph_key(B, H, Wd, add_sample, not has_cond, cond_embedded,
+                                                         self.dtype, kv_pair0))
 
     def forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True, cond_embedded=False, kv_pair0=0):
         """x: NHWC [B*H*W, 4] (dtype); t: fp32 [B]; time_ids fp32 [B, 6]; text_embeds fp32 [B, 1280];

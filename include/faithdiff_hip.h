@@ -353,6 +353,12 @@ int fd_time_features(const float* t, const float* time_ids, const float* text_em
 int fd_tlc_scale_input(const float* canvas, const int* row_org, int nr, const int* col_org, int nc, int H, int W,
                        int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma, void* out, int dtype,
                        void* stream);
+/* The same, also writing the step's UNet timestep into t_out[0 .. t_n) (t_n <= 256; the `t` row of the UNet call,
+ * :1350-1360) from inside the same launch: the denoise loop's per-step host-side fill of the timestep buffer (a
+ * separate elementwise launch) is gone. */
+int fd_tlc_scale_input_t(const float* canvas, const int* row_org, int nr, const int* col_org, int nc, int H, int W,
+                         int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma, void* out, int dtype,
+                         float* t_out, int t_n, float timestep, void* stream);
 /* CFG combine (+ rescale_noise_cfg when guidance_rescale > 0, :286-305,1363-1369) and the Euler step
  * (:1373; gamma = 0, fp32): eps NHWC [ntiles*cfg][kh*kw][4] (uncond row first), x = canvas tile,
  * out_tiles fp32 NCHW [ntiles][4][kh][kw] = x + ((x - (x - sigma*e)) / sigma) * (sigma_next - sigma). */

@@ -1,4 +1,6 @@
 """CPU tests of the product's host-side logic against the reference's golden vectors and the oracle."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -231,3 +233,25 @@ def test_upsample_conv_phase_packing_is_the_same_function():
             for b in range(2):
                 out[:, :, a::2, b::2] = F.conv2d(xp[:, :, a:a + H + 1, b:b + W + 1], wph[2 * a + b])
         torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_band_fixture_preprocessing_and_tile_grid():
+    """The reference's examples/band.png (tests/golden/band/band.png) through test_wo_llava.py:65,78-82 on the host
+    (convert('RGB'), x1 LANCZOS, check_image_size): the padded input is the one the band golden was generated from
+    (sha256), 1080x784 with edge-replicated padding, and the product's TLC grid cuts its 135x98 latent into the same
+    two ragged 128x98 tiles as the oracle (tests/golden/make_band_golden.py)."""
+    import hashlib
+
+    import numpy as np
+    from _det import band_inputs
+    from FaithDiff.pipelines.tlc import TileGrid
+    gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "band", "band_golden.npz"))
+    c = band_inputs(1)
+    u8 = np.asarray(c["img"], dtype=np.uint8)
+    assert (c["W"], c["H"], c["w0"], c["h0"]) == (1080, 784, 1079, 778)
+    assert hashlib.sha256(u8.tobytes()).hexdigest() == str(gold["input_sha256"])
+    src = np.asarray(c["image"], dtype=np.uint8)
+    assert np.array_equal(u8[:778, :1079], src) and np.array_equal(u8[778:, :1079], np.repeat(src[-1:], 6, 0))
+    g = TileGrid(c["H"] // 8, c["W"] // 8, (128, 128), 0.5)
+    assert (g.kh, g.kw, g.ntiles) == (98, 128, int(gold["ntiles"])) == (98, 128, 2)
+    assert gold["final"].shape == (1, 4, 98, 135) and np.isfinite(gold["final"]).all()
