@@ -193,6 +193,12 @@ class EventTimer:
         d = [a.elapsed_time(b) for a, b in zip(st[:-1], st[1:])]
         return d
 
+    def gather_ms(self):
+        """Per-step durations of the tile exchange (run_tile_loop's "gather_start" / "gather_end" events)."""
+        a = [e for (lab, _, e) in self.ev if lab == "gather_start"]
+        b = [e for (lab, _, e) in self.ev if lab == "gather_end"]
+        return [x.elapsed_time(y) for x, y in zip(a, b)]
+
     def span_ms(self, a, b):
         ea = next(e for (lab, _, e) in self.ev if lab == a)
         eb = next(e for (lab, _, e) in reversed(self.ev) if lab == b)
@@ -452,6 +458,9 @@ def c3_run(pipe, world, rank, dev, size, steps, warm=True, tag="C3"):
     s = max_over_ranks(s, world, dev)
     st = tm.step_ms()
     loop_s = max_over_ranks(sum(st) / 1e3, world, dev)
+    gm = tm.gather_ms()
+    per = -(-ntiles // world)
+    counts = [max(0, min(ntiles, r * per + per) - r * per) for r in range(world)]
     return {"workload": f"{tag}: {size}x{size} tiled restoration, {ntiles} TLC tiles x {steps} Euler steps, tiled VAE "
                         f"encode/decode, tiles sharded over {world} rank(s), one all_gather_into_tensor per step",
             "ntiles": ntiles, "steps": steps, "n_ranks": world, "s_per_image": round(s, 3),
@@ -459,14 +468,18 @@ def c3_run(pipe, world, rank, dev, size, steps, warm=True, tag="C3"):
             "step_ms_median": round(float(np.median(st)), 2),
             "pre_loop_ms": round(tm.span_ms("call_start", "loop_start"), 1),
             "decode_ms": round(tm.span_ms("decode_start", "decode"), 1),
-            "all_gather_bytes_per_step": (ntiles + (-ntiles) % world) * 4 * 128 * 128 * 4 if world > 1 else 0,
-            "latents_finite": tm.finite}
+            "all_gather_bytes_per_step": per * world * 4 * 128 * 128 * 4 if world > 1 else 0,
+            # the per-step exchange, HIP events around TileShard.gather on the loop's stream (max over ranks): with
+            # tiles_per_rank it tells whether the exchange or the largest shard bounds a multi-GPU step
+            "all_gather_ms_per_step": round(max_over_ranks(float(np.mean(gm)), world, dev), 3) if gm else 0.0,
+            "all_gather_ms_max": round(max_over_ranks(max(gm), world, dev), 3) if gm else 0.0,
+            "tiles_per_rank": counts, "latents_finite": tm.finite}
 
 
 def roofline_leg(loop, fp8):
     from fdhip import arch
     fam = family_times(lambda: loop.unet.forward(*loop.args(), cond_embedded=True), ["gemm", "flash_attn", "gemm_e4m3"])
-    n_g, fl_g, _, ms_g = fam["gemm"]
+    n_g, fl_g, nb_g, ms_g = fam["gemm"]
     gemm_tf = fl_g / (ms_g / 1e3) / 1e12
     res = {}
     tr = load_traffic(f"C2 {loop.h * 8}" + (" (use_fp8, e4m3 MFMA Linears)" if fp8 else ""))
@@ -477,6 +490,10 @@ def roofline_leg(loop, fp8):
         "traffic": None if tr16 is None else tr16["hbm_bytes_per_forward"],
         "kernel": "gemm8_kernel + gemm256_kernel + gemm_kernel (all MFMA GEMM + implicit-GEMM conv launches of one UNet forward)",
         "launches": n_g, "algorithmic_flops": fl_g, "kernel_ms_per_forward": round(ms_g, 3),
+        # every operand once per launch (ops._gemm_bytes: A or the conv source image, weights, output, residual);
+        # traffic / algorithmic_bytes is the re-read factor (per-XCD L2 replication)
+        "algorithmic_bytes": nb_g,
+        "traffic_ratio": None if tr16 is None else round(tr16["hbm_bytes_per_forward"] / nb_g, 3),
         "avg_launch_us": round(ms_g / n_g * 1e3, 2),
         "method": "the forward's GEMM launches captured on their own into one hipGraph, replayed 20x between HIP "
                   "events on the capture stream",
@@ -566,6 +583,7 @@ def main(argv=None):
               "knobs": knobs.changed()}
     if world > 1:  # rank 0 drew the weights, every other rank received them (FaithDiff_pipeline(process_group=))
         result["weights_broadcast"] = {"bytes": pipe.last_broadcast_bytes, "build_s": round(pipe.build_s, 2),
+                                       "broadcast_s": round(pipe.last_broadcast_s, 3),
                                        "backend": dist.get_backend()}
 
     if args.workload in ("c3", "c4"):

@@ -17,6 +17,7 @@ run on the HIP kernels (fdhip/clip.py) when built by from_pretrained, with a see
 only for pipelines constructed without them.
 """
 import inspect
+import time
 import zlib
 from types import SimpleNamespace
 from typing import Any, Callable, Dict, List, Optional, Tuple, Union
@@ -93,6 +94,7 @@ class FaithDiffStableDiffusionXLPipeline:
         self.last_timings = {}
         self._weights_group = None   # the group broadcast_weights last synchronised the weights over
         self.last_broadcast_bytes = 0
+        self.last_broadcast_s = 0.0
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -187,6 +189,7 @@ class FaithDiffStableDiffusionXLPipeline:
             raise RuntimeError("broadcast_weights: host weights were released (release_host_weights) before they "
                                f"were synchronised over the group (this rank: {released or 'none'})")
         total = 0
+        t0 = time.perf_counter()
         for name, m, sd in owners:
             if sd is None:
                 continue
@@ -194,8 +197,10 @@ class FaithDiffStableDiffusionXLPipeline:
             for attr in ("_hip", "_enc", "_dec"):
                 if getattr(m, attr, None) is not None:
                     setattr(m, attr, None)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
         self._weights_group = group
-        self.last_broadcast_bytes = total
+        self.last_broadcast_bytes, self.last_broadcast_s = total, time.perf_counter() - t0
         return total
 
     # ------------------------------------------------------------------ properties (:915-948)
@@ -571,7 +576,8 @@ class FaithDiffStableDiffusionXLPipeline:
 
         if timer is not None:  # timer(label, i): measurement hook (bench.py records a HIP event per call)
             timer("loop_start", 0)
-        final = run_tile_loop(num_inference_steps, shard, (4, kh, kw), compute, blend, dev, on_step=on_step)
+        final = run_tile_loop(num_inference_steps, shard, (4, kh, kw), compute, blend, dev, on_step=on_step,
+                              timer=timer)
         if final is None:
             final = canvas
         lat = final.view(1, 4, h, w)

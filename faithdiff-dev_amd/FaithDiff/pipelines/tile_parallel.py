@@ -97,8 +97,9 @@ def staging_device(group=None):
     return torch.device("cpu")
 
 
-def run_tile_loop(nsteps, shard, tile_shape, compute, blend, device, dtype=torch.float32, on_step=None):
-    """Returns the final canvas.  tile_shape = (4, kh, kw)."""
+def run_tile_loop(nsteps, shard, tile_shape, compute, blend, device, dtype=torch.float32, on_step=None, timer=None):
+    """Returns the final canvas.  tile_shape = (4, kh, kw).  timer(label, i) (a measurement hook, e.g. bench.py's
+    EventTimer) brackets each step's exchange with "gather_start" / "gather_end" when the tiles are sharded."""
     local = torch.zeros((shard.per,) + tuple(tile_shape), dtype=dtype, device=device)
     buf = torch.empty((shard.world * shard.per,) + tuple(tile_shape), dtype=dtype, device=device) \
         if shard.world > 1 else None
@@ -106,7 +107,11 @@ def run_tile_loop(nsteps, shard, tile_shape, compute, blend, device, dtype=torch
     for i in range(nsteps):
         if shard.count:
             compute(i, shard.begin, shard.count, local)
+        if timer is not None and shard.world > 1:
+            timer("gather_start", i)
         tiles = shard.gather(local, buf)
+        if timer is not None and shard.world > 1:
+            timer("gather_end", i)
         canvas = blend(tiles)
         if on_step is not None:
             on_step(i, canvas)

@@ -173,14 +173,34 @@ def _timed(kind, flops, nbytes, launch, label=None):
     _probe.append((kind, float(flops), float(nbytes), e0, e1) + ((label,) if label else ()))
 
 
+def _gemm_bytes(p):
+    """Algorithmic HBM bytes of one fd_gemm launch: every operand once (A -- for a conv the source image(s), not the
+    9x im2col --, B per distinct weight slot, C, the residual), no re-reads (bench.py roofline.algorithmic_bytes)."""
+    es = 4 if p.dtype == L.dtype_code(torch.float32) else 2
+    eo = {L.dtype_code(torch.float32): 4}.get(p.out_dtype, 2)
+    nb = max(p.batch, 1)
+    nout = p.N // 2 if p.act == L.ACT["geglu"] else p.N
+    a = (p.nimg * p.Hin * p.Win * p.Cin * es) if p.conv else p.M * p.K * es * nb
+    slots = nb if p.strideB else 1
+    if p.bsel_rows > 0:
+        groups = -(-p.M // p.bsel_rows)
+        slots = min(groups, p.bsel_mod) if p.bsel_mod > 0 else groups
+    b = p.N * p.K * es * slots
+    c = p.M * nout * eo * nb * (2 if p.residual else 1)
+    return float(a + b + c)
+
+
 def _launch_gemm(p, what):
     flops = 2.0 * p.M * p.N * p.K * max(p.batch, 1)
     label = None
+    nbytes = 0.0
+    if _recorder is not None:
+        nbytes = _gemm_bytes(p)
     if _probe is not None or _recorder is not None:
         act = {v: k for k, v in L.ACT.items()}[p.act]
         label = (f"{'conv' if p.conv else 'gemm'} M={p.M} N={p.N} K={p.K} b={p.batch} {act}"
                  f"{' up' if p.upsample else ''}{' cat' if p.A2 else ''}{' res' if p.residual else ''}")
-    _timed("gemm", flops, 0.0, lambda: L.check(L.load().fd_gemm(ctypes.byref(p), L.stream()), what), label)
+    _timed("gemm", flops, nbytes, lambda: L.check(L.load().fd_gemm(ctypes.byref(p), L.stream()), what), label)
 
 
 class GnStats:

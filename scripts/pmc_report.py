@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 passes of scripts/r02_prof.sh over one scripts/pmc_work.py workload.
+"""Summarise the rocprofv3 passes of scripts/prof.sh over one scripts/pmc_work.py workload.
 
 Input: <dir>/{trace,FETCH_SIZE,WRITE_SIZE,sq1,sq2,...}/**.csv + meta.json (dir default gpurun_out/pmc_<what>).  The measured window
 is the dispatches between the last two fd_postprocess_u8 markers; the calibration copy sits between the two
@@ -139,7 +139,7 @@ def main(what, out_path, base=None):
         res["calibration"] = {"bytes_read": meta["calib_bytes_read"], "bytes_written": meta["calib_bytes_written"],
                               "fetch_kib_x2": 2 * calib["FETCH_SIZE"] * 1024 if "FETCH_SIZE" in calib else None,
                               "write_kib": calib.get("WRITE_SIZE", 0) * 1024}
-    res["method"] = ("scripts/r02_prof.sh: rocprofv3 --kernel-trace (durations) and separate --pmc passes "
+    res["method"] = ("scripts/prof.sh: rocprofv3 --kernel-trace (durations) and separate --pmc passes "
                      "(FETCH_SIZE; WRITE_SIZE; SQ groups) over scripts/pmc_work.py --what " + what)
     json.dump(res, open(out_path, "w"), indent=1)
     print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "counters"} for k, v in out.items()}, indent=1))

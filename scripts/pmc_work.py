@@ -7,7 +7,7 @@ the Infinity Cache); fd_postprocess_u8 launches (never part of the workloads) ma
 copy, [m2, m3) = the measured workload.  The workload runs once eagerly first (warm caches and workspaces, same
 kernels as the graph replays).  Writes /tmp/fdprof/pmc_<what>/meta.json (launch / FLOP / algorithmic-byte counts
 per kernel family).  Run under rocprofv3 with ONE counter group per pass and no trace domains besides
---kernel-trace (scripts/r02_prof.sh)."""
+--kernel-trace (scripts/prof.sh)."""
 import argparse
 import json
 import os
