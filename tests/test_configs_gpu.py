@@ -152,3 +152,44 @@ def test_batched_call_forwards_embeddings_and_callbacks():
     assert seen == [0, 2]
     with pytest.raises(NotImplementedError):
         pipe(lr_img=imgs, prompt=prompts, num_images_per_prompt=2, **kw)
+
+
+def test_band_x4_wo_llava_tile_batch_bitwise():
+    """The reference's examples/band.png at test_wo_llava.py's default upscale 4 (:18,65,78-82): 1079x778 RGBA ->
+    convert('RGB') -> x4 LANCZOS 4316x3112 -> check_image_size 4320x3112, a 540x389 latent (neither a multiple of 4
+    nor of the 64-latent tile stride) in 48 TLC tiles with ragged right / bottom tiles, then the script's tail (crop to
+    4316x3112, adain colour fix).  2 Euler steps of the 20-step schedule (denoising_end), tiles batched 13 and 4 per UNet
+    forward: bitwise equal latents and pixels, every latent finite, the image not flat.  The full 20-step run is
+    scripts/band_x4.py (profiles/r05*_band_x4.json)."""
+    from _det import band_inputs
+    from FaithDiff.pipelines.tlc import TileGrid
+    from utils.color_fix import adain_color_fix
+    c = band_inputs(4)
+    assert (c["W"], c["H"], c["w0"], c["h0"]) == (4320, 3112, 4316, 3112)
+    assert TileGrid(c["H"] // 8, c["W"] // 8, (128, 128), 0.5).ntiles == 48
+    pipe = _build(seed=0)
+    res = []
+    for tb in (13, 4):
+        pipe.tile_batch = tb
+        cap = {}
+
+        def cb(p, i, t, k):
+            cap["lat"] = k["latents"].detach().float().cpu().clone()
+            cap["steps"] = i + 1
+            return {}
+        out = pipe(lr_img=c["img"], prompt_embeds=c["pe"], negative_prompt_embeds=c["npe"],
+                   pooled_prompt_embeds=c["ppe"], negative_pooled_prompt_embeds=c["nppe"], guidance_scale=5.0,
+                   start_point="lr", height=c["H"], width=c["W"], overlap=0.5, target_size=(1024, 1024),
+                   latents=c["noise"], posterior_noise=c["post"], num_inference_steps=20, denoising_end=0.1,
+                   callback_on_step_end=cb).images[0]
+        res.append((cap["lat"], out, cap["steps"]))
+    (lat13, img13, n13), (lat4, img4, n4) = res
+    assert n13 == n4 == 2
+    assert lat13.shape == (1, 4, 389, 540) and torch.isfinite(lat13).all()
+    assert torch.equal(lat13, lat4)
+    a13, a4 = np.asarray(img13), np.asarray(img4)
+    assert a13.shape == (3112, 4320, 3) and (a13 == a4).all()
+    fixed = adain_color_fix(img13.crop((0, 0, c["w0"], c["h0"])), c["image"])
+    assert fixed.size == c["image"].size == (4316, 3112)
+    parity.record("band_x4_image_std", float(a13.std()), bar=">1")
+    assert a13.std() > 1.0
