@@ -438,6 +438,10 @@ class FaithDiffStableDiffusionXLPipeline:
         callback_steps = kwargs.pop("callback_steps", None)
         posterior_noise = kwargs.pop("posterior_noise", None)  # explicit VAE posterior draw (parity tests)
         timer = kwargs.pop("timer", None)
+        # eps_hook(step, tile_begin, ntiles, eps): observation hook for the teacher-forced parity tests -- sees each
+        # UNet call's noise prediction (NHWC [ntiles * cfg * kh * kw, 4], CFG rows uncond-first; the graph's static
+        # output, valid only inside the call) before the CFG + Euler step consumes it
+        eps_hook = kwargs.pop("eps_hook", None)
 
         height = height or self.default_sample_size * self.vae_scale_factor
         width = width or self.default_sample_size * self.vae_scale_factor
@@ -555,6 +559,8 @@ class FaithDiffStableDiffusionXLPipeline:
                 # one hipGraph replay per tile batch after the first two steps (HipUNet.run, fdhip/graphs.py)
                 eps = unet.run(x_in, t_in, tid, text_rows[:rows], cond, rows, kh, kw,
                                add_sample=add_sample, cond_embedded=cond_emb)
+                if eps_hook is not None:
+                    eps_hook(i, begin + c0, n, eps)
                 ops.tlc_cfg_euler_step(eps, state["canvas"], rows_t, cols_t, h, w, kh, kw, begin + c0, n, cfg,
                                        guidance_scale, guidance_rescale, s, s_next, out[c0:c0 + n])
 

@@ -21,12 +21,22 @@
 // order whatever the tile shape (TH 16 or 8, BN 160 or 128), so tile choices never change a bit; it differs from
 // the implicit GEMM's tap-major order (not bitwise equal to gemm8, tested against fp32).
 #include <type_traits>
+#include <utility>
 
 #include "fd_common.h"
 
 __device__ __attribute__((aligned(256))) unsigned char g_zero_halo[256];
 
+#ifndef FD_HALO_CT
+#define FD_HALO_CT 1
+#endif
+
 namespace {
+
+template <int... I, typename F>
+__device__ __forceinline__ void halo_static_for(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>()), ...);
+}
 
 template <int N>
 __device__ __forceinline__ void hvm() {
@@ -34,6 +44,10 @@ __device__ __forceinline__ void hvm() {
 }
 
 constexpr int PW = 18;  // patch width: 16 output columns + halo
+// Patch LDS layout: pixel pix = py * PW + px at pix * 128 B, its 16-B channel chunk j at chunk slot j ^ ((px >> 1) & 7).
+// The XOR depends on the pixel's COLUMN only (PW * 128 B = 9 x 256 B, so the row never changes the bank): a fragment
+// read for tap (ky, kx) is then a per-lane offset of (kx, K half) plus an immediate (row, chunk buffer), with no
+// address arithmetic in the K loop (the per-step LDS address VALU had made the loop VALU-issue-bound, r05).
 constexpr int TR = 4;   // tap of chunk c at which chunk c + 1's patch is waited for
 constexpr int NPART = 8 - TR;  // ... and transformed in NPART pieces at taps TR .. 7 (published by tap 8's barrier)
 
@@ -81,6 +95,8 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   constexpr int PT_EP = SMEM_MAIN, PT_SLOT = PT_EP + PER * LDE * 4, PT_END = PT_SLOT + PER * VPR * 16;
   static_assert(!PH || (!GNI && !SK && !PT), "phase form: plain tiles only");
   constexpr int NTAP = PH ? 4 : 9;
+  // lane-constant LDS read bases in the K loop (below): every tile form but the persistent and the phase ones
+  constexpr bool CT = !PT && !PH && FD_HALO_CT;
   static_assert(!PT || (!SK && BN == 128 && TH == 16 && PER * VPR == 512 && PT_END <= 163840 &&
                         PER * LDE * 4 >= 512 * 8),
                 "PT layout: one 8-column vector per thread per pass, red[] in the pass buffer");
@@ -128,7 +144,9 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   // P_I loads per chunk and the epilogue's counted waits hold
   int img = 0, spi = 0, y0 = 0, x0 = 0, n0 = 0, nb = 0, pha = 0, phb = 0;  // nb: B row base (PH: phase-major)
   const T* b_row[PT ? 1 : PER_B];
-  const T* p_src[PT ? 1 : P_I];
+  // PSRC_RE: patch sources recomputed at each DMA issue instead of held in 2 * P_I VGPRs across the K loop (PT)
+  constexpr bool PSRC_RE = PT;
+  const T* p_src[PSRC_RE ? 1 : P_I];
   const float* __restrict__ aff = nullptr;
   auto b_src = [&] __attribute__((always_inline)) (int i) {
     int row = (w + 4 * i) * 8 + (lane >> 3);
@@ -139,7 +157,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   auto p_src_of = [&] __attribute__((always_inline)) (int i) -> const T* {
     const int j = p_row(i);
     int pix = j * 8 + (lane >> 3);
-    if constexpr (PT) asm volatile("" : "+v"(pix));  // PT: recomputed at each issue, never hoisted out of the loops
+    if constexpr (PSRC_RE) asm volatile("" : "+v"(pix));  // recomputed at each issue, never hoisted out of the loops
     const int py = pix / PW, px = pix - (pix / PW) * PW;
     const int iy = y0 - 1 + py, ix = x0 - 1 + px;
     const bool ok = j < P_TOT && pix < PIX && iy >= 0 && iy < Hg && ix >= 0 && ix < Wg;
@@ -148,7 +166,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       sy = up2 ? (iy >> 1) : (iy * p.Hin) / Ho;
       sx = up2 ? (ix >> 1) : (ix * p.Win) / Wo;
     }
-    return ok ? A + ((long long)(img * p.Hin + sy) * p.Win + sx) * p.lda + (((lane & 7) ^ ((pix >> 1) & 7)) * 8)
+    return ok ? A + ((long long)(img * p.Hin + sy) * p.Win + sx) * p.lda + (((lane & 7) ^ ((px >> 1) & 7)) * 8)
               : nullptr;
   };
   auto setup = [&] __attribute__((always_inline)) (int tile) {
@@ -183,7 +201,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       if (w < 4) {
 #pragma unroll
         for (int i = 0; i < PER_B; ++i) b_row[i] = b_src(i);
-      } else {
+      } else if constexpr (!PSRC_RE) {
 #pragma unroll
         for (int i = 0; i < P_I; ++i) p_src[i] = p_src_of(i);
       }
@@ -206,7 +224,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     for (int i = 0; i < P_I; ++i) {
       const int j = p_row(i);
       if (PT || j < P_TOT) {
-        const T* src = PT ? p_src_of(i) : p_src[PT ? 0 : i];
+        const T* src = PSRC_RE ? p_src_of(i) : p_src[PSRC_RE ? 0 : i];
         const void* s = src ? (const void*)(src + c * 64) : (const void*)g_zero_halo;
         __builtin_amdgcn_global_load_lds(s, LDS_PTR(dst + j * 1024), 16, 0, 0);
       }
@@ -240,7 +258,8 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     for (int it = 0; it < IT; ++it) {
       const int e = e0 + tid + it * 512;
       const int pix = e >> 3;
-      if (e < e1) xs[it] = *(const V8*)(buf + pix * 128 + ((lc ^ ((pix >> 1) & 7)) << 4));
+      const int pxs = pix - (pix / PW) * PW;
+      if (e < e1) xs[it] = *(const V8*)(buf + pix * 128 + ((lc ^ ((pxs >> 1) & 7)) << 4));
     }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -257,7 +276,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
           if (silu) f = silu_f(f);
           y[i] = ok ? (T)f : (T)0.f;
         }
-        *(V8*)(buf + pix * 128 + ((lc ^ ((pix >> 1) & 7)) << 4)) = y;
+        *(V8*)(buf + pix * 128 + ((lc ^ ((px >> 1) & 7)) << 4)) = y;
       }
     }
   };
@@ -269,7 +288,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const int pix = (wm * MT + mi + ky) * PW + fr + kx;
-      af[mi] = *(const V8*)(pa + pix * 128 + ((ch ^ ((pix >> 1) & 7)) << 4));
+      af[mi] = *(const V8*)(pa + pix * 128 + ((ch ^ (((fr + kx) >> 1) & 7)) << 4));
     }
 #pragma unroll
     for (int ni = 0; ni < NT; ++ni) {
@@ -324,6 +343,68 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   }
 
   V8 a0[MT], b0[NT], a1[MT], b1[NT];
+  if constexpr (CT) {
+    // ---- the K loop with cheap LDS read addresses.  With the column-only patch swizzle, fragment (mi, tap (ky, kx),
+    // K half h) sits at  la(kx, h) + [chunk buffer + (wm * MT + ky) * PW * 128] + mi * PW * 128  with
+    //   la(kx, h) = (fr + kx) * 128 + chunk slot ((h * 4 + fg) ^ ((fr + kx) >> 1 & 7))
+    // and the weights at lb(h) + rb * STAGE + ni * 2048 (r = wn * WN + fr; ni * 16 rows keep r >> 1 & 7): per half
+    // step one lane base (five VALU), two adds of a wave-uniform offset, and immediates -- the generic read_frags spends
+    // ~50 VALU per half step on the swizzled addresses, which made the loop VALU-issue-bound (r05 counters:
+    // 132 VALU per 32 MFMAs).  Same schedule, waits, DMA and GroupNorm pieces, same per-element K order.
+    // (the A lane base is recomputed per half step from the wave-uniform kx -- five VALU: a select among held bases
+    // is turned by the compiler into a lookup table in scratch, whose vmcnt wait would also wait out the DMA)
+    const int rr = wn * WN + fr;
+    const int lb0 = RING + rr * 128 + (((0 * 4 + fg) ^ ((rr >> 1) & 7)) << 4);
+    const int lb1 = RING + rr * 128 + (((1 * 4 + fg) ^ ((rr >> 1) & 7)) << 4);
+    auto rd = [=] __attribute__((always_inline)) (int c, int t, int rb, auto hcc, V8 (&af)[MT], V8 (&bf)[NT]) {
+      constexpr int H = decltype(hcc)::value;
+      const int ky = t / 3, kx = t - (t / 3) * 3;  // wave-uniform
+      const int px = fr + kx;
+      const int la = px * 128 + (((H * 4 + fg) ^ ((px >> 1) & 7)) << 4);
+      const int lboff_h = H ? lb1 : lb0;
+      const unsigned char* pa = smem + ((c & 1) * PBUF + (wm * MT + ky) * (PW * 128)) + la;
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) af[mi] = *(const V8*)(pa + mi * (PW * 128));
+      const unsigned char* sb = smem + rb * STAGE + lboff_h;
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) bf[ni] = *(const V8*)(sb + ni * 2048);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    rd(cb, 0, 0, I0(), a0, b0);
+    int c = cb, t = 0, rb = 0;
+    for (int s = 0; s < nsteps - 1; ++s) {
+      rd(c, t, rb, I1(), a1, b1);
+      mma(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (w < 4) wait_b(min(NS - 2, nsteps - 2 - s));  // stage s + 1 landed
+      else if (t == TR) hvm<0>();                      // chunk c + 1's patch landed
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+      if (w < 4) {
+        if (s + NS < nsteps) stage_b(s + NS, rb);
+      } else if (t == NTAP - 1 && c + 2 < ce) {
+        stage_p(c + 2);  // buffer c & 1: its last reads (this step's half 1) are behind the barrier
+      }
+      const int tc = (GNI && t >= TR && t < NTAP - 1 && c + 1 < ce) ? c + 1 : -1, tp = t - TR;
+      rb = rb == NS - 1 ? 0 : rb + 1;
+      if (t == NTAP - 1) {
+        ++c;
+        t = 0;
+      } else {
+        ++t;
+      }
+      rd(c, t, rb, I0(), a0, b0);
+      mma(a1, b1);
+      if (GNI && tc >= 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        transform(tc, tp, std::integral_constant<int, NPART>());
+      }
+    }
+    rd(c, t, rb, I1(), a1, b1);
+    mma(a0, b0);
+    mma(a1, b1);
+  } else {
   read_frags(cb, 0, 0, 0, a0, b0);
   int c = cb, t = 0, rb = 0;
   for (int s = 0; s < nsteps - 1; ++s) {
@@ -359,6 +440,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   read_frags(c, t, rb, 1, a1, b1);
   mma(a0, b0);
   mma(a1, b1);
+  }  // generic K loop
 
   if constexpr (PT) {
     // ---- PT epilogue: thread tid owns the 8-column vector cv of row rr of each 32-row pass.  This tile's bias and

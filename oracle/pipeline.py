@@ -30,8 +30,9 @@ def run_pipeline(unet, vae, denoise_encoder, lr_img, prompt_embeds, negative_pro
                  original_size=None, start_point="lr", guidance_rescale=0.0, add_sample=True,
                  decode=True, step_callback=None, eps_callback=None):
     """Returns dict(latents=final fp32 latent (1,4,h,w), image=decoded (1,3,H,W) or None).
-    ``eps_callback(i, n, x, eps)`` sees every tile's step input ``x`` (before scale_model_input) and the guided
-    noise prediction ``eps`` the Euler step consumes (the teacher-forced per-step pins)."""
+    ``eps_callback(i, n, x, eps, eps_raw)`` sees every tile's step input ``x`` (before scale_model_input), the UNet's
+    own noise prediction ``eps_raw`` (CFG rows [uncond, cond]) and the guided ``eps`` the Euler step consumes (the
+    teacher-forced per-step pins)."""
     _, _, H, W = lr_img.shape
     original_size = original_size or (H, W)
     target_size = target_size or (H, W)
@@ -66,13 +67,14 @@ def run_pipeline(unet, vae, denoise_encoder, lr_img, prompt_embeds, negative_pro
             eps = unet(xin, t, ctx if do_cfg else ctx[1:], {"text_embeds": text if do_cfg else text[1:],
                                                               "time_ids": tid}, input_embedding=cin,
                        add_sample=add_sample)
+            eps_raw = eps
             if do_cfg:
                 u, c_ = eps.chunk(2)
                 eps = u + guidance_scale * (c_ - u)
                 if guidance_rescale > 0.0:
                     eps = rescale_noise_cfg(eps, c_, guidance_rescale)
             if eps_callback is not None:
-                eps_callback(i, n, x, eps)
+                eps_callback(i, n, x, eps, eps_raw)
             outs.append(S.euler_step(eps, x, sigma, sigma_next))
         latents = tlc_lat.grids_inverse(torch.cat(outs, 0))
         if step_callback is not None:

@@ -7,9 +7,10 @@ Follows pipeline_FaithDiff_tlc.py:1187-1459 through oracle/pipeline.py:run_pipel
 tests/golden/c2/{c2_golden.npz, c2_image.png}: the latent after steps 1, 5, 10, 15 and 20 (fp32), the
 final decoded uint8 image, and the sha256 of the uint8 input image (the GPU test re-creates the input
 from the same seed and checks the hash first).  Also writes tests/golden/c2/c2_eps_golden.npz: the oracle's step
-input latent and guided noise prediction (after CFG, the eps the Euler step consumes) at steps 1, 10, 19 and 20 --
+input latent, the UNet's noise prediction (both CFG rows) and the guided one (after CFG, the eps the Euler step
+consumes) at steps 1, 10, 19 and 20 --
 the teacher-forced per-step eps pins of SURVEY 8(d) (tests/test_pipeline_gpu.py::test_c2_teacher_forced_eps).
-Run here (CPU, ~12 min on 8 cores):
+Run here (CPU, ~8 min on 8 cores):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_c2_golden.py
 """
@@ -67,10 +68,11 @@ def main():
 
     eps_kept = {}
 
-    def ecb(i, n, x, eps):
+    def ecb(i, n, x, eps, eps_raw):
         if i in EPS_STEPS:
             eps_kept[f"x_step{i + 1}"] = x.float().numpy().copy()
             eps_kept[f"eps_step{i + 1}"] = eps.float().numpy().copy()
+            eps_kept[f"unet_eps_step{i + 1}"] = eps_raw.float().numpy().copy()
 
     t0 = time.time()
     ref = run_pipeline(ru, rv, re_, x, c["pe"], c["npe"], c["ppe"], c["nppe"], c["noise"], c["post"],

@@ -321,3 +321,29 @@ def test_upsample_conv_in_four_phases(nimg, H, W, C, Cout, dt):
         assert rel_l2(a1[:nimg * Cout].cpu(), a2[:nimg * Cout].cpu()) < 1e-5
     else:
         assert H % 16 or W % 16  # statistics are written for whole tiles
+
+
+def test_short_rowbias_or_residual_is_refused_on_the_device_path():
+    """fd_gemm_params.rowbias_rows / residual_rows through the product host layer (ops.conv3x3 / ops.gemm fill them
+    from the tensors' extents): a time-embedding table with fewer rows than images, or a residual one row short, is
+    FD_ERR_SHAPE -> RuntimeError before any launch; the exact-size tables run."""
+    from fdhip import ops
+    nimg, H, W, C = 2, 23, 33, 320
+    x, w, b = _inputs(nimg, H, W, C, C, torch.bfloat16, seed=31)
+    with _knobs(FD_CONV_HALO_MIN_TILES=1):
+        wp = ops.pack_conv3x3(w.float()).to(DEV, torch.bfloat16)
+        xs, bd = _nhwc(x).to(DEV), b.float().to(DEV)
+        temb = torch.randn(nimg, C, device=DEV)
+        res = torch.randn(nimg * H * W, C, device=DEV).to(torch.bfloat16)
+        with pytest.raises(RuntimeError):
+            ops.conv3x3(xs, wp, bd, nimg, H, W, rowbias=temb[:1].contiguous())
+        with pytest.raises(RuntimeError):
+            ops.conv3x3(xs, wp, bd, nimg, H, W, residual=res[:-1])
+        a = torch.randn(64, 128, device=DEV).to(torch.bfloat16)
+        wt = torch.randn(160, 128, device=DEV).to(torch.bfloat16)
+        with pytest.raises(RuntimeError):
+            ops.gemm(a, wt, residual=torch.zeros(63, 160, device=DEV, dtype=torch.bfloat16))
+        y = ops.conv3x3(xs, wp, bd, nimg, H, W, rowbias=temb, residual=res)
+        g = ops.gemm(a, wt, residual=torch.zeros(64, 160, device=DEV, dtype=torch.bfloat16))
+    torch.cuda.synchronize()
+    assert torch.isfinite(y.float()).all() and g.shape == (64, 160)
