@@ -645,8 +645,41 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   const int G = BN / cpg, TPG = gn ? 512 / G : 512;
   const int gg = tid / TPG, gj = tid - (tid / TPG) * TPG;
   float gs = 0.f, gq = 0.f;
-#pragma unroll 1
-  for (int half = 0; half < BM / EROWS; ++half) {
+  // the residual rows of the whole tile requested before the first staging barrier: their memory round trip (HBM at
+  // the VAE's 1024^2 level) overlaps the staging instead of being paid once per 512-vector pass (the passes were a
+  // run-time loop, each waiting for its own loads; r05).  Only the VAE's 256 x 128 tiles: on the UNet's 160-column
+  // tiles the unrolled passes measured 1-2 % slower, so those keep the run-time loop and load in place.
+  constexpr int EIT = (EROWS * VPR + 511) / 512, NHALF = BM / EROWS;
+  constexpr bool EPF = TH == 16 && BN == 128;
+  constexpr int EU_H = EPF ? NHALF : 1, EU_I = EPF ? EIT : 1;
+  auto epi_row = [&] __attribute__((always_inline)) (int half, int e, int& cv, bool& ok, long long& m) {
+    const int r = e / VPR;
+    cv = e - r * VPR;
+    const int rt = half * EROWS + r;
+    const int oy = y0 + (rt >> 4), ox = x0 + (rt & 15);
+    ok = oy < Hg && ox < Wg;
+    m = PH ? ((long long)img * Ho + 2 * oy + pha) * Wo + 2 * ox + phb : ((long long)img * Ho + oy) * Wo + ox;
+  };
+  TO8 resv[EU_H][EU_I];
+  if (EPF && R) {
+#pragma unroll
+    for (int hh = 0; hh < NHALF; ++hh)
+#pragma unroll
+      for (int it = 0; it < EIT; ++it) {
+        const int e = tid + it * 512;
+        if ((EROWS * VPR) % 512 == 0 || e < EROWS * VPR) {
+          int cv;
+          bool ok;
+          long long m;
+          epi_row(hh, e, cv, ok, m);
+          if constexpr (EPF) {
+            if (ok) resv[hh][it] = *(const TO8*)(R + m * p.ldr + n0 + cv * 8);
+          }
+        }
+      }
+  }
+#pragma unroll EU_H
+  for (int half = 0; half < NHALF; ++half) {
     __syncthreads();  // the ring / patches (half 0) or the previous half's staging (half 1) fully consumed
     if ((wm * WM) / EROWS == half) {
 #pragma unroll
@@ -661,13 +694,15 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       }
     }
     __syncthreads();
-#pragma unroll 1
-    for (int e = tid; e < EROWS * VPR; e += 512) {
-      const int r = e / VPR, cv = e - (e / VPR) * VPR;
-      const int rt = half * EROWS + r;
-      const int oy = y0 + (rt >> 4), ox = x0 + (rt & 15);
-      const bool ok = oy < Hg && ox < Wg;
-      const long long m = PH ? ((long long)img * Ho + 2 * oy + pha) * Wo + 2 * ox + phb : ((long long)img * Ho + oy) * Wo + ox;
+#pragma unroll EU_I
+    for (int it = 0; it < EIT; ++it) {
+      const int e = tid + it * 512;
+      if ((EROWS * VPR) % 512 != 0 && e >= EROWS * VPR) break;
+      const int r = e / VPR;
+      int cv;
+      bool ok;
+      long long m;
+      epi_row(half, e, cv, ok, m);
       const int n = n0 + cv * 8;
       float v[8], bv[8], rv[8];
       TO8 res;
@@ -685,7 +720,10 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
         *(f32x4*)&rv[0] = *(const f32x4*)rr;
         *(f32x4*)&rv[4] = *(const f32x4*)(rr + 4);
       }
-      if (R && ok) res = *(const TO8*)(R + m * p.ldr + n);
+      if (R && ok) {
+        if constexpr (EPF) res = resv[half][it];
+        else res = *(const TO8*)(R + m * p.ldr + n);
+      }
       if (bias) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) v[i] += bv[i];
