@@ -568,68 +568,64 @@ extern "C" int fd_flash_attn_mx(const void* q, long long ldq, long long qbs, con
 // ------------------------------------------------------------------------------------------------
 // flash_attn_d512: single-head d = 512 attention of the VAE mid block (diffusers Attention with one head of 512
 // channels and upcast softmax; pipeline_FaithDiff_tlc.py:1436-1442 decodes through it, T = 16384 at 1024^2) --
-// the [T, T] score and probability matrices (1.5 GB at T = 16384) are never formed.  One workgroup = 4 waves x
+// the [T, T] score and probability matrices (1.5 GB at T = 16384) are never formed.  One workgroup = NW waves x
 // 16 queries; K / V tiles of 32 keys x 512 (32 KB each) double-buffered in LDS by global_load_lds (128 KB: one
-// workgroup per CU, one wave per SIMD, 512 VGPRs).  Per tile and wave: S^T = K Q^T (32 MFMAs, Q fragments held
-// in 64 VGPRs), online softmax in fp32 (one query per lane column, as flash_attn_d64), O^T += V^T P^T (32 MFMAs,
-// O^T in 128 VGPRs, V^T fragments by ds_read_b64_tr_b16), denominators on the MFMA pipe (ones . P^T).
+// workgroup per CU).  Per tile and wave: S^T = K Q^T (32 MFMAs, Q fragments held in 64 VGPRs), online softmax in
+// fp32 (one query per lane column, as flash_attn_d64), O^T += V^T P^T (32 MFMAs, O^T in 128 VGPRs, V^T fragments by
+// ds_read_b64_tr_b16), denominators on the MFMA pipe (ones . P^T).
 // LDS rows are 1024 B, so both tiles are XOR-swizzled at the source (K: 16-B chunk ^ (row & 15) for the 16-row
 // ds_read_b128 fragments; V: chunk ^ 2 (row & 7) for the 8-row transposed reads) -- conflict-free reads.
-template <typename T>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) flash_attn_d512_kernel(
-    const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V, long long ld, long long bs,
-    T* __restrict__ O, long long ldo, long long obs, int L, float scale_log2) {
+// What bounds it: every workgroup streams the image's whole K and V (32 MB at T = 16384) through its CU, one 64-KB
+// tile in flight -- ~30 GB/s per CU from the Infinity Cache, not the MFMAs.  NW = 8 (two waves per SIMD, 128
+// queries per tile fetch) halves the bytes per flop; the keys are then split over `ks` workgroups per query block
+// (so the grid still covers the CUs), each writing its O / l in fp32 and its log2-sum-exp to `part`, and
+// flash_d512_combine_kernel merges the splits in split order (r05).
+template <typename T, int NW, int QPW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4)))
+flash_attn_d512_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T* __restrict__ V, long long ld,
+                       long long bs, T* __restrict__ O, long long ldo, long long obs, int L, float scale_log2,
+                       float* __restrict__ part, int ks, int nbatch) {
   typedef typename VecT<T>::v8 V8;
   constexpr int KT = 32;            // keys per tile
   constexpr int TB = KT * 1024;     // bytes of one K (or V) tile in LDS
+  constexpr int QB = 16 * NW * QPW; // queries per workgroup (QPW groups of 16 per wave)
+  constexpr int RPW = KT / NW;      // K / V rows each wave stages per tile
+  constexpr int JG = NW == 8 ? 4 : 8;  // V^T d-blocks read per LDS wait (VGPR budget at two waves per SIMD)
   __shared__ __attribute__((aligned(1024))) unsigned char smem[4 * TB];  // [buf][K | V]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nq = (L + 63) / 64;
-  const int qblk = blockIdx.x % nq, b = blockIdx.x / nq;
+  const int nq = (L + QB - 1) / QB;
+  const int h = blockIdx.x % ks, qb = blockIdx.x / ks;
+  const int qblk = qb % nq, b = qb / nq;
   const T* Qb = Q + (long long)b * bs;
   const T* Kb = K + (long long)b * bs;
   const T* Vb = V + (long long)b * bs;
-  const int q0 = qblk * 64 + wave * 16;
+  const int q0 = qblk * QB + wave * 16 * QPW;
   const int fr = lane & 15, fg = lane >> 4;
-
-  V8 qf[16];  // B operand: Q[q0 + fr][32 ds + 8 fg .. +7]
-  {
-    const int q = min(q0 + fr, L - 1);
-#pragma unroll
-    for (int ds = 0; ds < 16; ++ds) qf[ds] = *(const V8*)(Qb + (long long)q * ld + ds * 32 + fg * 8);
-  }
-  // DMA: wave w stages K / V rows r = w + 4 i (i < 8); lane l fills LDS chunk l of the row with source chunk
-  // l ^ swz(r) (the swizzle is an involution on 0..63)
-  unsigned koff[8], voff[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = wave + 4 * i;
-    koff[i] = (unsigned)((r * ld + ((lane ^ (r & 15)) * 8)) * sizeof(T));
-    voff[i] = (unsigned)((r * ld + ((lane ^ (2 * (r & 7))) * 8)) * sizeof(T));
-  }
   const int nt = (L + KT - 1) / KT;
+  const int nts = (nt + ks - 1) / ks;
+  const int t0 = h * nts, t1 = min(nt, t0 + nts);
+
+  V8 qf[QPW][16];  // B operand: Q[q0 + 16 u + fr][32 ds + 8 fg .. +7]
+#pragma unroll
+  for (int u = 0; u < QPW; ++u) {
+    const int q = min(q0 + 16 * u + fr, L - 1);
+#pragma unroll
+    for (int ds = 0; ds < 16; ++ds) qf[u][ds] = *(const V8*)(Qb + (long long)q * ld + ds * 32 + fg * 8);
+  }
+  // DMA: wave w stages K / V rows r = w + NW i (i < RPW); lane l fills LDS chunk l of the row with source chunk
+  // l ^ swz(r) (the swizzle is an involution on 0..63)
   auto stage = [&](int t, int bi) {
     unsigned char* sk = smem + bi * 2 * TB;
     unsigned char* sv = sk + TB;
-    if (t * KT + KT <= L) {
-      const char* kt = (const char*)(Kb + (long long)t * KT * ld);
-      const char* vt = (const char*)(Vb + (long long)t * KT * ld);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        __builtin_amdgcn_global_load_lds((const void*)(kt + koff[i]), LDS_PTR(sk + (wave + 4 * i) * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(vt + voff[i]), LDS_PTR(sv + (wave + 4 * i) * 1024), 16, 0, 0);
-      }
-    } else {  // ragged last tile: rows past L re-read key L-1 (scored -inf)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = wave + 4 * i;
-        const long long key = min(t * KT + r, L - 1);
-        __builtin_amdgcn_global_load_lds((const void*)(Kb + key * ld + (lane ^ (r & 15)) * 8),
-                                         LDS_PTR(sk + r * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(Vb + key * ld + (lane ^ (2 * (r & 7))) * 8),
-                                         LDS_PTR(sv + r * 1024), 16, 0, 0);
-      }
+    for (int i = 0; i < RPW; ++i) {
+      const int r = wave + NW * i;
+      const long long key = min(t * KT + r, L - 1);  // ragged last tile: rows past L re-read key L-1 (scored -inf)
+      __builtin_amdgcn_global_load_lds((const void*)(Kb + key * ld + (lane ^ (r & 15)) * 8), LDS_PTR(sk + r * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Vb + key * ld + (lane ^ (2 * (r & 7))) * 8),
+                                       LDS_PTR(sv + r * 1024), 16, 0, 0);
     }
   };
   // lane-constant LDS read offsets.  K fragment (kb, ds): row kb*16 + fr, chunk (4 ds + fg) ^ fr =
@@ -645,115 +641,222 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     for (int j = 0; j < 8; ++j) vro[j] = r0 * 1024 + 32 * (j ^ (r0 & 7)) + 16 * (pp >> 1) + 8 * (pp & 1);
   }
 
-  f32x4 o[32];
+  f32x4 o[QPW][32], lsum[QPW];
+  float mrow[QPW];
 #pragma unroll
-  for (int i = 0; i < 32; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  f32x4 lsum = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float mrow = -INFINITY;
+  for (int u = 0; u < QPW; ++u) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) o[u][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    lsum[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    mrow[u] = -INFINITY;
+  }
   V8 ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (T)1.0f;
 
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int t = 0; t < nt; ++t) {
-    const int bi = t & 1;
-    if (t + 1 < nt) stage(t + 1, bi ^ 1);  // buffer bi^1 held tile t-1: every wave passed the barrier after it
+  if (t0 < t1) {
+    stage(t0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  for (int t = t0; t < t1; ++t) {
+    const int bi = (t - t0) & 1;
+    if (t + 1 < t1) stage(t + 1, bi ^ 1);  // buffer bi^1 held tile t-1: every wave passed the barrier after it
     const unsigned char* sk = smem + bi * 2 * TB;
-    f32x4 sc[2] = {(f32x4){0.f, 0.f, 0.f, 0.f}, (f32x4){0.f, 0.f, 0.f, 0.f}};
+    f32x4 sc[QPW][2];
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) sc[u][0] = sc[u][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int ds = 0; ds < 16; ++ds) {
-        const V8 kf = *(const V8*)(sk + kro[ds & 3] + 256 * (ds >> 2) + 16384 * kb);
-        sc[kb] = mfma16x16x32(kf, qf[ds], sc[kb]);
+        const V8 kf = *(const V8*)(sk + kro[ds & 3] + 256 * (ds >> 2) + 16384 * kb);  // one read, QPW MFMAs
+#pragma unroll
+        for (int u = 0; u < QPW; ++u) sc[u][kb] = mfma16x16x32(kf, qf[u][ds], sc[u][kb]);
       }
-    if (t * KT + KT > L) {
+    V8 pf[QPW];
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) {
+      if (t * KT + KT > L) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (t * KT + kb * 16 + fg * 4 + i >= L) sc[u][kb][i] = -INFINITY;
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[u][kb][i]);
+      mx = xor_max_16_32(mx);
+      const float mnew = fmaxf(mrow[u], mx * scale_log2);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (t * KT + kb * 16 + fg * 4 + i >= L) sc[kb][i] = -INFINITY;
+          pf[u][kb * 4 + i] = (T)__builtin_amdgcn_exp2f(fmaf(sc[u][kb][i], scale_log2, -mnew));
+      if (__any(mnew != mrow[u])) {  // exact skip when no query of this group raised its running max
+        const float alpha = __builtin_amdgcn_exp2f(mrow[u] - mnew);
+        lsum[u] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) o[u][i] *= alpha;
+      }
+      mrow[u] = mnew;
     }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[kb][i]);
-    mx = xor_max_16_32(mx);
-    const float mnew = fmaxf(mrow, mx * scale_log2);
-    V8 pf;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) pf[kb * 4 + i] = (T)__builtin_amdgcn_exp2f(fmaf(sc[kb][i], scale_log2, -mnew));
-    if (__any(mnew != mrow)) {  // exact skip when no query of this wave raised its running max
-      const float alpha = __builtin_amdgcn_exp2f(mrow - mnew);
-      lsum *= alpha;
-#pragma unroll
-      for (int i = 0; i < 32; ++i) o[i] *= alpha;
-    }
-    mrow = mnew;
-    // O^T += V^T P^T in four groups of 8 d-blocks (transposed V reads by inline asm: the builtin makes hipcc
-    // drain vmcnt(0) -- the next tile's DMA -- in front of it)
+    // O^T += V^T P^T in groups of JG d-blocks (transposed V reads by inline asm: the builtin makes hipcc drain
+    // vmcnt(0) -- the next tile's DMA -- in front of it); each V^T fragment feeds QPW MFMAs
     const unsigned vb = (unsigned)(unsigned long)LDS_PTR(smem + bi * 2 * TB + TB);
 #pragma unroll
-    for (int dg = 0; dg < 4; ++dg) {
-      s16x4 vtr[8][2];
+    for (int dg = 0; dg < 4; ++dg)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[j][0]) : "v"(vb + vro[j]), "i"(256 * dg));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[j][1]) : "v"(vb + vro[j]),
-                     "i"(256 * dg + 16384));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
+      for (int jh = 0; jh < 8 / JG; ++jh) {
+        s16x4 vtr[JG][2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        typedef __attribute__((ext_vector_type(8))) short s16x8;
-        const s16x4 lo = vtr[j][0], hi = vtr[j][1];
-        const s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[dg * 8 + j] = mfma16x16x32(__builtin_bit_cast(V8, w), pf, o[dg * 8 + j]);
+        for (int jj = 0; jj < JG; ++jj) {
+          const int j = jh * JG + jj;
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[jj][0]) : "v"(vb + vro[j]), "i"(256 * dg));
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vtr[jj][1]) : "v"(vb + vro[j]),
+                       "i"(256 * dg + 16384));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jj = 0; jj < JG; ++jj) {
+          typedef __attribute__((ext_vector_type(8))) short s16x8;
+          const s16x4 lo = vtr[jj][0], hi = vtr[jj][1];
+          const s16x8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int u = 0; u < QPW; ++u)
+            o[u][dg * 8 + jh * JG + jj] = mfma16x16x32(__builtin_bit_cast(V8, w), pf[u], o[u][dg * 8 + jh * JG + jj]);
+        }
       }
-    }
-    lsum = mfma16x16x32(ones, pf, lsum);
-    if (t + 1 < nt) {
+#pragma unroll
+    for (int u = 0; u < QPW; ++u) lsum[u] = mfma16x16x32(ones, pf[u], lsum[u]);
+    if (t + 1 < t1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 landed
       __builtin_amdgcn_s_waitcnt(0xc07f);                // this wave's reads of tile t retired
       __builtin_amdgcn_s_barrier();
     }
   }
-  // lane holds O^T[d = 16 db + 4 fg + j][q = q0 + fr]
-  const int q = q0 + fr;
-  if (q < L) {
-    const float inv = 1.0f / lsum[0];
-    T* orow = O + (long long)b * obs + (long long)q * ldo;
-    typedef __attribute__((ext_vector_type(4))) T T4;
+  // lane holds O^T[d = 16 db + 4 fg + j][q = q0 + 16 u + fr]
 #pragma unroll
-    for (int db = 0; db < 32; ++db) {
-      T4 w;
+  for (int u = 0; u < QPW; ++u) {
+    const int q = q0 + 16 * u + fr;
+    if (q >= L) continue;
+    const float inv = lsum[u][0] > 0.f ? 1.0f / lsum[u][0] : 0.f;
+    if (!part) {
+      T* orow = O + (long long)b * obs + (long long)q * ldo;
+      typedef __attribute__((ext_vector_type(4))) T T4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = (T)(o[db][j] * inv);
-      *(T4*)(orow + db * 16 + fg * 4) = w;
+      for (int db = 0; db < 32; ++db) {
+        T4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (T)(o[u][db][j] * inv);
+        *(T4*)(orow + db * 16 + fg * 4) = w;
+      }
+      continue;
     }
+    // split partial: O / l (fp32) and log2(sum_j 2^(s_j scale_log2)) = m + log2(l) (-inf for an empty key range)
+    const long long row = ((long long)b * ks + h) * L + q;
+    float* prow = part + row * 512;
+#pragma unroll
+    for (int db = 0; db < 32; ++db) *(f32x4*)(prow + db * 16 + fg * 4) = o[u][db] * inv;
+    if (fg == 0)
+      part[(long long)nbatch * ks * L * 512 + row] = lsum[u][0] > 0.f ? mrow[u] + __log2f(lsum[u][0]) : -INFINITY;
   }
+}
+
+// Merge of the key splits: O = sum_h w_h (O_h / l_h) / sum_h w_h with w_h = 2^(lse_h - max_h lse_h), in split
+// order.  64 threads per output row, 8 channels each.
+template <typename T>
+__global__ void __launch_bounds__(256) flash_d512_combine_kernel(const float* __restrict__ part, int ks, int nbatch,
+                                                                 int L, T* __restrict__ O, long long ldo,
+                                                                 long long obs) {
+  const long long rr = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (rr >= (long long)nbatch * L) return;
+  const int b = (int)(rr / L), q = (int)(rr - (long long)b * L);
+  const int c = (threadIdx.x & 63) * 8;
+  const float* lse = part + (long long)nbatch * ks * L * 512;
+  float mx = -INFINITY;
+  for (int h = 0; h < ks; ++h) mx = fmaxf(mx, lse[((long long)b * ks + h) * L + q]);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, den = 0.f;
+  for (int h = 0; h < ks; ++h) {
+    const long long row = ((long long)b * ks + h) * L + q;
+    const float w = __builtin_amdgcn_exp2f(lse[row] - mx);  // 0 for an empty split (lse -inf)
+    const f32x4 v0 = *(const f32x4*)(part + row * 512 + c), v1 = *(const f32x4*)(part + row * 512 + c + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc[j] = fmaf(w, v0[j], acc[j]);
+      acc[4 + j] = fmaf(w, v1[j], acc[4 + j]);
+    }
+    den += w;
+  }
+  const float inv = 1.0f / den;
+  typedef typename VecT<T>::v8 V8;
+  V8 out;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = (T)(acc[j] * inv);
+  *(V8*)(O + (long long)b * obs + (long long)q * ldo + c) = out;
+}
+
+static int d512_check(const void* q, const void* k, const void* v, long long ld, long long bs, const void* o,
+                      long long ldo, long long obs, int batch, int L) {
+  if (!q || !k || !v || !o) return FD_ERR_ARG;
+  if (batch <= 0 || L <= 0 || (long long)batch * ((L + 63) / 64) * 8 > 0x7fffffff) return FD_ERR_SHAPE;
+  if ((ld & 7) || (ldo & 3) || ld < 512 || ldo < 512 || (bs & 7) || (obs & 3)) return FD_ERR_SHAPE;
+  if ((((unsigned long long)q) | ((unsigned long long)k) | ((unsigned long long)v)) & 15) return FD_ERR_ARG;
+  if (((unsigned long long)o) & 7) return FD_ERR_ARG;
+  return FD_OK;
 }
 
 extern "C" int fd_flash_attn_d512(const void* q, const void* k, const void* v, long long ld, long long bs, void* o,
                                   long long ldo, long long obs, int batch, int L, float scale, int dtype,
                                   void* stream) {
-  if (!q || !k || !v || !o) return FD_ERR_ARG;
-  if (batch <= 0 || L <= 0 || (long long)batch * ((L + 63) / 64) > 0x7fffffff) return FD_ERR_SHAPE;
-  if ((ld & 7) || (ldo & 3) || ld < 512 || ldo < 512 || (bs & 7) || (obs & 3)) return FD_ERR_SHAPE;
-  if (32LL * ld * 2 > 0xffffffffLL) return FD_ERR_SHAPE;  // 32-bit DMA row offsets
-  if ((((unsigned long long)q) | ((unsigned long long)k) | ((unsigned long long)v)) & 15) return FD_ERR_ARG;
-  if (((unsigned long long)o) & 7) return FD_ERR_ARG;
+  const int rc = d512_check(q, k, v, ld, bs, o, ldo, obs, batch, L);
+  if (rc != FD_OK) return rc;
   dim3 grid((unsigned)(batch * ((L + 63) / 64))), block(256);
   const float sl2 = scale * 1.4426950408889634f;
-  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d512_kernel<T>), grid, block, 0, (hipStream_t)stream,
-                                          (const T*)q, (const T*)k, (const T*)v, ld, bs, (T*)o, ldo, obs, L, sl2));
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d512_kernel<T, 4, 1>), grid, block, 0, (hipStream_t)stream,
+                                          (const T*)q, (const T*)k, (const T*)v, ld, bs, (T*)o, ldo, obs, L, sl2,
+                                          (float*)nullptr, 1, batch));
   FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
+extern "C" int fd_flash_attn_d512_ksplit(int batch, int L) {
+  if (batch <= 0 || L <= 0) return 1;
+  const long long wgs = (long long)batch * ((L + 127) / 128);
+  const int nt = (L + 31) / 32;
+  int ks = 1;
+  while (ks < 8 && wgs * ks * 2 <= 320 && nt / (ks * 2) >= 4) ks *= 2;
+  return ks;
+}
+
+extern "C" int fd_flash_attn_d512_split(const void* q, const void* k, const void* v, long long ld, long long bs,
+                                        void* o, long long ldo, long long obs, int batch, int L, float scale,
+                                        int dtype, float* part, long long part_floats, int ks, void* stream) {
+  const int rc = d512_check(q, k, v, ld, bs, o, ldo, obs, batch, L);
+  if (rc != FD_OK) return rc;
+  if (ks < 1 || ks > 64) return FD_ERR_SHAPE;
+  if (ks > 1 && (!part || (((unsigned long long)part) & 15))) return FD_ERR_ARG;
+  if (ks > 1 && part_floats < (long long)batch * ks * L * 513) return FD_ERR_SHAPE;
+  if (ks > 1 && ((ldo & 7) || (obs & 7) || (((unsigned long long)o) & 15))) return FD_ERR_SHAPE;  // combine: 16-B rows
+  dim3 grid((unsigned)(batch * ((L + 127) / 128) * ks));
+  const float sl2 = scale * 1.4426950408889634f;
+  float* pp = ks > 1 ? part : (float*)nullptr;
+  // 8 waves x 16 queries (two waves per SIMD).  4 waves x 32 queries (QPW = 2: each K / V^T fragment read feeding
+  // two MFMAs) needs 256 O accumulators + 128 Q registers per wave and spills 78-388 VGPRs in either register form.
+  FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_attn_d512_kernel<T, 8, 1>), grid, dim3(512), 0, (hipStream_t)stream,
+                                          (const T*)q, (const T*)k, (const T*)v, ld, bs, (T*)o, ldo, obs, L, sl2, pp,
+                                          ks, batch));
+  FD_LAUNCH_CHECK();
+  if (ks > 1) {
+    dim3 g2((unsigned)(((long long)batch * L + 3) / 4)), b2(256);
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((flash_d512_combine_kernel<T>), g2, b2, 0, (hipStream_t)stream,
+                                            (const float*)part, ks, batch, L, (T*)o, ldo, obs));
+    FD_LAUNCH_CHECK();
+  }
   return FD_OK;
 }
 

@@ -30,6 +30,12 @@ __device__ __attribute__((aligned(256))) unsigned char g_zero_halo[256];
 #ifndef FD_HALO_CT
 #define FD_HALO_CT 1
 #endif
+// diagnostic builds only (-DFD_HALO_DIAG=m, wrong answers; 0 in the product), CT K loop: 1 = no DMA waits, 2 = no
+// MFMAs (fragments still read), 4 = no DMA issued after the prologue, 8 = no barriers, 16 = no fragment reads,
+// 32 = no K loop at all (prologue DMA + wait, epilogue)
+#ifndef FD_HALO_DIAG
+#define FD_HALO_DIAG 0
+#endif
 
 namespace {
 
@@ -358,6 +364,13 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     const int lb1 = RING + rr * 128 + (((1 * 4 + fg) ^ ((rr >> 1) & 7)) << 4);
     auto rd = [=] __attribute__((always_inline)) (int c, int t, int rb, auto hcc, V8 (&af)[MT], V8 (&bf)[NT]) {
       constexpr int H = decltype(hcc)::value;
+      if constexpr ((FD_HALO_DIAG & 16) != 0) {
+#pragma unroll
+        for (int mi = 0; mi < MT; ++mi) asm volatile("v_mov_b32 %0, 0" : "=v"(af[mi][0]));
+#pragma unroll
+        for (int ni = 0; ni < NT; ++ni) asm volatile("v_mov_b32 %0, 0" : "=v"(bf[ni][0]));
+        return;
+      }
       const int ky = t / 3, kx = t - (t / 3) * 3;  // wave-uniform
       const int px = fr + kx;
       const int la = px * 128 + (((H * 4 + fg) ^ ((px >> 1) & 7)) << 4);
@@ -371,20 +384,35 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
+    constexpr int DG = FD_HALO_DIAG;
+    auto mmd = [&] __attribute__((always_inline)) (const V8 (&af)[MT], const V8 (&bf)[NT]) {
+      if constexpr (DG & 2) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+        for (int i = 0; i < NT; ++i) asm volatile("" ::"v"(bf[i]));
+      } else {
+        mma(af, bf);
+      }
+    };
     rd(cb, 0, 0, I0(), a0, b0);
     int c = cb, t = 0, rb = 0;
-    for (int s = 0; s < nsteps - 1; ++s) {
+    for (int s = 0; s < ((DG & 32) ? 0 : nsteps - 1); ++s) {
       rd(c, t, rb, I1(), a1, b1);
-      mma(a0, b0);
+      mmd(a0, b0);
       __builtin_amdgcn_sched_barrier(0);
-      if (w < 4) wait_b(min(NS - 2, nsteps - 2 - s));  // stage s + 1 landed
-      else if (t == TR) hvm<0>();                      // chunk c + 1's patch landed
+      if constexpr (!(DG & 1)) {
+        if (w < 4) wait_b(min(NS - 2, nsteps - 2 - s));  // stage s + 1 landed
+        else if (t == TR) hvm<0>();                      // chunk c + 1's patch landed
+      }
       __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_s_barrier();
-      if (w < 4) {
-        if (s + NS < nsteps) stage_b(s + NS, rb);
-      } else if (t == NTAP - 1 && c + 2 < ce) {
-        stage_p(c + 2);  // buffer c & 1: its last reads (this step's half 1) are behind the barrier
+      if constexpr (!(DG & 8)) __builtin_amdgcn_s_barrier();
+      if constexpr (!(DG & 4)) {
+        if (w < 4) {
+          if (s + NS < nsteps) stage_b(s + NS, rb);
+        } else if (t == NTAP - 1 && c + 2 < ce) {
+          stage_p(c + 2);  // buffer c & 1: its last reads (this step's half 1) are behind the barrier
+        }
       }
       const int tc = (GNI && t >= TR && t < NTAP - 1 && c + 1 < ce) ? c + 1 : -1, tp = t - TR;
       rb = rb == NS - 1 ? 0 : rb + 1;
@@ -395,15 +423,16 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
         ++t;
       }
       rd(c, t, rb, I0(), a0, b0);
-      mma(a1, b1);
+      mmd(a1, b1);
       if (GNI && tc >= 0) {
         __builtin_amdgcn_sched_barrier(0);
         transform(tc, tp, std::integral_constant<int, NPART>());
       }
     }
     rd(c, t, rb, I1(), a1, b1);
-    mma(a0, b0);
-    mma(a1, b1);
+    mmd(a0, b0);
+    mmd(a1, b1);
+    if constexpr ((DG & 1) != 0) hvm<0>();  // nothing in flight past the loop
   } else {
   read_frags(cb, 0, 0, 0, a0, b0);
   int c = cb, t = 0, rb = 0;

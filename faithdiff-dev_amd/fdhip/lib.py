@@ -77,6 +77,9 @@ _SIGS = {
     "fd_conv3x3_narrow_gn": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_int, c_vp]),
     "fd_flash_attn_d512": (c_int, [c_vp, c_vp, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_int, c_int, c_f, c_int, c_vp]),
+    "fd_flash_attn_d512_ksplit": (c_int, [c_int, c_int]),
+    "fd_flash_attn_d512_split": (c_int, [c_vp, c_vp, c_vp, c_ll, c_ll, c_vp, c_ll, c_ll, c_int, c_int, c_f, c_int, c_vp,
+                                         c_ll, c_int, c_vp]),
     "fd_mha_seq_axis": (c_int, [c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]),
     "fd_softmax_rows": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_f, c_int, c_vp]),
     "fd_xattn_consts": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_ll, c_ll, c_vp, c_int, c_int, c_int, c_f, c_vp, c_vp,

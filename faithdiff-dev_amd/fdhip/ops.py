@@ -762,9 +762,26 @@ def flash_attn(q, k, v, out, batch, heads, Lq, Lk, ldq, ldk, ldv, ldo, qbs, kbs,
     return out
 
 
-def flash_attn_d512(qkv, out, nimg, T, scale=512 ** -0.5):
-    """Single-head d=512 attention on the qkv projection [nimg*T, 1536] (q | k | v) -> out [nimg*T, 512]."""
+def flash_attn_d512(qkv, out, nimg, T, scale=512 ** -0.5, split=None):
+    """Single-head d=512 attention on the qkv projection [nimg*T, 1536] (q | k | v) -> out [nimg*T, 512].
+    split (default: the FD_D512_SPLIT path switch): the 8-wave kernel with the keys split over
+    fd_flash_attn_d512_ksplit(nimg, T) workgroups per 128-query block, merged by a second launch through an fp32
+    scratch of nimg * ks * T * 513 floats; else the 4-wave single-pass kernel."""
+    from . import knobs
     ld = qkv.stride(0)
+    if split is None:
+        split = knobs.get("FD_D512_SPLIT") != 0
+    if split:
+        lib = L.load()
+        ks = lib.fd_flash_attn_d512_ksplit(nimg, T)
+        nfl = nimg * ks * T * 513 if ks > 1 else 0
+        part = torch.empty(max(nfl, 4), dtype=torch.float32, device=qkv.device)
+        _timed("flash_attn_d512", 4.0 * nimg * T * T * 512, 0, label=f"flash512 n={nimg} T={T} ks={ks}",
+               launch=lambda: L.check(lib.fd_flash_attn_d512_split(
+                   L.ptr(qkv), L.ptr(qkv[:, 512:]), L.ptr(qkv[:, 1024:]), ld, T * ld, L.ptr(out), out.stride(0),
+                   T * out.stride(0), nimg, T, scale, L.dtype_code(qkv.dtype), L.ptr(part), nfl, ks, L.stream()),
+                   "fd_flash_attn_d512_split"))
+        return out
     _timed("flash_attn_d512", 4.0 * nimg * T * T * 512, 0, label=f"flash512 n={nimg} T={T}", launch=lambda: L.check(
         L.load().fd_flash_attn_d512(L.ptr(qkv), L.ptr(qkv[:, 512:]), L.ptr(qkv[:, 1024:]), ld, T * ld, L.ptr(out),
                                     out.stride(0), T * out.stride(0), nimg, T, scale, L.dtype_code(qkv.dtype),

@@ -294,6 +294,16 @@ int fd_mha_seq_axis(const void* qkv, void* o, int L, int groups, int N, int E, i
  * stride obs.  L may be any size (masked tail).  No [L, L] buffer is formed.  16-B aligned q/k/v, ld % 8 == 0. */
 int fd_flash_attn_d512(const void* q, const void* k, const void* v, long long ld, long long bs, void* o,
                        long long ldo, long long obs, int batch, int L, float scale, int dtype, void* stream);
+/* The same attention on 8-wave workgroups (128 queries per K/V tile fetch, half the operand bytes per flop of
+ * fd_flash_attn_d512) with the keys of each query block split over `ks` workgroups.  ks > 1: each split writes
+ * its O / l (fp32) and log2-sum-exp into `part` (>= batch * ks * L * 513 floats, 16-B aligned) and a second launch
+ * merges the splits in split order into o (then o, ldo and obs must be 16-B / 8-element aligned).  ks = 1 writes o
+ * directly and `part` may be NULL.  fd_flash_attn_d512_ksplit returns the split count the library plans for
+ * (batch, L): enough workgroups for the 256 CUs, at least 4 key tiles of 32 per split. */
+int fd_flash_attn_d512_ksplit(int batch, int L);
+int fd_flash_attn_d512_split(const void* q, const void* k, const void* v, long long ld, long long bs, void* o,
+                             long long ldo, long long obs, int batch, int L, float scale, int dtype, float* part,
+                             long long part_floats, int ks, void* stream);
 
 /* Row softmax of fp32 scores s[R][C] (scaled by `scale`) into p[R][ldp] (dtype).  With fd_gemm this forms
  * a materialised single-head attention (kept for head dims other than 512; the VAE uses fd_flash_attn_d512). */

@@ -55,7 +55,7 @@ def main():
     for k, (n, t) in by.items():
         kk = k.split()[0]
         kinds[kk] = round(kinds.get(kk, 0.0) + t, 3)
-    tag = {k: v for k, v in os.environ.items() if k.startswith(("FD_LIB", "FD_GN", "FD_GEMM", "AB_TAG"))}
+    tag = {k: v for k, v in os.environ.items() if k.startswith(("FD_LIB", "FD_GN", "FD_GEMM", "FD_D512", "AB_TAG"))}
     top = sorted(by.items(), key=lambda kv: -kv[1][1])[:12]
     print(json.dumps({**tag, "decode_ms_median": round(sorted(times)[4], 3), "decode_ms_min": round(min(times), 3),
                       "eager_kind_ms": kinds,

@@ -409,21 +409,46 @@ def test_tlc_grids_nhwc():
         assert torch.equal(out[2 * t + 1], cv[r:r + k, c:c + k])
 
 
+def _d512_ref(qkv, n, T, C=512):
+    x = qkv.float()
+    q, k, v = x[..., :C], x[..., C:2 * C], x[..., 2 * C:]
+    return F.scaled_dot_product_attention(q[:, None], k[:, None], v[:, None])[:, 0].reshape(n * T, C)
+
+
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("n,T", [(1, 4096), (2, 1000), (1, 77), (1, 16384)])
-def test_flash_attn_d512(dtype, n, T):
-    """fd_flash_attn_d512 (the VAE mid-block attention, one head of 512 channels) against fp32 SDPA on the same
-    qkv projection rows [q | k | v] (ld 1536), incl. ragged tails (T = 1000, 77) and the 1024^2 size (16384)."""
+def test_flash_attn_d512(dtype, n, T, split):
+    """fd_flash_attn_d512 (the VAE mid-block attention, one head of 512 channels; split: the 8-wave split-key form
+    fd_flash_attn_d512_split at the planned ks) against fp32 SDPA on the same qkv projection rows [q | k | v]
+    (ld 1536), incl. ragged tails (T = 1000, 77) and the 1024^2 size (16384)."""
     from fdhip import ops
     C = 512
     scale = 1.0 if T > 4096 else 2.0  # score spread: keep the softmax peaked enough to be a real test
     qkv = (rnd(n, T, 3 * C, dtype=torch.float32) * scale).to(dtype)
     o = torch.empty(n * T, C, dtype=dtype, device=DEV)
-    ops.flash_attn_d512(qkv.view(n * T, 3 * C), o, n, T)
-    x = qkv.float()
-    q, k, v = x[..., :C], x[..., C:2 * C], x[..., 2 * C:]
-    ref = F.scaled_dot_product_attention(q[:, None], k[:, None], v[:, None])[:, 0].reshape(n * T, C)
-    assert rel_l2(o, ref) < 1.5 * TOL[dtype], rel_l2(o, ref)
+    ops.flash_attn_d512(qkv.view(n * T, 3 * C), o, n, T, split=split)
+    assert rel_l2(o, _d512_ref(qkv, n, T)) < 1.5 * TOL[dtype], rel_l2(o, _d512_ref(qkv, n, T))
+
+
+@pytest.mark.parametrize("ks", [1, 2, 3, 5, 64])
+def test_flash_attn_d512_key_splits(ks):
+    """Every split count through the C ABI, incl. splits with no key tile (T = 300: 10 tiles, ks = 64 leaves most
+    splits empty: log2-sum-exp -inf, weight 0 in the merge), against fp32 SDPA; an undersized scratch is refused."""
+    from fdhip import lib as L
+    n, T, C = 2, 300, 512
+    qkv = (rnd(n, T, 3 * C, dtype=torch.float32) * 2.0).to(torch.float16)
+    o = torch.empty(n * T, C, dtype=torch.float16, device=DEV)
+    nfl = n * ks * T * 513
+    part = torch.empty(max(nfl, 4), dtype=torch.float32, device=DEV)
+    args = lambda nf: (L.ptr(qkv), L.ptr(qkv[..., 512:]), L.ptr(qkv[..., 1024:]), 3 * C, T * 3 * C, L.ptr(o), C,
+                       T * C, n, T, C ** -0.5, L.dtype_code(qkv.dtype), L.ptr(part), nf, ks, L.stream())
+    L.check(L.load().fd_flash_attn_d512_split(*args(nfl)), "fd_flash_attn_d512_split")
+    torch.cuda.synchronize()
+    assert rel_l2(o, _d512_ref(qkv, n, T)) < 1.5 * TOL[torch.float16]
+    if ks > 1:
+        assert L.load().fd_flash_attn_d512_split(*args(nfl - 1)) == -1  # FD_ERR_SHAPE
+    assert 1 <= L.load().fd_flash_attn_d512_ksplit(1, 16384) <= 8
 
 
 @pytest.mark.parametrize("nimg,H,W,Cin,Cout,up,expect", [
