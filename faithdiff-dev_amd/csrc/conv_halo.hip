@@ -102,7 +102,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   static_assert(!PH || (!GNI && !SK && !PT), "phase form: plain tiles only");
   constexpr int NTAP = PH ? 4 : 9;
   // lane-constant LDS read bases in the K loop (below): every tile form but the persistent and the phase ones
-  constexpr bool CT = !PT && !PH && FD_HALO_CT;
+  constexpr bool CT = !PH && FD_HALO_CT;
   static_assert(!PT || (!SK && BN == 128 && TH == 16 && PER * VPR == 512 && PT_END <= 163840 &&
                         PER * LDE * 4 >= 512 * 8),
                 "PT layout: one 8-column vector per thread per pass, red[] in the pass buffer");
@@ -160,21 +160,22 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     return Bw + (long long)(nb + row) * p.ldb + (((lane & 7) ^ ((row >> 1) & 7)) * 8);
   };
   auto p_row = [&] __attribute__((always_inline)) (int i) { return PT ? min((w - 4) + 4 * i, P_TOT - 1) : (w - 4) + 4 * i; };
-  auto p_src_of = [&] __attribute__((always_inline)) (int i) -> const T* {
+  auto p_src_at = [&] __attribute__((always_inline)) (int i, int img_, int y0_, int x0_) -> const T* {
     const int j = p_row(i);
     int pix = j * 8 + (lane >> 3);
     if constexpr (PSRC_RE) asm volatile("" : "+v"(pix));  // recomputed at each issue, never hoisted out of the loops
     const int py = pix / PW, px = pix - (pix / PW) * PW;
-    const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+    const int iy = y0_ - 1 + py, ix = x0_ - 1 + px;
     const bool ok = j < P_TOT && pix < PIX && iy >= 0 && iy < Hg && ix >= 0 && ix < Wg;
     int sy = iy, sx = ix;
     if (ups) {
       sy = up2 ? (iy >> 1) : (iy * p.Hin) / Ho;
       sx = up2 ? (ix >> 1) : (ix * p.Win) / Wo;
     }
-    return ok ? A + ((long long)(img * p.Hin + sy) * p.Win + sx) * p.lda + (((lane & 7) ^ ((px >> 1) & 7)) * 8)
+    return ok ? A + ((long long)(img_ * p.Hin + sy) * p.Win + sx) * p.lda + (((lane & 7) ^ ((px >> 1) & 7)) * 8)
               : nullptr;
   };
+  auto p_src_of = [&] __attribute__((always_inline)) (int i) -> const T* { return p_src_at(i, img, y0, x0); };
   auto setup = [&] __attribute__((always_inline)) (int tile) {
     // tile order: output-channel tiles outer (the ~32 workgroups an XCD holds share one weight panel in its L2).
     // PH: the 4 x Cout / BN column tiles come in groups of G whose weight panels fit together in ~2 MB of L2, the
@@ -224,13 +225,14 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       __builtin_amdgcn_global_load_lds((const void*)((PT ? b_src(i) : b_row[PT ? 0 : i]) + off),
                                        LDS_PTR(dst + (w + 4 * i) * 1024), 16, 0, 0);
   };
-  auto stage_p = [&] __attribute__((always_inline)) (int c) {  // patch of chunk c into buffer c & 1 (+ its affine table)
+  // patch of chunk c of the tile at (img_, y0_, x0_) into buffer c & 1 (+ its affine table; aff_: that tile's image)
+  auto stage_p_at = [&] __attribute__((always_inline)) (int c, int img_, int y0_, int x0_, const float* aff_) {
     unsigned char* dst = smem + (c & 1) * PBUF;
 #pragma unroll
     for (int i = 0; i < P_I; ++i) {
       const int j = p_row(i);
       if (PT || j < P_TOT) {
-        const T* src = PSRC_RE ? p_src_of(i) : p_src[PSRC_RE ? 0 : i];
+        const T* src = PSRC_RE ? p_src_at(i, img_, y0_, x0_) : p_src[PSRC_RE ? 0 : i];
         const void* s = src ? (const void*)(src + c * 64) : (const void*)g_zero_halo;
         __builtin_amdgcn_global_load_lds(s, LDS_PTR(dst + j * 1024), 16, 0, 0);
       }
@@ -238,9 +240,10 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     // 64 channels x (scale, shift) = 512 B; the upper half of the 1 KB is never read.  PT: every patch wave loads it
     // (identical bytes), for the uniform DMA count
     if (GNI && (PT || w == 4))
-      __builtin_amdgcn_global_load_lds((const void*)(aff + (long long)c * 128 + lane * 4), LDS_PTR(dst + PATCH), 16, 0,
+      __builtin_amdgcn_global_load_lds((const void*)(aff_ + (long long)c * 128 + lane * 4), LDS_PTR(dst + PATCH), 16, 0,
                                        0);
   };
+  auto stage_p = [&] __attribute__((always_inline)) (int c) { stage_p_at(c, img, y0, x0, aff); };
   // GroupNorm affine (+ SiLU) in place on patch buffer c & 1: y = silu(fma(x, a, b)) rounded to T (fd_group_norm's
   // bits), zero outside the image.  Each thread keeps one logical 8-channel slot (tid % 8) for every pixel.  Piece
   // `part` of `nparts` covers pixels [part * PIX / nparts, (part + 1) * PIX / nparts): the main loop transforms the
@@ -318,24 +321,43 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     else hvm<0>();
   };
 
-  // ---- prologue DMA: weight stages 0..NS-1, patches of chunks 0 and 1
-  auto prologue_dma = [&] __attribute__((always_inline)) () {
+  // ---- prologue DMA: weight stages 0..NS-1, patches of chunks 0 (unless skip0: already in flight) and 1
+  auto prologue_dma = [&] __attribute__((always_inline)) (bool skip0) {
     if (w < 4) {
 #pragma unroll
       for (int s0 = 0; s0 < NS; ++s0)
         if (s0 < nsteps) stage_b(s0, s0);
     } else {
-      stage_p(cb);
+      if (!skip0) stage_p(cb);
       if (cb + 1 < ce) stage_p(cb + 1);
     }
   };
+  // PT: the next tile's coordinates, so its chunk-0 patch can be DMA'd inside this tile's K loop (into patch buffer 0
+  // once this tile's last chunk pair has started: an even chunk count) -- at the VAE's 1024^2 level the patch comes
+  // from HBM, and fetched under the epilogue (the round-4 PT form) it still made every tile start on an HBM round
+  // trip in lockstep with every other CU (r05 diagnostics: prologue + epilogue alone 175 of 381 us)
+  constexpr int PCNT = P_I + (GNI ? 1 : 0);  // DMA instructions per patch wave and chunk (PT: uniform)
+  auto tile_xy = [&] __attribute__((always_inline)) (int tile, int& img_, int& y0_, int& x0_) {
+    const int nt_ = tile / nsp, sp_ = tile - nt_ * nsp;
+    img_ = sp_ / (tiles_y * tiles_x);
+    const int spi_ = sp_ - img_ * (tiles_y * tiles_x), ty_ = spi_ / tiles_x;
+    y0_ = ty_ * TH;
+    x0_ = (spi_ - ty_ * tiles_x) * 16;
+  };
   setup(tl);
-  prologue_dma();
+  prologue_dma(false);
+  bool pf_prev = false;  // PT: this tile's chunk 0 was DMA'd inside the previous tile's K loop
   for (bool first = true;; first = false) {
-  // PT after the first tile: the DMA went out under the previous tile's epilogue, whose 8 output stores (one per
-  // pass; wave 0 also the GroupNorm partial) are the only younger vector-memory operations
-  if (PT && !first) hvm<8>();
-  else if (w < 4) wait_b(min(nsteps, NS) - 1);
+  int nx_img = 0, nx_y0 = 0, nx_x0 = 0;
+  const bool pf_next = PT && !SK && tl + tl_step < tl_hi && ce % 2 == 0;
+  if (PT && pf_next) tile_xy(tl + tl_step, nx_img, nx_y0, nx_x0);
+  // PT after the first tile: the weight stages and chunk 1 went out after the previous tile's epilogue stores; a
+  // chunk 0 prefetched inside the previous K loop is older than those 8 stores (one per pass)
+  if (PT && !first) {
+    if (w < 4) hvm<(NS - 1) * PER_B>();
+    else if (pf_prev) hvm<PCNT + 8>();
+    else hvm<PCNT>();
+  } else if (w < 4) wait_b(min(nsteps, NS) - 1);
   else hvm<0>();
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -403,7 +425,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (!(DG & 1)) {
         if (w < 4) wait_b(min(NS - 2, nsteps - 2 - s));  // stage s + 1 landed
-        else if (t == TR) hvm<0>();                      // chunk c + 1's patch landed
+        else if (t == TR && c + 1 < ce) hvm<0>();        // chunk c + 1's patch landed
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       if constexpr (!(DG & 8)) __builtin_amdgcn_s_barrier();
@@ -412,6 +434,9 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
           if (s + NS < nsteps) stage_b(s + NS, rb);
         } else if (t == NTAP - 1 && c + 2 < ce) {
           stage_p(c + 2);  // buffer c & 1: its last reads (this step's half 1) are behind the barrier
+        } else if (PT && pf_next && t == NTAP - 1 && c + 2 == ce) {
+          // the next tile's chunk 0 into buffer 0 (c even): waited for at that tile's start
+          stage_p_at(0, nx_img, nx_y0, nx_x0, GNI ? (const float*)p.gi_affine + (long long)nx_img * Cin * 2 : nullptr);
         }
       }
       const int tc = (GNI && t >= TR && t < NTAP - 1 && c + 1 < ce) ? c + 1 : -1, tp = t - TR;
@@ -499,10 +524,6 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
     const int cimg = img, cspi = spi, cn0 = n0;
     lds_barrier();
     const int tl_next = tl + tl_step;
-    if (tl_next < tl_hi) {
-      setup(tl_next);
-      prologue_dma();
-    }
     T* __restrict__ C = (T*)p.C;
     float* ep = (float*)(smem + PT_EP);
     f32x4* const slots = (f32x4*)(smem + PT_SLOT);
@@ -587,6 +608,14 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
         ((float2*)p.gn_part)[blk * p.gn_groups + cn0 / cpg + tid] = make_float2(S, Q);
       }
     }
+    // the next tile's weight stages and chunk 1 (chunk 0 too unless the K loop prefetched it) only now: DMA issued
+    // before the passes made the compiler's waits for this tile's bias / residual registers wait for it as well
+    // (round 4: PT 2.3x slower on the residual convs)
+    if (tl_next < tl_hi) {
+      setup(tl_next);
+      prologue_dma(pf_next);
+    }
+    pf_prev = pf_next;
     tl = tl_next;
     if (tl >= tl_hi) return;
     continue;
@@ -841,8 +870,13 @@ int cu_count() {
 // The PT form: 256-row x 128-column tiles over whole images (every tile full: one store per thread and pass), at
 // least two chunks of input channels (the prologue DMA count the epilogue waits rely on), no per-image row bias,
 // and at least two tiles per CU (below that there is no next tile to overlap).  Returns its workgroup count.
+// FD_CONV_HALO_PT = 3 (default, "auto"): only the GroupNorm-folded convs without a residual -- the VAE 1024^2 resnet
+// conv1s, 470 -> 431 us with the next tile's chunk-0 patch DMA'd inside the K loop; the residual convs run 2.3x
+// slower in this form and the plain ones ~2 % slower (profiles/r05k_*)
 int halo_pt_grid(const fd_gemm_params* p, int th, int bn, int sk, long long tiles) {
-  if (!fd_knob(FDK_CONV_HALO_PT) || th != 16 || bn != 128 || sk || p->Cin < 128 || p->rowbias) return 0;
+  const int mode = fd_knob(FDK_CONV_HALO_PT);
+  if (!mode || (mode == 3 && (!p->gi_affine || p->residual))) return 0;
+  if (th != 16 || bn != 128 || sk || p->Cin < 128 || p->rowbias) return 0;
   if (p->Hout % 16 || p->Wout % 16) return 0;
   const int cus = cu_count();
   if (tiles < 2LL * cus || cus < 8) return 0;
@@ -912,6 +946,11 @@ int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
   const int min_tiles = fd_knob(FDK_CONV_HALO_MIN_TILES);
   int th = 0, sk = 0;
   if (tiles(16) >= min_tiles) th = 16;
+  // 256-row tiles with the input channels split over two workgroups before 128-row tiles: half the weight bytes per
+  // MFMA flop (the UNet's 64^2 level, whose 128-row tiles are bound by the weight stream into LDS, r05 diagnostics);
+  // from 640 input channels (K >= 5760): below that the pairwise hand-off costs more than it saves (320 -> 640:
+  // 42.7 -> 49.0 us; 1920 -> 640: 160 -> 145 us, profiles/r05i_conv_ab_split16_*.jsonl)
+  else if (fd_knob(FDK_CONV_HALO_SPLIT16) && p->Cin >= 640 && 2 * tiles(16) >= min_tiles) th = 16, sk = 1;
   else if (tiles(8) >= min_tiles) th = 8;
   else if (fd_knob(FDK_CONV_HALO_SPLIT) && p->Cin >= 128 && 2 * tiles(8) >= min_tiles) th = 8, sk = 1;
   if (!th || p->Wout < 16 || p->Hout < th) return 0;
@@ -923,7 +962,7 @@ int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
   pl->pt = halo_pt_grid(p, th, bn, sk, pl->tiles);
   // a 128-row tile's K step is half the MFMA work of a 256-row one: its weight stages need a deeper ring to cover
   // the L2 latency (the 256-row tile's LDS holds 3 stages at 160 columns, 4 at 128)
-  pl->ns = th == 8 ? fd_knob(FDK_CONV_HALO_NS8) : (bn == 128 && !pl->pt ? fd_knob(FDK_CONV_HALO_NS16) : 3);
+  pl->ns = th == 8 ? fd_knob(FDK_CONV_HALO_NS8) : (bn == 128 && !pl->pt && !sk ? fd_knob(FDK_CONV_HALO_NS16) : 3);
   if (g256 && !pl->pt) return 0;  // FD_CONV_HALO_PT = 2 takes a gemm256 conv only in the PT form
   return 1;
 }
@@ -979,6 +1018,8 @@ int launch_halo(const fd_gemm_params* p, const HaloPlan& pl, hipStream_t s) {
   FD_HALO(8, 128, 0, 3)
   FD_HALO(8, 160, 1, 3)
   FD_HALO(8, 128, 1, 3)
+  FD_HALO(16, 160, 1, 3)
+  FD_HALO(16, 128, 1, 3)
   FD_HALO(8, 160, 0, 5)
   FD_HALO(8, 128, 0, 5)
   FD_HALO(8, 160, 1, 5)

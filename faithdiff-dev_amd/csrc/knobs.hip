@@ -51,9 +51,11 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_GEMM8_W128", 1},          // gemm8 128 x 160 tiles on eight waves of 32 x 80 (0: four of 64 x 80)
     {"FD_GEMM8_LNP_K", 4096},      // least K of the LN-fold producers taken by the 128 x 160 pairwise split
     {"FD_XATTN_SPLIT", 0},         // cross-attention score GEMM: 128 x 160 tiles with K split in two
-    {"FD_CONV_HALO_PT", 0},        // halo conv persistent over tiles (next tile's DMA under the epilogue) for launches of
-                                   // >= 2 tiles per CU; 2: also the gemm256-eligible ones; 0: off
+    {"FD_CONV_HALO_PT", 3},        // halo conv persistent over tiles (next tile's chunk 0 DMA'd in the K loop) for launches
+                                   // of >= 2 tiles per CU: 3 GroupNorm-folded convs without residual, 1 all, 2 also the
+                                   // gemm256-eligible ones, 0 off
     {"FD_CONV_HALO_NS16", 3},      // weight-ring depth of its 256 x 128 tiles (3 or 4)
+    {"FD_CONV_HALO_SPLIT16", 1},   // 256-row tiles with a pairwise input-channel split before 128-row tiles
 };
 int g_knobs[FDK_COUNT];
 bool g_init = false;

@@ -646,13 +646,15 @@ def halo_conv_rows(x, wp, nimg, H, W, stride=1, pad=1, upsample=False, x2=None, 
     return int(L.load().fd_conv_halo_plan(ctypes.byref(p)))
 
 
-def halo_conv_pt(x, wp, nimg, H, W, upsample=False, upsample_size=None, residual=False, rowbias=False):
+def halo_conv_pt(x, wp, nimg, H, W, upsample=False, upsample_size=None, residual=False, rowbias=False, gn_in=False):
     """Workgroups of the halo kernel's persistent form for this conv (0: one workgroup per tile, or not the halo
-    kernel).  Shapes only."""
+    kernel).  Shapes only (gn_in: with a consumer GroupNorm folded into the staging)."""
     dummy = torch.empty((1, wp.shape[0]), dtype=x.dtype, device=x.device)
     p, _ = _conv_params(x, wp, None, nimg, H, W, 1, 1, upsample, None, None, dummy, None, None, "none", None,
                         upsample_size, None, 1.0)
     p.C, p.ldc = x.data_ptr(), wp.shape[0]
+    if gn_in:
+        p.gi_affine = x.data_ptr()
     if residual:
         p.residual, p.ldr, p.residual_rows = x.data_ptr(), wp.shape[0], p.M
     if rowbias:

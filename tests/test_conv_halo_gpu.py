@@ -108,12 +108,30 @@ def test_halo_conv_batch_and_tile_shape_invariant():
     with _knobs(FD_CONV_HALO_MIN_TILES=100000):
         assert ops.halo_conv_rows(xs, wp, nimg, H, W) == 0  # the implicit GEMM
     # TH = 8 tiles: a threshold between the two tile counts (16-row: 2 x 4 x 4 x 2 = 64 tiles; 8-row: 128)
-    with _knobs(FD_CONV_HALO_MIN_TILES=100):
+    with _knobs(FD_CONV_HALO_MIN_TILES=100, FD_CONV_HALO_SPLIT16=0):
         assert ops.halo_conv_rows(xs, wp, nimg, H, W) == 128
         th8 = ops.conv3x3(xs, wp, bd, nimg, H, W)
     torch.cuda.synchronize()
     assert torch.equal(both, one)
     assert torch.equal(both, th8)
+
+
+def test_halo_conv_split16():
+    """From 640 input channels the planner prefers 16-row tiles with the input channels split over two workgroups
+    (2 x 64 tiles >= 100) to 8-row tiles: a different K association (the halves are summed last), so compared with
+    fp32; below 640 channels it keeps the 8-row tiles."""
+    from fdhip import ops
+    nimg, H, W, C = 2, 64, 64, 640
+    x, w, b = _inputs(nimg, H, W, C, 320, torch.bfloat16, seed=6)
+    wp = ops.pack_conv3x3(w.float()).to(DEV, torch.bfloat16)
+    xs = _nhwc(x).to(DEV)
+    with _knobs(FD_CONV_HALO_MIN_TILES=100):
+        assert ops.halo_conv_rows(xs, wp, nimg, H, W) == 256
+        sk16 = ops.conv3x3(xs, wp, b.float().to(DEV), nimg, H, W)
+        assert ops.halo_conv_rows(xs[:, :320].contiguous(), wp[:, :9 * 320].contiguous(), nimg, H, W) == 128
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.float(), w.float(), b, padding=1)
+    assert rel_l2(_nchw(sk16.float().cpu(), nimg, H, W), ref) < 6e-3
 
 
 @pytest.mark.parametrize("up", [(32, 32), (31, 23)])
@@ -275,6 +293,18 @@ def test_halo_conv_persistent_form_is_bitwise_the_per_tile_form(case):
         ref = F.conv2d(xr, w.float(), b, padding=1) + _nchw(res.float().cpu(), nimg, H, W)
         rel = rel_l2(_nchw(outs[2][0].float().cpu(), nimg, H, W), ref)
         assert rel < 6e-3, rel
+
+
+def test_halo_conv_persistent_form_default_takes_gn_convs_without_residual():
+    """FD_CONV_HALO_PT's default (3): the persistent form only for GroupNorm-folded convs without a residual (the VAE
+    1024^2 resnet conv1s); the residual convs and the plain ones keep one workgroup per tile."""
+    from fdhip import ops
+    nimg, H, W, C = 1, 512, 256, 128
+    xs = torch.zeros(nimg * H * W, C, dtype=torch.float16, device=DEV)
+    wp = torch.zeros(C, 9 * C, dtype=torch.float16, device=DEV)
+    assert ops.halo_conv_pt(xs, wp, nimg, H, W, gn_in=True) > 0
+    assert ops.halo_conv_pt(xs, wp, nimg, H, W, gn_in=True, residual=True) == 0
+    assert ops.halo_conv_pt(xs, wp, nimg, H, W) == 0
 
 
 @pytest.mark.parametrize("nimg,H,W,C,Cout,dt", [(1, 64, 64, 512, 512, torch.float16), (1, 32, 48, 256, 256, torch.float16),
