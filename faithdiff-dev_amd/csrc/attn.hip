@@ -59,6 +59,10 @@ __device__ __forceinline__ float xor_max_16_32(float x) {
 #ifndef FD_FLASH_KPRE
 #define FD_FLASH_KPRE 0
 #endif
+// DIAG (timing builds only, wrong results): 1 = no K/V loads after the prologue (the ring is reused as it stands)
+#ifndef FD_FLASH_DIAG
+#define FD_FLASH_DIAG 0
+#endif
 #ifndef FD_FLASH_TR_EARLY
 #define FD_FLASH_TR_EARLY 1
 #endif
@@ -288,7 +292,7 @@ flash_attn_d64_kernel(
     constexpr int BUF = decltype(bufc)::value;
     constexpr bool MASK = decltype(maskc)::value;
     // buffer (BUF+NBUF-1)%NBUF was last read in the previous tile, which every wave finished before the barrier
-    if (!KPRE && t + NBUF - 1 < nt) stage(t + NBUF - 1, (BUF + NBUF - 1) % NBUF);
+    if (!KPRE && !FD_FLASH_DIAG && t + NBUF - 1 < nt) stage(t + NBUF - 1, (BUF + NBUF - 1) % NBUF);
     Sc sc;
     if constexpr (KPRE) qk_regs(sc);
     else qk(bufc, sc);
@@ -490,7 +494,7 @@ flash_attn_d64_kernel(
       T4 w;
 #pragma unroll
       for (int j = 0; j < 4; ++j) w[j] = (T)(o[db][qb][j] * inv);
-      *(T4*)(orow + db * 16 + fg * 4) = w;
+      st_out8((T4*)(orow + db * 16 + fg * 4), w);
     }
   }
 }
@@ -753,7 +757,7 @@ flash_attn_d512_kernel(const T* __restrict__ Q, const T* __restrict__ K, const T
         T4 w;
 #pragma unroll
         for (int j = 0; j < 4; ++j) w[j] = (T)(o[u][db][j] * inv);
-        *(T4*)(orow + db * 16 + fg * 4) = w;
+        st_out8((T4*)(orow + db * 16 + fg * 4), w);
       }
       continue;
     }
@@ -797,7 +801,7 @@ __global__ void __launch_bounds__(256) flash_d512_combine_kernel(const float* __
   V8 out;
 #pragma unroll
   for (int j = 0; j < 8; ++j) out[j] = (T)(acc[j] * inv);
-  *(V8*)(O + (long long)b * obs + (long long)q * ldo + c) = out;
+  st_out16((V8*)(O + (long long)b * obs + (long long)q * ldo + c), out);
 }
 
 static int d512_check(const void* q, const void* k, const void* v, long long ld, long long bs, const void* o,

@@ -565,7 +565,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = (T)v[i];
       const int rt = k * PER + rr;
-      *(TO8*)(C + (m0 + (long long)(rt >> 4) * Wo + (rt & 15)) * p.ldc + n) = o;
+      st_out16((TO8*)(C + (m0 + (long long)(rt >> 4) * Wo + (rt & 15)) * p.ldc + n), o);
       if (gn) {
         const int sp8 = ((cv * 8) / cpg + 1) * cpg - cv * 8;
         float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
@@ -801,7 +801,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       TO8 o;
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = (T)v[i];
-      if (ok) *(TO8*)(C + m * p.ldc + n) = o;
+      if (ok) st_out16((TO8*)(C + m * p.ldc + n), o);
       if (gn) {  // (sum, sumsq) of the stored values, split at the group boundary inside the chunk
         const int split = ((cv * 8) / cpg + 1) * cpg - cv * 8;
         float s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;

@@ -23,7 +23,7 @@ __global__ void concat_channels_kernel(const T* __restrict__ a, int C1, const T*
     const int v = e - m * VPR;
     const int c = v * 8;
     const V8 val = c < C1 ? *(const V8*)(a + m * C1 + c) : *(const V8*)(b + m * C2 + (c - C1));
-    *(V8*)(y + m * C + c) = val;
+    st_out16((V8*)(y + m * C + c), val);
   }
 }
 

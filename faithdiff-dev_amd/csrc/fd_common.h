@@ -29,6 +29,46 @@ extern "C" int fd_conv_halo_try(fd_gemm_params* p, void* stream);
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
+// Cache policy of the output stores of the GEMM / conv epilogues, GroupNorm apply, concat and flash attention
+// (FD_EPI_WT, build time): 0 plain (write-back L2: the kernel-end release then writes every dirty line back, after
+// the last wave), 1 sc1 (device scope: written through as stored, nothing left dirty at the end), 2 nt, 4 sc1 nt.
+// Inline asm: the waitcnt pass does not see these stores, which can only make a later vmcnt wait longer; nor does
+// the hazard recognizer, so the 16-B form carries its own wait states (a VALU may not overwrite the data VGPRs of a
+// > 8-byte VMEM store in the next cycles: hipcc placed a v_add into v0 of a v[0:3] store right behind it).
+#ifndef FD_EPI_WT
+#define FD_EPI_WT 1
+#endif
+#if FD_EPI_WT == 1
+#define FD_WT_BITS "sc1"
+#elif FD_EPI_WT == 2
+#define FD_WT_BITS "nt"
+#elif FD_EPI_WT == 4
+#define FD_WT_BITS "sc1 nt"
+#else
+#define FD_WT_BITS ""
+#endif
+// 16-B store (other widths: plain)
+template <typename V>
+__device__ __forceinline__ void st_out16(V* p, const V& v) {
+  if constexpr (FD_EPI_WT == 0 || sizeof(V) != 16) {
+    *p = v;
+  } else {
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    asm volatile("global_store_dwordx4 %0, %1, off " FD_WT_BITS "\n\ts_nop 1" ::"v"(p), "v"(__builtin_bit_cast(u4, v))
+                 : "memory");
+  }
+}
+// 8-B store (other widths: plain)
+template <typename V>
+__device__ __forceinline__ void st_out8(V* p, const V& v) {
+  if constexpr (FD_EPI_WT == 0 || sizeof(V) != 8) {
+    *p = v;
+  } else {
+    typedef __attribute__((ext_vector_type(2))) unsigned u2;
+    asm volatile("global_store_dwordx2 %0, %1, off " FD_WT_BITS ::"v"(p), "v"(__builtin_bit_cast(u2, v)) : "memory");
+  }
+}
+
 template <typename T> struct VecT;
 template <> struct VecT<bf16> { typedef bf16x8 v8; };
 template <> struct VecT<f16> { typedef f16x8 v8; };

@@ -466,7 +466,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
         TO8 o;
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
-        *(TO8*)(C + (long long)m * p.ldc + n) = o;
+        st_out16((TO8*)(C + (long long)m * p.ldc + n), o);
         if (GN4 && gn) gna.add(o, gsplit);
         if (lno) {  // statistics of the values as stored (what the consumer GEMM multiplies)
           float s = 0.f, q = 0.f;

@@ -318,7 +318,7 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
           TO8 o;
 #pragma unroll
           for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
-          *(TO8*)(C + (long long)m * p.ldc + n) = o;
+          st_out16((TO8*)(C + (long long)m * p.ldc + n), o);
           if (gn) gna.add(o, gsplit);
         }
       }

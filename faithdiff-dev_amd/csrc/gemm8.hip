@@ -867,7 +867,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
         TO8 o;
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = (TO)v[it][i];
-        *(TO8*)(C + (long long)m * p.ldc + n) = o;
+        st_out16((TO8*)(C + (long long)m * p.ldc + n), o);
         if (gn) gna.add(o, gsplit);
         if (GN160 && gn160) {
           const int gs = ((cv * 8) / gcpg + 1) * gcpg - cv * 8;

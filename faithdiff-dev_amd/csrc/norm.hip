@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(256) gn_apply_kernel(const T* __restrict__ x, 
         if (silu) f = silu_f(f);
         out[i] = (T)f;
       }
-      *(V8*)(y + base + ee * 8) = out;
+      st_out16((V8*)(y + base + ee * 8), out);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) val[u] = nxt[u];
@@ -315,7 +315,7 @@ __global__ void __launch_bounds__(256) gn_apply2_kernel(const T* __restrict__ x,
         if (silu) f = silu_f(f);
         out[i] = (T)f;
       }
-      *(V8*)(yb + (long long)rr * C) = out;
+      st_out16((V8*)(yb + (long long)rr * C), out);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) val[u] = nxt[u];
@@ -639,7 +639,7 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(const T* __restrict__ x
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         out[i] = round_f32<T>(__builtin_fmaf((vals[k][i] - mean) * rstd, g4[k][i >> 2][i & 3], b4[k][i >> 2][i & 3]));
-      *(V8*)(yr + v * 8) = out;
+      st_out16((V8*)(yr + v * 8), out);
     }
   }
 }
