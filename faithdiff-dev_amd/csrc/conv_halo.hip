@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
 #pragma unroll
     for (int i = 0; i < PER_B; ++i)
       __builtin_amdgcn_global_load_lds((const void*)((PT ? b_src(i) : b_row[PT ? 0 : i]) + off),
-                                       LDS_PTR(dst + (w + 4 * i) * 1024), 16, 0, 0);
+                                       LDS_PTR(dst + (w + 4 * i) * 1024), 16, 0, FD_WLD_AUX);
   };
   // patch of chunk c of the tile at (img_, y0_, x0_) into buffer c & 1 (+ its affine table; aff_: that tile's image)
   auto stage_p_at = [&] __attribute__((always_inline)) (int c, int img_, int y0_, int x0_, const float* aff_) {

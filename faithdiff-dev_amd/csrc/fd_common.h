@@ -47,6 +47,10 @@ extern "C" int fd_conv_halo_try(fd_gemm_params* p, void* stream);
 #else
 #define FD_WT_BITS ""
 #endif
+// Cache-policy bits of the GEMM / conv weight-operand LDS-DMA loads (build-time A/B): 0 default, 2 nt
+#ifndef FD_WLD_AUX
+#define FD_WLD_AUX 0
+#endif
 // 16-B store (other widths: plain)
 template <typename V>
 __device__ __forceinline__ void st_out16(V* p, const V& v) {

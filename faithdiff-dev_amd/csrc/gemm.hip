@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(256 * KS) gemm_kernel(const fd_gemm_params p, 
     unsigned char* sb = sa + A_BYTES;
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (i * NL + lw) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (i * NL + lw) * 1024), 16, 0, FD_WLD_AUX);
   };
 
   f32x4 acc[MT][NT];

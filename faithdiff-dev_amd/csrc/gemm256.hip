@@ -152,7 +152,7 @@ gemm256_kernel(const fd_gemm_params p, const int group_m) {
 #pragma unroll
     for (int i = 0; i < AI; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(Bw + (b_off[i] + k0)), LDS_PTR(sb + (w + NW * i) * 1024), 16, 0,
-                                       0);
+                                       FD_WLD_AUX);
   };
 
   const int fr = lane & 15, fg = lane >> 4;

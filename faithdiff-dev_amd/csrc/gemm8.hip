@@ -286,7 +286,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
 #pragma unroll
     for (int i = 0; i < B_I; ++i)
       if (i < B_LO || hi)
-        __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (w + NW * i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(b_row[i] + k0), LDS_PTR(sb + (w + NW * i) * 1024), 16, 0, FD_WLD_AUX);
     if constexpr (MXI)  // the 4 block scales of this K step (128 elements = 4 blocks) of rows w * RPW .. + 63
       __builtin_amdgcn_global_load_lds((const void*)(s_src + kt * 4), LDS_PTR(smem + SCL_OFF + buf * SCR + w * RPW * 4),
                                        4, 0, 0);
