@@ -65,6 +65,10 @@ __device__ __forceinline__ void vm_wait() {
 #ifndef FD_GEMM8_DIAG
 #define FD_GEMM8_DIAG 0
 #endif
+// timing build only (wrong results): 1 = the GEGLU epilogue multiplies by g instead of gelu(g)
+#ifndef FD_GEGLU_DIAG
+#define FD_GEGLU_DIAG 0
+#endif
 
 // BM x BN tile over NW waves (WAVES_M x WAVES_N).  Instances: 256 x 128 over 8 waves (the split-K kernel
 // above) and 64 x 160 over 4 waves (one wave per SIMD, 32 x 80 each: the M = 2048 projections' 256-tile
@@ -723,7 +727,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
               if (F8) {  // explicit fma (contraction would otherwise be the compiler's choice): gemm_fp8.hip's form
                 hv = __builtin_fmaf(acc[mi][ni][j], rsc[j], gbh[ni / 2]);
                 g = __builtin_fmaf(acc[mi][ni + 1][j], rsc[j], gbg[ni / 2]);
-                ep[(rl + j) * LDE + col] = hv * gelu_f(g);
+                ep[(rl + j) * LDE + col] = hv * (FD_GEGLU_DIAG ? g : gelu_f(g));
                 continue;
               }
               if (LNF) {
@@ -732,7 +736,7 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
               }
               hv += gbh[ni / 2];
               g += gbg[ni / 2];
-              ep[(rl + j) * LDE + col] = hv * gelu_f(g);
+              ep[(rl + j) * LDE + col] = hv * (FD_GEGLU_DIAG ? g : gelu_f(g));
             }
           }
         } else {
