@@ -20,7 +20,8 @@ enum fd_knob_id {
   FDK_GEMM8_N128, FDK_GEMM8_LNP, FDK_GEMM8_LNP_S, FDK_GEMM8_MIDK, FDK_F8_TILE, FDK_F8_KERNEL, FDK_GEMM_CFG,
   FDK_GEMM_NS, FDK_GEMM_KS, FDK_GEMM_SWZ, FDK_GEMM_MODE, FDK_GEMV, FDK_GEMM256, FDK_GEMM256_MIN_TILES,
   FDK_GN_MIN_CHUNKS, FDK_GN_APPLY_V, FDK_GN_APPLY_BLOCKS, FDK_GN_APPLY_U, FDK_FLASH_SWZ, FDK_FLASH_WAVES,
-  FDK_FLASH_QPW, FDK_CONV_HALO, FDK_CONV_HALO_MIN_TILES, FDK_CONV_HALO_SPLIT, FDK_CONV_HALO_NS8, FDK_GEMM_GMP, FDK_GEMM8_W128, FDK_GEMM8_LNP_K, FDK_XATTN_SPLIT, FDK_CONV_HALO_PT, FDK_CONV_HALO_NS16, FDK_CONV_HALO_SPLIT16, FDK_COUNT
+  FDK_FLASH_QPW, FDK_CONV_HALO, FDK_CONV_HALO_MIN_TILES, FDK_CONV_HALO_SPLIT, FDK_CONV_HALO_NS8, FDK_GEMM_GMP, FDK_GEMM8_W128, FDK_GEMM8_LNP_K, FDK_XATTN_SPLIT, FDK_CONV_HALO_PT, FDK_CONV_HALO_NS16, FDK_CONV_HALO_SPLIT16,
+  FDK_GEMM8_LNP_BIG, FDK_COUNT
 };
 int fd_knob(int id);
 // gemm256.hip: whether fd_gemm256_try takes this launch

@@ -1094,6 +1094,19 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     // of the 32^2 level, 2048 x 1280 x 5120 at C2): 128 x 160 tiles with K split in two (pairwise combine),
     // 0.64x the operand bytes per CU of the 4-wave 64 x 160 producer (probe with cold weights 47.1 -> 40.6 us,
     // profiles/r02e_m2048_split.jsonl); anything else stays on that producer (return 0).
+    // large-M producers (>= 256 tiles of 256 x 160 per TLC tile: the information transformer's out_proj / c_proj at
+    // 128^2, M = 32768): eight-wave 256 x 160 tiles in one K pass, 2+ rounds on 256 CUs, instead of 2048 4-wave
+    // 64 x 160 tiles (0.47x the operand bytes per output); the partial layout is the same (per row and 160 columns)
+    if (fd_knob(FDK_GEMM8_LNP_BIG) && p->act != FD_ACT_GEGLU && !p->conv && p->N % 160 == 0 && m_ref >= 256 &&
+        (long long)(m_ref / 256) * (p->N / 160) >= 256) {
+      q.bm = 256;
+      q.bn = 160;
+      q.nw = 8;
+      q.waves_m = 8;
+      q.ns = 3;
+      q.S = 1;
+      goto planned;
+    }
     const int lnp = fd_knob(FDK_GEMM8_LNP);
     const int lnp_s = fd_knob(FDK_GEMM8_LNP_S);  // splits of the 256 x 160 form (lnp = 2)
     // FD_GEMM8_LNP_K: the least K routed here (4096: the ff outs; 1024 also takes the K = 1280 / 1600 producers of

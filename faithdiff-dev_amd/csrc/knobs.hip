@@ -56,6 +56,8 @@ const KnobDef kDefs[FDK_COUNT] = {
                                    // gemm256-eligible ones, 0 off
     {"FD_CONV_HALO_NS16", 3},      // weight-ring depth of its 256 x 128 tiles (3 or 4)
     {"FD_CONV_HALO_SPLIT16", 1},   // 256-row tiles with a pairwise input-channel split before 128-row tiles
+    {"FD_GEMM8_LNP_BIG", 0},       // LN-fold producers of >= 256 256-row tiles per TLC tile (the information transformer
+                                   // at 128^2: out_proj / c_proj, M = 32768) on gemm8 256 x 160 instead of 4-wave 64 x 160
 };
 int g_knobs[FDK_COUNT];
 bool g_init = false;
