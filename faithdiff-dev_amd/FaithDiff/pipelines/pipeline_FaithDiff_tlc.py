@@ -32,7 +32,7 @@ from fdhip import knobs, ops
 from ..schedulers import DDPMScheduler, EulerDiscreteScheduler
 from .pipeline_output import FaithDiffStableDiffusionXLPipelineOutput
 from .tile_parallel import TileShard, broadcast, broadcast_state_dict, run_tile_loop, staging_device
-from .tlc import TileGrid
+from .tlc import TileGrid, tile_batches
 
 
 class SyntheticTextEncoder:
@@ -90,6 +90,9 @@ class FaithDiffStableDiffusionXLPipeline:
         # TLC tiles per UNet forward (B = 2 * tile_batch rows; C3 4096^2: 4 -> 13 tiles = 51.6 -> 53.2 tile-steps/s,
         # scripts/tb_sweep.sh); FD_TILE_BATCH overrides (A/B timing)
         self.tile_batch = knobs.get("FD_TILE_BATCH")
+        # FD_TILE_BALANCE=1: a rank's tiles in ceil(count / tile_batch) batches of equal size (+-1) instead of full
+        # batches and a short remainder (C4 225 tiles: 17 x 13 + 4 -> 9 x 13 + 9 x 12)
+        self.tile_balance = knobs.get("FD_TILE_BALANCE")
         self.process_group = None    # torch.distributed group for tile parallelism (None: single GPU)
         self.last_timings = {}
         self._weights_group = None   # the group broadcast_weights last synchronised the weights over
@@ -545,8 +548,7 @@ class FaithDiffStableDiffusionXLPipeline:
 
         def compute(i, begin, count, out):
             s, s_next = float(sig[i]), float(sig[i + 1])
-            for c0 in range(0, count, tb):
-                n = min(tb, count - c0)
+            for c0, n in tile_batches(count, tb, self.tile_balance):
                 rows = n * cfg
                 cond = cond_tiles[c0 * cfg:(c0 + n) * cfg].reshape(rows * kh * kw, cond_tiles.shape[-1])
                 tid = tids_all[(begin + c0) * cfg:(begin + c0 + n) * cfg]

@@ -26,6 +26,24 @@ def axis_origins(n, k, overlap):
     return out, k
 
 
+def tile_batches(count, tb, balance=False):
+    """(first tile, tile count) of each UNet forward over a rank's `count` tiles, at most `tb` per forward: full
+    batches and a remainder, or with `balance` ceil(count / tb) batches whose sizes differ by at most one (the
+    larger ones first).  Every tile's result is independent of the batch it rides in (the tile-batch bitwise tests)."""
+    if count <= 0:
+        return []
+    if not balance:
+        return [(c0, min(tb, count - c0)) for c0 in range(0, count, tb)]
+    nb = -(-count // tb)
+    q, r = divmod(count, nb)
+    out, c0 = [], 0
+    for b in range(nb):
+        n = q + (1 if b < r else 0)
+        out.append((c0, n))
+        c0 += n
+    return out
+
+
 class TileGrid:
     def __init__(self, h, w, kernel_size, overlap=0.5):
         self.h, self.w = h, w

@@ -38,8 +38,10 @@ def main():
             print(f"... {time.perf_counter() - t_start:.0f} s", flush=True)
     threading.Thread(target=beat, daemon=True).start()
 
+    from fdhip import knobs
     from fdhip import lib as L
     from FaithDiff.pipelines.tlc import TileGrid
+    applied = knobs.apply_env()  # A/B runs (FD_TILE_BATCH ...); reported in the result line
     from PIL import Image
     L.require_device()
     dev = torch.device("cuda", 0)
@@ -80,7 +82,7 @@ def main():
            "decode_s": round(tm.span_ms("decode_start", "decode") / 1e3, 2),
            "latents_finite": bool(torch.isfinite(last["lat"]).all().item()) if "lat" in last else None,
            "image_size": list(arr.shape), "image_std": round(float(arr.std()), 2),
-           "peak_gpu_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
+           "peak_gpu_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1), "knobs": applied}
     print(json.dumps(res), flush=True)
 
 

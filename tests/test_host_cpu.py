@@ -36,6 +36,20 @@ def test_tile_counts_for_survey_configs():
     assert TileGrid(128, 128, (128, 128), 0.5).ntiles == 1         # C2
 
 
+@pytest.mark.parametrize("count,tb", [(225, 13), (49, 13), (1947, 13), (13, 13), (5, 13), (1, 4), (112, 15)])
+def test_tile_batches_cover_every_tile_once(count, tb):
+    """The denoise loop's tile batches (full + remainder, or balanced): every tile once, in order, <= tb per forward;
+    balanced sizes differ by at most one and use the same number of forwards."""
+    from FaithDiff.pipelines.tlc import tile_batches
+    plain, bal = tile_batches(count, tb), tile_batches(count, tb, True)
+    for bs in (plain, bal):
+        assert [c0 for c0, _ in bs] == list(np.cumsum([0] + [n for _, n in bs])[:-1])
+        assert sum(n for _, n in bs) == count and all(0 < n <= tb for _, n in bs)
+    assert len(bal) == len(plain) == -(-count // tb)
+    assert max(n for _, n in bal) - min(n for _, n in bal) <= 1
+    assert tile_batches(0, tb) == tile_batches(0, tb, True) == []
+
+
 @pytest.mark.parametrize("n", [4, 20, 50])
 def test_euler_schedule_matches_oracle(n):
     from FaithDiff.schedulers import DDPMScheduler, EulerDiscreteScheduler
