@@ -88,7 +88,9 @@ class FaithDiffStableDiffusionXLPipeline:
         self.watermark = None
         self.device = torch.device("cpu")
         # TLC tiles per UNet forward (B = 2 * tile_batch rows; C3 4096^2: 4 -> 13 tiles = 51.6 -> 53.2 tile-steps/s,
-        # scripts/tb_sweep.sh); FD_TILE_BATCH overrides (A/B timing)
+        # scripts/tb_sweep.sh; C4 225 tiles: 13 -> 25 = 70.1 -> 72.2 tile-steps/s, profiles/r05ad_tile_batch_ab.txt).
+        # 25 keeps the largest activation (the 128^2 level's 2 * 25 * 16384 rows x 1280) at 1.05e9 elements, half of
+        # the 32-bit index range the kernels' offsets assume.  FD_TILE_BATCH overrides (A/B timing)
         self.tile_batch = knobs.get("FD_TILE_BATCH")
         # FD_TILE_BALANCE=1: a rank's tiles in ceil(count / tile_batch) batches of equal size (+-1) instead of full
         # batches and a short remainder (C4 225 tiles: 17 x 13 + 4 -> 9 x 13 + 9 x 12)

@@ -25,8 +25,8 @@ HOST_DEFAULTS = {
     "FD_VAE_NARROW": 1,     # VAE conv_norm_out + SiLU + conv_out in the narrow strip kernel (fd_conv3x3_narrow_gn)
     "FD_UP2_PHASE": 1,      # Upsample2D convs (VAE decoder, UNet up blocks) as four 2x2 phase convs of the low-res input
     "FD_GRAPHS": 1,         # hipGraph capture / replay of the UNet, VAE and text encoders
-    "FD_TILE_BATCH": 13,    # TLC tiles per UNet forward
-    "FD_TILE_BALANCE": 0,   # split a rank's tiles into equal batches (+-1) of at most FD_TILE_BATCH
+    "FD_TILE_BATCH": 25,    # TLC tiles per UNet forward (at most; the largest rows * channels stays < 2^31 / 2)
+    "FD_TILE_BALANCE": 1,   # split a rank's tiles into equal batches (+-1) of at most FD_TILE_BATCH
     "FD_XATTN_GEMM": 1,     # attn2 as two GEMMs (scores + softmax epilogue, P . V W_o) against per-prompt products
     "FD_HALO_GN_CIN_MAX": 640,  # GroupNorm folded into the halo conv's staging pass up to this many input channels
     "FD_D512_SPLIT": 1,     # VAE d=512 attention on 8 waves (128 queries per K/V fetch) with the keys split + merged

@@ -136,7 +136,7 @@ def test_call_tile_parallel_two_ranks_one_gpu_bitwise():
 def test_c3_49_tiles_tile_batch_bitwise():
     """BASELINE configs[2] shape on the GPU: a 4096^2 input restored at target 1024 (latent 512^2 -> 49 TLC tiles,
     tiled VAE encode / decode and tiled denoise encoder at their default 1024-px tiles), one Euler step, through
-    the product __call__.  The tiles are batched 13 and 4 per UNet forward: every latent and pixel must be equal
+    the product __call__.  The tiles are batched 25 (the default: 25 + 24) and 4 per UNet forward: every latent and pixel must be equal
     (a tile's rows never depend on which tiles share its forward; m_ref keeps the kernel choices per tile)."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
@@ -150,7 +150,7 @@ def test_c3_49_tiles_tile_batch_bitwise():
     noise, post = det_tensor((1, 4, S // 8, S // 8), 41), det_tensor((1, 4, S // 8, S // 8), 42)
     res = []
     try:
-        for tb in (13, 4):
+        for tb in (25, 4):
             pipe.tile_batch = tb
             cap = {}
 
