@@ -32,7 +32,7 @@ from fdhip import knobs, ops
 from ..schedulers import DDPMScheduler, EulerDiscreteScheduler
 from .pipeline_output import FaithDiffStableDiffusionXLPipelineOutput
 from .tile_parallel import TileShard, broadcast, broadcast_state_dict, run_tile_loop, staging_device
-from .tlc import TileGrid, tile_batches
+from .tlc import TileGrid, max_tile_batch, tile_batches
 
 
 class SyntheticTextEncoder:
@@ -525,7 +525,8 @@ class FaithDiffStableDiffusionXLPipeline:
 
         # 7. per-row conditioning, computed once per image
         unet.set_context(ctx.to(dev))
-        tb = max(1, min(self.tile_batch, shard.count or 1))
+        # capped where the widest activation of one forward would leave the kernels' 32-bit offset range
+        tb = max(1, min(self.tile_batch, shard.count or 1, max_tile_batch(kh, kw, cfg)))
         # the FaithDiff condition embedding (ext:528-534) of every tile's image latents: fixed across the denoise
         # loop, so computed once per image here (the reference recomputes it inside every UNet call, :1350),
         # per tile batch, bitwise what the forward would compute (HipUNet.cond_embed)
@@ -727,7 +728,7 @@ class FaithDiffStableDiffusionXLPipeline:
                 ops.vae_sample_add_noise(None, None, noise.contiguous(), canvas[i], h * w, 1.0, init_sigma, 0.0, 1.0,
                                          False)
         unet.set_context(ctx.to(dev), ncfg=cfg)
-        tb = max(1, min(self.tile_batch, nimg))
+        tb = max(1, min(self.tile_batch, nimg, max_tile_batch(kh, kw, cfg)))
         cond_emb = False
         if unet.has_extras:  # the condition embedding of every image's tile, once per call (HipUNet.cond_embed)
             ie = torch.empty((nimg * cfg, kh * kw, 320), dtype=cond_dt, device=dev)

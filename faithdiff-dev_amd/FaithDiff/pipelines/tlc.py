@@ -26,6 +26,17 @@ def axis_origins(n, k, overlap):
     return out, k
 
 
+# widest activation per latent position in a UNet forward (the information transformer's c_fc output at the tile's
+# full resolution, 1280 channels; the up blocks' concats are 960)
+WIDEST_CHANNELS = 1280
+
+
+def max_tile_batch(kh, kw, cfg=2):
+    """Most tiles one UNet forward may carry: the widest activation (cfg * tiles * kh * kw rows x WIDEST_CHANNELS)
+    stays below 2^31 elements, the range of the kernels' 32-bit element offsets (51 for 128^2 tiles with CFG)."""
+    return max(1, ((1 << 31) - 1) // (cfg * kh * kw * WIDEST_CHANNELS))
+
+
 def tile_batches(count, tb, balance=False):
     """(first tile, tile count) of each UNet forward over a rank's `count` tiles, at most `tb` per forward: full
     batches and a remainder, or with `balance` ceil(count / tb) batches whose sizes differ by at most one (the

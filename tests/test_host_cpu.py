@@ -50,6 +50,18 @@ def test_tile_batches_cover_every_tile_once(count, tb):
     assert tile_batches(0, tb) == tile_batches(0, tb, True) == []
 
 
+def test_max_tile_batch_keeps_32bit_offsets():
+    """The tile-batch cap: 128^2 tiles with CFG fit 51 per forward (the default 25 is half of it); the widest
+    activation of a capped forward stays inside 2^31 elements, one more tile would not."""
+    from FaithDiff.pipelines.tlc import WIDEST_CHANNELS, max_tile_batch
+    assert max_tile_batch(128, 128, 2) == 51
+    for kh, kw, cfg in [(128, 128, 2), (128, 98, 2), (64, 64, 1), (128, 128, 1)]:
+        tb = max_tile_batch(kh, kw, cfg)
+        assert tb * cfg * kh * kw * WIDEST_CHANNELS < 2 ** 31 <= (tb + 1) * cfg * kh * kw * WIDEST_CHANNELS
+    from fdhip import knobs
+    assert knobs.default("FD_TILE_BATCH") <= max_tile_batch(128, 128, 2) // 2
+
+
 @pytest.mark.parametrize("n", [4, 20, 50])
 def test_euler_schedule_matches_oracle(n):
     from FaithDiff.schedulers import DDPMScheduler, EulerDiscreteScheduler
