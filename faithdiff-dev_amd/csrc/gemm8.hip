@@ -1312,17 +1312,23 @@ int plan_e4m3(const fd_gemm_params* p, bool mx_out, Plan8* pl) {
   const int nout = geglu ? p->N / 2 : p->N;
   int best = -1;
   double bt = 1e30;
+  bool ok128 = false;
   for (int c = 0; c < 4; ++c) {
     const Cand& q = cands[c];
     if (geglu && (q.bn / (q.nw / q.wm)) % 32) continue;
     if (force && force != q.bm * 1000 + q.bn) continue;
     const int bno = geglu ? q.bn / 2 : q.bn;
     if (mx_out && (bno % 32 || nout % bno || p->M % q.bm)) continue;
+    if (c == 1) ok128 = true;
     const long long tiles = (long long)((p->M + q.bm - 1) / q.bm) * ((p->N + q.bn - 1) / q.bn);
     // the 256 x 160 GEGLU tile stores 80 columns: its fixed part is relatively smaller (fit: 0.9x)
     const double t = (double)((tiles + 255) / 256) * (q.a + q.b * p->K / 1280.0) * (geglu && c == 0 ? 0.9 : 1.0);
     if (t < bt * 0.999) { bt = t; best = c; }
   }
+  // M >= 16384 (the tiled C4 forwards: 25 tiles = 51200 / 204800 rows): many rounds per launch, where the model's
+  // per-tile fit (C2 shapes, M <= 8192) no longer ranks the tiles -- every launch on 256 x 128 measured 72.56 vs
+  // 71.32 tile-steps/s for the modelled mix (profiles/r05am_f8_tile_c4_ab.txt).  C2's e4m3 launches stay as planned.
+  if (!force && p->M >= 16384 && ok128) best = 1;
   if (best < 0) return 0;
   pl->bm = cands[best].bm;
   pl->bn = cands[best].bn;
