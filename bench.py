@@ -240,6 +240,7 @@ class C2Loop:
         self.ie = torch.empty((self.B * k * k, 320), dtype=unet.dtype, device=dev)
         self.t_buf = torch.full((self.B,), self.ts[0], device=dev)
         self.static = None
+        self.static_tried = False  # graph_inputs() asked once after the capture step (None for good with FD_GRAPHS=0)
         self.per_image()
         self.out_tiles = torch.empty((self.grid.ntiles, 4, k, k), device=dev)
         ops.reserve_gn_workspace(1 << 24, dev)
@@ -265,7 +266,10 @@ class C2Loop:
 
     def step(self, i):
         ops, k, h = self.ops, self.k, self.h
-        if i % 20 == 0 or (self.static is None and i >= 2):  # once per 20-step image, as __call__ does
+        # once per 20-step image, as __call__ does; and once at step 2, when run()'s graph has been captured, to move
+        # the per-image inputs into its static buffers (never again when graphs are off: FD_GRAPHS=0 A/B arms)
+        if i % 20 == 0 or (i >= 2 and not self.static_tried):
+            self.static_tried = i >= 2
             self.per_image()
         s_, sn = self.sig[i % 20], self.sig[i % 20 + 1]
         ops.tlc_scale_input(self.canvas, self.rows, self.cols, h, h, k, k, 0, self.grid.ntiles, self.cfg, s_,

@@ -533,8 +533,10 @@ class FaithDiffStableDiffusionXLPipeline:
         cond_emb = False
         if cond_tiles is not None and unet.has_extras:
             ie_tiles = torch.empty((cond_tiles.shape[0], kh * kw, 320), dtype=cond_dt, device=dev)
-            for c0 in range(0, shard.count, tb):
-                r0, r1 = c0 * cfg, min(c0 + tb, shard.count) * cfg
+            # the same tile batches as the denoise loop below (every kernel is bitwise batch-invariant, but the
+            # hoisted embedding then rides in exactly the batches the loop's forwards would have used)
+            for c0, n in tile_batches(shard.count, tb, self.tile_balance):
+                r0, r1 = c0 * cfg, (c0 + n) * cfg
                 unet.cond_embed(cond_tiles[r0:r1].reshape(-1, 512), r1 - r0, kh, kw,
                                 out=ie_tiles[r0:r1].reshape(-1, 320))
             cond_tiles, cond_emb = ie_tiles, True
@@ -603,6 +605,7 @@ class FaithDiffStableDiffusionXLPipeline:
             if timer is not None:
                 timer("decode", 0)
             image = self._postprocess(y, height, width, output_type)
+        ops.split_k_health()  # a timed-out split-K hand-off (never expected) raises here, counters reset
         if not return_dict:
             return (image,)
         return FaithDiffStableDiffusionXLPipelineOutput(images=image)
@@ -787,6 +790,7 @@ class FaithDiffStableDiffusionXLPipeline:
                 images.extend(im if isinstance(im, list) else [im])
             if timer is not None:
                 timer("decode", 0)
+        ops.split_k_health()
         if not return_dict:
             return (images,)
         return FaithDiffStableDiffusionXLPipelineOutput(images=images)

@@ -26,6 +26,9 @@
 #include "fd_common.h"
 
 __device__ __attribute__((aligned(256))) unsigned char g_zero_halo[256];
+// split-K hand-off health of the channel-split form (as gemm8.hip: timed-out pairwise waits, test hook)
+__device__ unsigned g_halo_sk_timeouts;
+__device__ unsigned g_halo_sk_drop;
 
 #ifndef FD_HALO_CT
 #define FD_HALO_CT 1
@@ -35,6 +38,13 @@ __device__ __attribute__((aligned(256))) unsigned char g_zero_halo[256];
 // 32 = no K loop at all (prologue DMA + wait, epilogue)
 #ifndef FD_HALO_DIAG
 #define FD_HALO_DIAG 0
+#endif
+// ping-pong K loop (build-time A/B): first tap of the GroupNorm transform pieces; s_setprio(1) for waves 4-7
+#ifndef FD_HALO_PP_TR
+#define FD_HALO_PP_TR 5
+#endif
+#ifndef FD_HALO_PP_PRIO
+#define FD_HALO_PP_PRIO 0
 #endif
 
 namespace {
@@ -74,7 +84,14 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // low-resolution grid; the combined N = 4 * Cout is phase-major (an N tile never straddles two phases); a tile's
 // 4 taps read the window at rows a + {0, 1}, columns b + {0, 1} of its (TH + 2) x 18 patch, and its epilogue writes
 // the strided output pixels.  GroupNorm partials: one block per (image, phase, tile) -- 256 output pixels each.
-template <typename T, int TH, int BN, bool GNI, bool SK, int NS, bool PT, bool PH>
+//
+// PP (ping-pong K loop, every form but PT): the 8 waves run as two groups of four -- group 0 = waves 0-3 = the
+// tile's rows [0, BM / 2), group 1 = waves 4-7 = rows [BM / 2, BM); waves w and w + 4 share a SIMD -- and group 1
+// starts one barrier late, so on every SIMD one wave issues its MFMAs while its partner reads fragments, issues
+// LDS-DMA and transforms the next chunk's patch (the gemm256 scheme).  Per K step (one tap of one chunk) a wave runs
+// a LOAD segment (both halves' fragments of the step) and a COMPUTE segment (the step's MFMAs, half 0 then half 1),
+// each closed by a raw s_barrier.  Same per-element K order as the one-barrier loop: the same bits.
+template <typename T, int TH, int BN, bool GNI, bool SK, int NS, bool PT, bool PH, bool PP>
 __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, float* __restrict__ slabs,
                                                           unsigned* __restrict__ counters) {
   typedef typename VecT<T>::v8 V8;
@@ -100,6 +117,7 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   constexpr int PER = 32;  // PT epilogue pass: 32 rows x BN fp32 + their GroupNorm slots, past the ring
   constexpr int PT_EP = SMEM_MAIN, PT_SLOT = PT_EP + PER * LDE * 4, PT_END = PT_SLOT + PER * VPR * 16;
   static_assert(!PH || (!GNI && !SK && !PT), "phase form: plain tiles only");
+  static_assert(!(PP && PT), "ping-pong loop: per-tile forms");
   constexpr int NTAP = PH ? 4 : 9;
   // lane-constant LDS read bases in the K loop (below): every tile form but the persistent and the phase ones
   constexpr bool CT = !PH && FD_HALO_CT;
@@ -371,7 +389,85 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
   }
 
   V8 a0[MT], b0[NT], a1[MT], b1[NT];
-  if constexpr (CT) {
+  if constexpr (PP) {
+    // ---- ping-pong K loop.  Interval i (between barriers i - 1 and i): group 0 runs segment i, group 1 segment
+    // i - 1; segment 2s = LOAD(s), 2s + 1 = COMPUTE(s).  So step s's fragments are read in intervals 2s (group 0)
+    // and 2s + 1 (group 1).  Hazards:
+    //  * weight stage s + NS - 1 is DMA'd by group 0 in LOAD(s) (interval 2s) into slot (s - 1) % NS, whose last
+    //    reader (group 1, step s - 1) finished in interval 2s - 1; group 0 waits for stage s + 1 at the end of
+    //    COMPUTE(s) (interval 2s + 1), before either group reads it (intervals 2s + 2, 2s + 3);
+    //  * chunk c + 2's patch is DMA'd by group 1 at the end of COMPUTE(chunk c, tap 8) (interval 2(9c + 8) + 2) into
+    //    buffer c & 1, whose last readers were group 0's and group 1's LOAD(chunk c, tap 8) (intervals 2(9c + 8) and
+    //    + 1); group 1 waits for it at the end of LOAD(chunk c + 1, tap TW): before the first transform piece (GNI,
+    //    tap PTR) or the first read of chunk c + 2;
+    //  * GNI: each group transforms its threads' share of chunk c + 1's patch a piece per tap PTR .. 8 in its LOAD
+    //    segments (under the partner's MFMAs); every LOAD ends with lgkmcnt(0), so the last piece (group 1,
+    //    interval 2(9c + 8) + 1) is visible before group 0 reads chunk c + 1 (interval 2(9c + 9)).
+    const int grp = w >> 2;
+    // the next chunk's patch: DMA'd at the end of the last COMPUTE of chunk c - 1 (buffer (c + 1) & 1 is free once
+    // both groups' LOAD of chunk c - 1's last tap is behind them), waited for by group 1 at the end of LOAD(tap TW)
+    // of chunk c, transformed (GNI) in pieces at taps PTR .. NTAP - 1 -- the last piece (group 1, tap 8) still lands
+    // an interval before group 0's first read of chunk c + 1
+    constexpr int PTR = FD_HALO_PP_TR, PNP = NTAP - PTR > 0 ? NTAP - PTR : 1;
+    constexpr int TW = GNI ? PTR - 1 : NTAP - 1;
+    static_assert(!GNI || (PTR >= 1 && PTR < NTAP), "ping-pong transform taps");
+    const int rr = wn * WN + fr;
+    const int lb0 = RING + rr * 128 + (((0 * 4 + fg) ^ ((rr >> 1) & 7)) << 4);
+    const int lb1 = RING + rr * 128 + (((1 * 4 + fg) ^ ((rr >> 1) & 7)) << 4);
+    // fragment (mi, tap (ky, kx), K half h): the lane's column base la(kx, h) plus wave-uniform row offsets (the
+    // column-only patch swizzle, as in the one-barrier loop below); PH: the tap's 2 x 2 window at (pha, phb)
+    auto rd = [&] __attribute__((always_inline)) (int c, int t, int rb, auto hcc, V8 (&af)[MT], V8 (&bf)[NT]) {
+      constexpr int H = decltype(hcc)::value;
+      const int ky = PH ? pha + (t >> 1) : t / 3, kx = PH ? phb + (t & 1) : t - (t / 3) * 3;  // wave-uniform
+      const int px = fr + kx;
+      const int la = px * 128 + (((H * 4 + fg) ^ ((px >> 1) & 7)) << 4);
+      const unsigned char* pa = smem + ((c & 1) * PBUF + (wm * MT + ky) * (PW * 128)) + la;
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) af[mi] = *(const V8*)(pa + mi * (PW * 128));
+      const unsigned char* sb = smem + rb * STAGE + (H ? lb1 : lb0);
+#pragma unroll
+      for (int ni = 0; ni < NT; ++ni) bf[ni] = *(const V8*)(sb + ni * 2048);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    if (grp == 1) {
+      __builtin_amdgcn_s_barrier();  // the stagger
+      if (FD_HALO_PP_PRIO) __builtin_amdgcn_s_setprio(1);  // the younger half wins VALU arbitration (guide item 4)
+    }
+    int c = cb, t = 0, rb = 0;
+    for (int s = 0; s < nsteps; ++s) {
+      // LOAD(s)
+      rd(c, t, rb, I0(), a0, b0);
+      rd(c, t, rb, I1(), a1, b1);
+      if (w < 4) {
+        if (s >= 1 && s + NS - 1 < nsteps) stage_b(s + NS - 1, rb == 0 ? NS - 1 : rb - 1);
+      } else if (t == TW && c + 1 < ce) {
+        hvm<0>();  // chunk c + 1's patch (the only patch DMA in flight)
+      }
+      if constexpr (GNI) {
+        if (t >= PTR && c + 1 < ce) transform(c + 1, t - PTR, std::integral_constant<int, PNP>());
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this step's fragments, the transform's LDS writes
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      // COMPUTE(s)
+      mma(a0, b0);
+      mma(a1, b1);
+      if (w < 4) wait_b(min(NS - 2, nsteps - 2 - s));  // weight stage s + 1 landed
+      else if (t == NTAP - 1 && c + 2 < ce) stage_p(c + 2);  // buffer c & 1: both groups' last reads are behind
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      rb = rb == NS - 1 ? 0 : rb + 1;
+      if (t == NTAP - 1) {
+        ++c;
+        t = 0;
+      } else {
+        ++t;
+      }
+    }
+    if (grp == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+    else if (FD_HALO_PP_PRIO) __builtin_amdgcn_s_setprio(0);
+  } else if constexpr (CT) {
     // ---- the K loop with cheap LDS read addresses.  With the column-only patch swizzle, fragment (mi, tap (ky, kx),
     // K half h) sits at  la(kx, h) + [chunk buffer + (wm * MT + ky) * PW * 128] + mi * PW * 128  with
     //   la(kx, h) = (fr + kx) * 128 + chunk slot ((h * 4 + fg) ^ ((fr + kx) >> 1 & 7))
@@ -648,13 +744,13 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
                                                  ((mi * NT + ni) * 512 + tid) * 16, 0, 16);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0 && !__hip_atomic_load(&g_halo_sk_drop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
     if (tid == 0) {
-      // bounded: a lost flag poisons the tile (NaN, so the forward's finiteness checks see it) instead of hanging
-      // the GPU; the flag and the counter are reset only after the partner's flag was seen, never on the timeout
-      // path (a late partner's flag must not be taken for a later launch's)
+      // bounded: a lost flag poisons the tile (NaN) instead of hanging the GPU and counts a timeout (the host
+      // checks it and re-zeroes the counters: gemm8.hip's pairwise form has the same protocol)
       unsigned got = 0u;
       for (int it = 0; it < (1 << 24) && !got; ++it) {
         got = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -663,6 +759,8 @@ __global__ void __launch_bounds__(512) conv_halo_kernel(const fd_gemm_params p, 
       if (got) {
         __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(counters + tlin, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_fetch_add(&g_halo_sk_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       ((volatile unsigned*)smem)[1] = got;
     }
@@ -962,7 +1060,7 @@ int halo_plan(const fd_gemm_params* p, HaloPlan* pl) {
   pl->pt = halo_pt_grid(p, th, bn, sk, pl->tiles);
   // a 128-row tile's K step is half the MFMA work of a 256-row one: its weight stages need a deeper ring to cover
   // the L2 latency (the 256-row tile's LDS holds 3 stages at 160 columns, 4 at 128)
-  pl->ns = th == 8 ? fd_knob(FDK_CONV_HALO_NS8) : (bn == 128 && !pl->pt && !sk ? fd_knob(FDK_CONV_HALO_NS16) : 3);
+  pl->ns = th == 8 ? 3 : (bn == 128 && !pl->pt && !sk ? fd_knob(FDK_CONV_HALO_NS16) : 3);
   if (g256 && !pl->pt) return 0;  // FD_CONV_HALO_PT = 2 takes a gemm256 conv only in the PT form
   return 1;
 }
@@ -975,12 +1073,19 @@ int launch_halo(const fd_gemm_params* p, const HaloPlan& pl, hipStream_t s) {
   float* slabs = pl.sk ? (float*)((char*)p->ws + 65536 * sizeof(unsigned)) : nullptr;
   unsigned* cnt = pl.sk ? (unsigned*)p->ws : nullptr;
   const dim3 grid(pl.pt ? pl.pt : pl.tiles * (1 + pl.sk));
+  // ping-pong loop for the 256-row tiles (per-tile forms); the 128-row tiles' 10-20 MFMAs per half step measured
+  // slower split in two segments (profiles/r06a_conv_ab_pp*.jsonl)
+  const bool pp = fd_knob(FDK_CONV_HALO_PP) != 0 && pl.th == 16;
   if (pl.ph) {
     if (gi || pl.sk || pl.pt || pl.ns != 3) return FD_ERR_ARG;
 #define FD_HALO_PH(TH_, BN_)                                                                                          \
     if (pl.th == TH_ && pl.bn == BN_) {                                                                              \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, false, 3, false, true>), grid, dim3(512), 0, s, *p,   \
-                         slabs, cnt);                                                                                \
+      if (pp)                                                                                                        \
+        hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, false, 3, false, true, true>), grid, dim3(512), 0, s, \
+                           *p, slabs, cnt);                                                                          \
+      else                                                                                                           \
+        hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, false, 3, false, true, false>), grid, dim3(512), 0, s, \
+                           *p, slabs, cnt);                                                                          \
       FD_LAUNCH_CHECK();                                                                                             \
       return FD_OK;                                                                                                  \
     }
@@ -994,20 +1099,21 @@ int launch_halo(const fd_gemm_params* p, const HaloPlan& pl, hipStream_t s) {
   if (pl.pt) {
     if (pl.th != 16 || pl.bn != 128 || pl.sk || pl.ns != 3) return FD_ERR_ARG;
     if (gi)
-      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, true, false, 3, true, false>), grid, dim3(512), 0, s, *p, slabs, cnt);
+      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, true, false, 3, true, false, false>), grid, dim3(512), 0, s, *p, slabs, cnt);
     else
-      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, false, false, 3, true, false>), grid, dim3(512), 0, s, *p, slabs, cnt);
+      hipLaunchKernelGGL((conv_halo_kernel<T, 16, 128, false, false, 3, true, false, false>), grid, dim3(512), 0, s, *p, slabs, cnt);
     FD_LAUNCH_CHECK();
     return FD_OK;
   }
+#define FD_HALO_L(TH_, BN_, GI_, SK_, NS_, PP_)                                                                      \
+  hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, GI_, SK_, NS_, false, false, PP_>), grid, dim3(512), 0, s, *p, slabs, \
+                     cnt)
 #define FD_HALO(TH_, BN_, SK_, NS_)                                                                                  \
   if (pl.th == TH_ && pl.bn == BN_ && pl.sk == SK_ && pl.ns == NS_) {                                                \
-    if (gi)                                                                                                          \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, true, SK_, NS_, false, false>), grid, dim3(512), 0, s, *p, slabs,   \
-                         cnt);                                                                                       \
-    else                                                                                                             \
-      hipLaunchKernelGGL((conv_halo_kernel<T, TH_, BN_, false, SK_, NS_, false, false>), grid, dim3(512), 0, s, *p, slabs,  \
-                         cnt);                                                                                       \
+    if (gi && pp) FD_HALO_L(TH_, BN_, true, SK_, NS_, true);                                                                   \
+    else if (gi) FD_HALO_L(TH_, BN_, true, SK_, NS_, false);                                                                   \
+    else if (pp) FD_HALO_L(TH_, BN_, false, SK_, NS_, true);                                                                   \
+    else FD_HALO_L(TH_, BN_, false, SK_, NS_, false);                                                                          \
     FD_LAUNCH_CHECK();                                                                                               \
     return FD_OK;                                                                                                    \
   }
@@ -1020,11 +1126,8 @@ int launch_halo(const fd_gemm_params* p, const HaloPlan& pl, hipStream_t s) {
   FD_HALO(8, 128, 1, 3)
   FD_HALO(16, 160, 1, 3)
   FD_HALO(16, 128, 1, 3)
-  FD_HALO(8, 160, 0, 5)
-  FD_HALO(8, 128, 0, 5)
-  FD_HALO(8, 160, 1, 5)
-  FD_HALO(8, 128, 1, 5)
 #undef FD_HALO
+#undef FD_HALO_L
   return FD_ERR_ARG;
 }
 
@@ -1077,4 +1180,15 @@ extern "C" int fd_conv_halo_try(fd_gemm_params* p, void* stream) {
   else rc = launch_halo<f16>(&q, pl, (hipStream_t)stream);
   if (rc == FD_OK && q.gn_part) p->gn_done = pl.th * 16;
   return rc == FD_OK ? 1 : rc;
+}
+
+// Split-K hand-off health of this translation unit (see g8_splitk_health).
+int halo_splitk_health(unsigned* timeouts, int reset, int drop) {
+  unsigned v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_halo_sk_timeouts), sizeof(v)) != hipSuccess) return FD_ERR_HIP;
+  if (timeouts) *timeouts += v;
+  const unsigned z = 0u, d = (unsigned)drop;
+  if (reset && hipMemcpyToSymbol(HIP_SYMBOL(g_halo_sk_timeouts), &z, sizeof(z)) != hipSuccess) return FD_ERR_HIP;
+  if (drop >= 0 && hipMemcpyToSymbol(HIP_SYMBOL(g_halo_sk_drop), &d, sizeof(d)) != hipSuccess) return FD_ERR_HIP;
+  return FD_OK;
 }

@@ -539,7 +539,9 @@ __global__ void tlc_scale_input_kernel(const float* __restrict__ canvas, const i
                                        const int* __restrict__ col_org, int nc, int H, int W, int kh, int kw,
                                        int tile_begin, int ntiles, int cfg, float s, TO* __restrict__ out,
                                        float* __restrict__ t_out, int t_n, float t_val) {
-  if (t_out && blockIdx.x == 0 && (int)threadIdx.x < t_n) t_out[threadIdx.x] = t_val;  // the step's UNet timesteps
+  if (t_out) {  // the step's UNet timesteps (grid-stride: any number of UNet rows)
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < t_n; i += gridDim.x * blockDim.x) t_out[i] = t_val;
+  }
   const long long per = (long long)kh * kw;
   const long long total = (long long)ntiles * per;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
@@ -563,7 +565,7 @@ extern "C" int fd_tlc_scale_input_t(const float* canvas, const int* row_org, int
                                     int H, int W, int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma,
                                     void* out, int dtype, float* t_out, int t_n, float timestep, void* stream) {
   if (!canvas || !row_org || !col_org || !out) return FD_ERR_ARG;
-  if (t_n < 0 || t_n > 256 || (t_n > 0 && !t_out)) return FD_ERR_SHAPE;
+  if (t_n < 0 || (t_n > 0 && !t_out)) return FD_ERR_SHAPE;
   if (ntiles <= 0 || tile_begin < 0 || tile_begin + ntiles > nr * nc || kh > H || kw > W || cfg <= 0)
     return FD_ERR_SHAPE;
   // scale_model_input divides by (sigma^2 + 1)^0.5 (diffusers EulerDiscreteScheduler; pipeline:1336): `sigma`

@@ -16,51 +16,55 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 
 // Launch-planner knobs (knobs.hip): tested defaults, switched only by tests / probes through fd_set_knob.
 enum fd_knob_id {
-  FDK_GEMM8, FDK_GEMM8_S, FDK_GEMM8_GM, FDK_GEMM_R4, FDK_GEMM_P128, FDK_GEMM_R4_NS, FDK_GEMM_B4, FDK_GEMM8_W160,
-  FDK_GEMM8_N128, FDK_GEMM8_LNP, FDK_GEMM8_LNP_S, FDK_GEMM8_MIDK, FDK_F8_TILE, FDK_F8_KERNEL, FDK_GEMM_CFG,
-  FDK_GEMM_NS, FDK_GEMM_KS, FDK_GEMM_SWZ, FDK_GEMM_MODE, FDK_GEMV, FDK_GEMM256, FDK_GEMM256_MIN_TILES,
+  FDK_GEMM8, FDK_GEMM8_S, FDK_GEMM8_GM, FDK_GEMM8_W160, FDK_GEMM8_LNP, FDK_GEMM8_MIDK, FDK_F8_TILE, FDK_GEMM_CFG,
+  FDK_GEMM_SWZ, FDK_GEMM_MODE, FDK_GEMV, FDK_GEMM256, FDK_GEMM256_MIN_TILES,
   FDK_GN_MIN_CHUNKS, FDK_GN_APPLY_V, FDK_GN_APPLY_BLOCKS, FDK_GN_APPLY_U, FDK_FLASH_SWZ, FDK_FLASH_WAVES,
-  FDK_FLASH_QPW, FDK_CONV_HALO, FDK_CONV_HALO_MIN_TILES, FDK_CONV_HALO_SPLIT, FDK_CONV_HALO_NS8, FDK_GEMM_GMP, FDK_GEMM8_W128, FDK_GEMM8_LNP_K, FDK_XATTN_SPLIT, FDK_CONV_HALO_PT, FDK_CONV_HALO_NS16, FDK_CONV_HALO_SPLIT16,
-  FDK_GEMM8_LNP_BIG, FDK_COUNT
+  FDK_FLASH_QPW, FDK_CONV_HALO, FDK_CONV_HALO_MIN_TILES, FDK_CONV_HALO_SPLIT, FDK_GEMM_GMP, FDK_CONV_HALO_PT,
+  FDK_CONV_HALO_NS16, FDK_CONV_HALO_SPLIT16, FDK_CONV_HALO_PP, FDK_COUNT
 };
 int fd_knob(int id);
 // gemm256.hip: whether fd_gemm256_try takes this launch
 int gemm256_takes(const fd_gemm_params* p);
 extern "C" int fd_conv_halo_try(fd_gemm_params* p, void* stream);
+// split-K hand-off health per translation unit (gemm8.hip, conv_halo.hip); fd_splitk_health sums them
+int g8_splitk_health(unsigned* timeouts, int reset, int drop);
+int halo_splitk_health(unsigned* timeouts, int reset, int drop);
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
 // Cache policy of the output stores of the GEMM / conv epilogues, GroupNorm apply, concat and flash attention
 // (FD_EPI_WT, build time): 0 plain (write-back L2: the kernel-end release then writes every dirty line back, after
 // the last wave), 1 sc1 (device scope: written through as stored, nothing left dirty at the end), 2 nt, 4 sc1 nt.
-// Inline asm: the waitcnt pass does not see these stores, which can only make a later vmcnt wait longer; nor does
-// the hazard recognizer, so the 16-B form carries its own wait states (a VALU may not overwrite the data VGPRs of a
-// > 8-byte VMEM store in the next cycles: hipcc placed a v_add into v0 of a v[0:3] store right behind it).
+// The policy bits ride on a buffer store (raw_buffer_store_b128 / _b64 with the cache-policy operand), which the
+// compiler sees -- its waitcnt pass and hazard recognizer account for it.  (Round 5 used inline-asm global stores
+// with a hand-placed s_nop after the compiler put a VALU write into a store's data VGPRs right behind it.)  The
+// buffer resource is wave-uniform: the first active lane's address - 2^31, so each lane's 32-bit offset is
+// 2^31 + (its address - that lane's); every caller's per-instruction span across a wave is far below 2 GiB.
 #ifndef FD_EPI_WT
 #define FD_EPI_WT 1
 #endif
-#if FD_EPI_WT == 1
-#define FD_WT_BITS "sc1"
-#elif FD_EPI_WT == 2
-#define FD_WT_BITS "nt"
-#elif FD_EPI_WT == 4
-#define FD_WT_BITS "sc1 nt"
-#else
-#define FD_WT_BITS ""
-#endif
+constexpr int kWtAux = FD_EPI_WT == 1 ? 16 : FD_EPI_WT == 2 ? 2 : FD_EPI_WT == 4 ? 18 : 0;  // gfx950 cpol: sc1 16, nt 2
 // Cache-policy bits of the GEMM / conv weight-operand LDS-DMA loads (build-time A/B): 0 default, 2 nt
 #ifndef FD_WLD_AUX
 #define FD_WLD_AUX 0
 #endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* p, unsigned& voff) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const unsigned long long base = (((unsigned long long)hi << 32) | lo) - 0x80000000ull;
+  voff = (unsigned)(a - base);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)0xffffffff, 0x00020000);
+}
 // 16-B store (other widths: plain)
 template <typename V>
 __device__ __forceinline__ void st_out16(V* p, const V& v) {
   if constexpr (FD_EPI_WT == 0 || sizeof(V) != 16) {
     *p = v;
   } else {
-    typedef __attribute__((ext_vector_type(4))) unsigned u4;
-    asm volatile("global_store_dwordx4 %0, %1, off " FD_WT_BITS "\n\ts_nop 1" ::"v"(p), "v"(__builtin_bit_cast(u4, v))
-                 : "memory");
+    unsigned off;
+    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(p, off);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, off, 0, kWtAux);
   }
 }
 // 8-B store (other widths: plain)
@@ -69,8 +73,9 @@ __device__ __forceinline__ void st_out8(V* p, const V& v) {
   if constexpr (FD_EPI_WT == 0 || sizeof(V) != 8) {
     *p = v;
   } else {
-    typedef __attribute__((ext_vector_type(2))) unsigned u2;
-    asm volatile("global_store_dwordx2 %0, %1, off " FD_WT_BITS ::"v"(p), "v"(__builtin_bit_cast(u2, v)) : "memory");
+    unsigned off;
+    const __amdgpu_buffer_rsrc_t rs = wt_rsrc(p, off);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, off, 0, kWtAux);
   }
 }
 

@@ -572,26 +572,20 @@ static int pick_cfg(const fd_gemm_params* p) {
   return best;
 }
 
-// Tuning overrides (knob table, benchmarks only): FD_GEMM_CFG=<0..3> forces the tile, FD_GEMM_NS=<2|3|4> the ring
-// depth, FD_GEMM_SWZ=<0|1> the tile order.
+// Tuning overrides (knob table, benchmarks only): FD_GEMM_CFG=<0..3> forces the tile, FD_GEMM_SWZ=<0|1> the tile
+// order.  Ring depth: 4 stages (one workgroup per CU) when one round of tiles covers the launch and K >= 512, else 2;
+// each K step split over two wave groups (KS = 2, 8 waves).  (Round 6: the knob-only 3-stage ring and KS = 1 forms,
+// measured slower -- profiles/r04zl_gemm_ns_ab.txt, scripts/gemm_ks.sh history -- were removed.)
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
-static int dispatch_ns(const fd_gemm_params* p, hipStream_t s, int ns, int ks, int swz) {
+static int dispatch_ns(const fd_gemm_params* p, hipStream_t s, int ns, int swz) {
   constexpr int STAGE = (BM + BN) * 128;
-  constexpr bool NS3 = 3 * STAGE <= 160 * 1024, NS4 = 4 * STAGE <= 160 * 1024;
-  if (ns == 4 && !NS4) ns = NS3 ? 3 : 2;
-  if (ns == 3 && !NS3) ns = 2;
+  constexpr bool NS4 = 4 * STAGE <= 160 * 1024;
   if constexpr (std::is_same<T, TO>::value) {
-    if (ks == 2) {
-      if (ns == 2) return launch_cfg<T, BM, BN, WM, WN, 2, TO, 2>(p, s, swz);
-      if constexpr (NS3) if (ns == 3) return launch_cfg<T, BM, BN, WM, WN, 3, TO, 2>(p, s, swz);
-      if constexpr (NS4) return launch_cfg<T, BM, BN, WM, WN, 4, TO, 2>(p, s, swz);
-      return FD_ERR_ARG;
+    if constexpr (NS4) {
+      if (ns == 4) return launch_cfg<T, BM, BN, WM, WN, 4, TO, 2>(p, s, swz);
     }
-    if (ns == 2) return launch_cfg<T, BM, BN, WM, WN, 2, TO>(p, s, swz);
-    if constexpr (NS3) if (ns == 3) return launch_cfg<T, BM, BN, WM, WN, 3, TO>(p, s, swz);
-    if constexpr (NS4) return launch_cfg<T, BM, BN, WM, WN, 4, TO>(p, s, swz);
-    return FD_ERR_ARG;
+    return launch_cfg<T, BM, BN, WM, WN, 2, TO, 2>(p, s, swz);
   } else {
     return launch_cfg<T, BM, BN, WM, WN, 2, TO>(p, s, swz);
   }
@@ -636,7 +630,7 @@ static int plan_group_m(long long tiles_total, int tiles_m, int tiles_n, int bm,
 
 template <typename T, typename TO>
 static int dispatch_tiles(fd_gemm_params* p0, hipStream_t s) {
-  const int g_cfg = fd_knob(FDK_GEMM_CFG), g_ns = fd_knob(FDK_GEMM_NS), g_ks = fd_knob(FDK_GEMM_KS);
+  const int g_cfg = fd_knob(FDK_GEMM_CFG);
   const int g_swz = fd_knob(FDK_GEMM_SWZ) | (fd_knob(FDK_GEMM_MODE) << 4);
   int cfg = g_cfg >= 0 && g_cfg < CFG_COUNT ? g_cfg : pick_cfg(p0);
   if (p0->ln_out) cfg = CFG_64x160;  // LN-fold producer: partials per 160 columns, whatever M (batch-invariant)
@@ -651,16 +645,15 @@ static int dispatch_tiles(fd_gemm_params* p0, hipStream_t s) {
   // KS = 2 (8 waves, intra-WG split of each K step) measured >= KS = 1 on every UNet shape
   // (scripts/gemm_ks.sh: 2048x1280x5120 60 -> 42 us); the 4-deep ring pays whenever one wave of tiles
   // covers the launch (one WG per CU either way).
-  const int ns = g_ns ? g_ns : ((tiles <= 256 && p->K >= 512) ? 4 : 2);
-  const int ks = g_ks ? g_ks : 2;
+  const int ns = (tiles <= 256 && p->K >= 512) ? 4 : 2;
   const int tm_ = (p->M + CFG_BM[cfg] - 1) / CFG_BM[cfg], tn_ = (p->N + CFG_BN[cfg] - 1) / CFG_BN[cfg];
   const int swz = g_swz | (plan_group_m(tm_ * (long long)tn_, tm_, tn_, CFG_BM[cfg], CFG_BN[cfg]) << 8);
   int rc;
   switch (cfg) {
-    case CFG_128x128: rc = dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, ks, swz); break;
-    case CFG_64x160: rc = dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, ks, swz); break;
-    case CFG_128x64: rc = dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, ks, swz); break;
-    default: rc = dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, ks, swz);
+    case CFG_128x128: rc = dispatch_ns<T, TO, 128, 128, 64, 64>(p, s, ns, swz); break;
+    case CFG_64x160: rc = dispatch_ns<T, TO, 64, 160, 32, 80>(p, s, ns, swz); break;
+    case CFG_128x64: rc = dispatch_ns<T, TO, 128, 64, 64, 32>(p, s, ns, swz); break;
+    default: rc = dispatch_ns<T, TO, 64, 64, 32, 32>(p, s, ns, swz);
   }
   if (rc == FD_OK && q.gn_part) p0->gn_done = 128;
   return rc;

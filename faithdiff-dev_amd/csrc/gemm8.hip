@@ -82,6 +82,11 @@ __device__ __forceinline__ void vm_wait() {
 // T = mx8_t: A carries E8M0 block scales ([M][K / 32] bytes): each stage also DMAs the tile's BM x 4 scale bytes
 // (one dword per row) into LDS, and every MFMA takes its lane's byte as the A scale.  TO = uint8_t: the output is
 // written as MX e4m3 (+ block scales f8.o_bs), each 32-column block's amax reduced over its 4 epilogue threads.
+// Split-K hand-off health (fd_splitk_health): pairwise waits that timed out in this library's gemm8 launches, and
+// a test hook that makes the publishing split skip its flag (forces the timeout path).
+__device__ unsigned g_g8_sk_timeouts;
+__device__ unsigned g_g8_sk_drop;
+
 template <typename T, int BM, int BN, int NW, int WAVES_M, int NS, bool CONV, bool GEGLU, typename TO,
           bool LNF = false>
 __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, const int S, const int gm_mode,
@@ -562,13 +567,15 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
                                                  ((mi * NT + ni) * NTHR + tid) * 16, 0, 16);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0 && !__hip_atomic_load(&g_g8_sk_drop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
     if (tid == 0) {
-      // bounded: a lost flag poisons the tile (NaN, so the forward's finiteness checks see it) instead of hanging
-      // the GPU; the flag and the counter are reset only after the partner's flag was seen, never on the timeout
-      // path (a late partner's flag must not be taken for a later launch's)
+      // bounded: a lost flag poisons the tile (NaN) instead of hanging the GPU, and counts a timeout in
+      // g_g8_sk_timeouts.  The flag and the counter are reset only after the partner's flag was seen, so after a
+      // timeout this tile's slot is stale (a late flag could be taken by a later launch): the host checks the count
+      // at its sync points (fd_splitk_health, ops.split_k_health) and re-zeroes every workspace's counters.
       unsigned got = 0u;
       for (int it = 0; it < (1 << 24) && !got; ++it) {
         got = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -577,6 +584,8 @@ __global__ void __launch_bounds__(64 * NW) gemm8_kernel(const fd_gemm_params p, 
       if (got) {
         __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(counters + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        __hip_atomic_fetch_add(&g_g8_sk_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       ((volatile unsigned*)smem)[1] = got;
     }
@@ -1013,7 +1022,13 @@ int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
   dim3 grid(pl.tiles * pl.S), block(64 * NW);
   float* slabs = (float*)((char*)p->ws + 65536 * sizeof(unsigned));
   unsigned* cnt = (unsigned*)p->ws;
-  if (p->conv) {
+  if constexpr (BM < 256) {  // 128 / 64-row tiles: plan8 gives them only plain GEMMs (LN-fold producers, score GEMMs)
+    if (p->conv || p->act == FD_ACT_GEGLU || p->ln_in) return FD_ERR_ARG;
+  }
+  if constexpr (BM < 256) {
+    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO>), grid, block, 0, s, *p, pl.S,
+                       pl.group_m, slabs, cnt, f8_args{});
+  } else if (p->conv) {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, true, false, TO>), grid, block, 0, s, *p, pl.S,
                        pl.group_m, slabs, cnt, f8_args{});
   } else if (p->act == FD_ACT_GEGLU) {
@@ -1046,30 +1061,21 @@ int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
 // and any tile shape of the same kernel family gives the same k order.
 static int plan8(const fd_gemm_params* p, Plan8* pl) {
   const int enabled = fd_knob(FDK_GEMM8), force_s = fd_knob(FDK_GEMM8_S), force_gm = fd_knob(FDK_GEMM8_GM);
-  // 64 x 160 one-wave-per-SIMD kernel: 0 off (default: 0.5 % slower in the bench step than the 4-wave kernel though
-  // faster in isolation), 1 <= 256 tiles, 2 every non-GEGLU
-  const int r4 = fd_knob(FDK_GEMM_R4), pair128 = fd_knob(FDK_GEMM_P128), r4_ns = fd_knob(FDK_GEMM_R4_NS);
-  const int b4 = fd_knob(FDK_GEMM_B4);
   const int w160 = fd_knob(FDK_GEMM8_W160);  // bit 0: 256 x 160 tiles where faster; bit 1: also take N = 320
   const int m_ref = p->m_ref > 0 ? p->m_ref : p->M;
   if (!enabled || p->batch > 1 || p->K < 128) return 0;
-  // 128-channel 3x3 convs on >= 512^2 images (the VAE decoder's last up block and the encoders' first level at
-  // 1024^2: 2048+ tiles, 8+ rounds) on the 4-wave kernel's 128 x 128 tiles, two workgroups per CU (one tile's
-  // prologue / epilogue under the other's main loop): 15 % faster than gemm8 256 x 128 without GroupNorm
-  // statistics (profiles/r03_vae_tile_ab.txt), but only 3 % with them, and the decode as a whole 0.1 ms slower
-  // (profiles/r03_n128_ab.txt).  Off by default; FD_GEMM8_N128=1 routes them (A/B).
-  const int n128 = fd_knob(FDK_GEMM8_N128);
-  if (n128 && p->conv && p->N == 128 && m_ref >= 262144) return 0;
+  // (round 6: the variants measured slower and kept only as knobs were removed -- the 64 x 160 one-wave-per-SIMD
+  // instance, the pairwise 128-row split at M = 2048, the 4-deep 128 x 160 ring, the 128-channel convs on the 4-wave
+  // kernel, the split cross-attention score GEMM, the 256 x 160 S-way and large-M LN-fold producers, and the four-wave
+  // 128 x 160 tile; their measurements are in DESIGN.md section 5 and git history)
   Plan8 q;
   if (p->act == FD_ACT_SOFTMAX) {
     // the attention-score GEMM: 160-column tiles (two 80-column head groups): the tile with the fewest operand bytes
     // per CU, rounds on 256 CUs x (BM + BN); FD_XATTN_SPLIT: the 128 x 160 form with K split in two (pairwise
     // combine, softmax after it) -- 320 half-K workgroups instead of 160 full ones at M = 2048 (measured slower)
     if (p->N % 160) return 0;
-    // one K pass: every tile shape gives the same bits, so the batched M may choose (C3's 13 tiles: 256 x 160);
-    // with the split the plan must come from m_ref (the split changes the summation order)
-    const int xsplit = fd_knob(FDK_XATTN_SPLIT);
-    const int m_plan = xsplit ? m_ref : p->M;
+    // one K pass: every tile shape gives the same bits, so the batched M may choose (C3's 13 tiles: 256 x 160)
+    const int m_plan = p->M;
     int best = 0;
     long long bc = 0;
     for (int bm = 256; bm >= 64; bm /= 2) {
@@ -1082,11 +1088,10 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     }
     q.bm = best;
     q.bn = 160;
-    const int w8 = fd_knob(FDK_GEMM8_W128);
-    q.nw = (best == 256 || (best == 128 && w8)) ? 8 : 4;
-    q.waves_m = best == 256 ? 8 : (best == 128 && w8) ? 4 : 2;
+    q.nw = best >= 128 ? 8 : 4;  // 128 x 160: eight waves of 32 x 80 (two per SIMD)
+    q.waves_m = best == 256 ? 8 : best == 128 ? 4 : 2;
     q.ns = 3;
-    q.S = (best == 128 && xsplit && p->K >= 1024) ? 2 : 1;
+    q.S = 1;
     goto planned;
   }
   if (p->ln_out) {
@@ -1094,40 +1099,15 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
     // of the 32^2 level, 2048 x 1280 x 5120 at C2): 128 x 160 tiles with K split in two (pairwise combine),
     // 0.64x the operand bytes per CU of the 4-wave 64 x 160 producer (probe with cold weights 47.1 -> 40.6 us,
     // profiles/r02e_m2048_split.jsonl); anything else stays on that producer (return 0).
-    // large-M producers (>= 256 tiles of 256 x 160 per TLC tile: the information transformer's out_proj / c_proj at
-    // 128^2, M = 32768): eight-wave 256 x 160 tiles in one K pass, 2+ rounds on 256 CUs, instead of 2048 4-wave
-    // 64 x 160 tiles (0.47x the operand bytes per output); the partial layout is the same (per row and 160 columns)
-    if (fd_knob(FDK_GEMM8_LNP_BIG) && p->act != FD_ACT_GEGLU && !p->conv && p->N % 160 == 0 && m_ref >= 256 &&
-        (long long)(m_ref / 256) * (p->N / 160) >= 256) {
-      q.bm = 256;
-      q.bn = 160;
-      q.nw = 8;
-      q.waves_m = 8;
-      q.ns = 3;
-      q.S = 1;
-      goto planned;
-    }
     const int lnp = fd_knob(FDK_GEMM8_LNP);
-    const int lnp_s = fd_knob(FDK_GEMM8_LNP_S);  // splits of the 256 x 160 form (lnp = 2)
-    // FD_GEMM8_LNP_K: the least K routed here (4096: the ff outs; 1024 also takes the K = 1280 / 1600 producers of
-    // the 32^2 level -- attention out-projections, proj_in -- on the eight-wave 128 x 160 pairwise split)
-    if (!lnp || p->act == FD_ACT_GEGLU || p->conv || p->N % 160 || p->K < fd_knob(FDK_GEMM8_LNP_K) || m_ref < 128)
-      return 0;
+    // K >= 4096 (the ff outs); shorter producers (attention out-projections, proj_in) stay on the 4-wave 64 x 160 tile
+    if (!lnp || p->act == FD_ACT_GEGLU || p->conv || p->N % 160 || p->K < 4096 || m_ref < 128) return 0;
     if ((long long)((m_ref + 63) / 64) * (p->N / 160) > 256) return 0;
-    if (lnp == 2 && m_ref >= 256) {  // 256 x 160 tiles (0.76x the operand bytes per CU of 128 x 160), S-way K split
-      q.bm = 256;
-      q.bn = 160;
-      q.nw = 8;
-      q.waves_m = 8;
-      q.ns = 3;
-      q.S = lnp_s;
-      goto planned;
-    }
     q.bm = 128;
     q.bn = 160;
-    // eight waves of 32 x 80 (two per SIMD: one wave's fragment reads under the other's MFMAs) or four of 64 x 80
-    q.nw = fd_knob(FDK_GEMM8_W128) ? 8 : 4;
-    q.waves_m = q.nw == 8 ? 4 : 2;
+    // eight waves of 32 x 80 (two per SIMD: one wave's fragment reads under the other's MFMAs)
+    q.nw = 8;
+    q.waves_m = 4;
     q.ns = 3;
     q.S = 2;
     goto planned;
@@ -1157,38 +1137,7 @@ static int plan8(const fd_gemm_params* p, Plan8* pl) {
       }
     }
   }
-  if (q.S <= 0) {
-    const long long tiles_ref = (long long)((m_ref + 63) / 64) * ((p->N + 159) / 160);
-    const long long tiles128 = (long long)((m_ref + 127) / 128) * ((p->N + 159) / 160);
-    if (b4 && p->act != FD_ACT_GEGLU && p->N >= 160 && tiles128 >= 256) {
-      // large M (the 64^2 / 128^2 levels): 128 x 160 tiles, one wave per SIMD, 0.64x the operand bytes
-      // per output of the 64 x 160 tile
-      q.bm = 128;
-      q.bn = 160;
-      q.nw = 4;
-      q.waves_m = 2;
-      q.ns = 3;
-      q.S = 1;
-      goto planned;
-    }
-    {
-    const bool ok = r4 && p->act != FD_ACT_GEGLU && m_ref >= 64 && p->N >= 160 &&
-                    (r4 == 2 || (!p->conv && tiles_ref <= 256));
-    if (!ok) return 0;
-    q.bm = 64;
-    q.bn = 160;
-    q.nw = 4;
-    q.waves_m = 2;
-    q.ns = r4_ns;
-    q.S = 1;
-    if (pair128 && m_ref >= 128 && tiles_ref <= 256 && p->K >= 1024) {
-      // 128 x 160 tiles with K split in two (pairwise combine): 0.64x the operand bytes per CU
-      q.bm = 128;
-      q.ns = 3;
-      q.S = 2;
-    }
-    }
-  }
+  if (q.S <= 0) return 0;  // few tiles and short K: the 4-wave kernel (gemm.hip)
 planned:
   if (q.S > p->K / 64) q.S = p->K / 64;
   const int tiles_m = (p->M + q.bm - 1) / q.bm, tiles_n = (p->N + q.bn - 1) / q.bn;
@@ -1262,16 +1211,10 @@ extern "C" int fd_gemm8_try(fd_gemm_params* p0, void* stream) {
     FD_G8(256, 160, 8, 8, 3);
   } else if (pl.bm == 256) {
     FD_G8(256, 128, 8, 4, 3);
-  } else if (pl.bm == 128 && pl.nw == 8) {
-    FD_G8(128, 160, 8, 4, 3);
   } else if (pl.bm == 128) {
-    FD_G8(128, 160, 4, 2, 3);
-  } else if (pl.ns >= 5) {
-    FD_G8(64, 160, 4, 2, 5);
-  } else if (pl.ns == 4) {
-    FD_G8(64, 160, 4, 2, 4);
+    FD_G8(128, 160, 8, 4, 3);
   } else {
-    FD_G8(64, 160, 4, 2, 3);
+    FD_G8(64, 160, 4, 2, 3);  // the 64-row score-GEMM tile (M <= 64 per launch)
   }
 #undef FD_G8
   if (rc == FD_OK) p0->gn_done = q.gn_part != nullptr ? 256 : 0;
@@ -1334,7 +1277,7 @@ int plan_e4m3(const fd_gemm_params* p, bool mx_out, Plan8* pl) {
   pl->bn = cands[best].bn;
   pl->nw = cands[best].nw;
   pl->waves_m = cands[best].wm;
-  if (pl->bm == 128 && fd_knob(FDK_GEMM8_W128)) {  // eight waves of 32 x 80 (as the 16-bit 128 x 160 tiles)
+  if (pl->bm == 128) {  // eight waves of 32 x 80 (as the 16-bit 128 x 160 tiles)
     pl->nw = 8;
     pl->waves_m = 4;
   }
@@ -1361,8 +1304,7 @@ int launch_e4m3(const fd_gemm_params* p, const Plan8& pl, const f8_args& f8, int
 #define FD_G8F(TO_)                                                                            \
   if (pl.bm == 256 && pl.bn == 160) rc = launch8_e4m3<T, TO_, 256, 160, 8, 8>(p, pl, f8, s);   \
   else if (pl.bm == 256) rc = launch8_e4m3<T, TO_, 256, 128, 8, 4>(p, pl, f8, s);              \
-  else if (pl.bm == 128 && pl.nw == 8) rc = launch8_e4m3<T, TO_, 128, 160, 8, 4>(p, pl, f8, s); \
-  else if (pl.bm == 128) rc = launch8_e4m3<T, TO_, 128, 160, 4, 2>(p, pl, f8, s);              \
+  else if (pl.bm == 128) rc = launch8_e4m3<T, TO_, 128, 160, 8, 4>(p, pl, f8, s);              \
   else rc = launch8_e4m3<T, TO_, 64, 160, 4, 2>(p, pl, f8, s);
   if (out_dtype == FD_BF16) {
     FD_G8F(bf16)
@@ -1435,4 +1377,16 @@ extern "C" int fd_gemm_mxe4m3(const void* A8, long long lda, const void* a_bs, l
   if (!plan_e4m3(&p, mx_out, &pl)) return FD_ERR_SHAPE;
   f8_args f8{nullptr, (const uint8_t*)a_bs, ldas, (uint8_t*)c_bs, ldcs};
   return launch_e4m3<mx8_t>(&p, pl, f8, out_dtype, (hipStream_t)stream);
+}
+
+// Split-K hand-off health of this translation unit (fd_splitk_health in knobs.hip sums the units): adds the timed-out
+// pairwise waits to *timeouts; reset: zero the count; drop >= 0: set the test hook (1: publishers skip their flag).
+int g8_splitk_health(unsigned* timeouts, int reset, int drop) {
+  unsigned v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_g8_sk_timeouts), sizeof(v)) != hipSuccess) return FD_ERR_HIP;
+  if (timeouts) *timeouts += v;
+  const unsigned z = 0u, d = (unsigned)drop;
+  if (reset && hipMemcpyToSymbol(HIP_SYMBOL(g_g8_sk_timeouts), &z, sizeof(z)) != hipSuccess) return FD_ERR_HIP;
+  if (drop >= 0 && hipMemcpyToSymbol(HIP_SYMBOL(g_g8_sk_drop), &d, sizeof(d)) != hipSuccess) return FD_ERR_HIP;
+  return FD_OK;
 }

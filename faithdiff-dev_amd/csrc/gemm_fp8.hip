@@ -8,9 +8,10 @@
 //   (act = SiLU / GELU / QuickGELU, or GEGLU over packed [hidden | gate] row groups -> N/2 columns)
 //
 // Tiles: 128x128 (or 64x128 when 128-row tiles cannot fill 256 CUs) per 256-thread workgroup, 2x2 waves,
-// K-step 128 bytes.  K % 128 == 0: operands go global -> LDS by DMA into a 2/3-stage ring (gemm_e4m3_dma_kernel).
-// Ragged K: global -> registers (next K-step prefetched while the MFMAs run) -> double-buffered LDS (144-B pitch:
-// the 16 rows one ds_read_b128 phase touches land on 16 disjoint 4-bank groups) -> fragments.
+// K-step 128 bytes.  These 4-wave kernels take ragged K only (K % 128 != 0); K % 128 == 0 runs on the eight-wave
+// family (gemm8.hip).  Operands go global -> registers (next K-step prefetched while the MFMAs run) ->
+// double-buffered LDS (144-B pitch: the 16 rows one ds_read_b128 phase touches land on 16 disjoint 4-bank groups)
+// -> fragments.
 // MFMA operand map (16x16x128, 8-bit): lane l holds row (l & 15), k = 32*(l >> 4) + j, j = 0..31,
 // i.e. 32 contiguous bytes of one row; C/D: col = l & 15, row = 4*(l >> 4) + r.
 #include <stdlib.h>
@@ -201,169 +202,6 @@ template <> struct F8Vec<float> {
   }
 };
 
-// Vector epilogue through LDS (needs BM * 128 * 4 bytes of `ep`, the drained operand ring): phase 1 writes
-// act(scale * acc + bias) -- GEGLU already combined -- as fp32 into a [BM][W] tile (W = 128, or 64 output
-// columns for GEGLU); phase 2 gives each thread 8 contiguous columns: one 16-B residual load and one 16-B
-// store per chunk instead of eight 2-byte ones.  Requires nout % 8 == 0, ldc % 8 == 0, ldr % 8 == 0.
-template <typename TO, int BM, int MI>
-__device__ __forceinline__ void f8_epilogue_vec(const f32x4 (&acc)[MI][4], float* ep, int m0, int n0, int wm,
-                                                int wn, int lane, const float* __restrict__ a_scale,
-                                                float w_scale, TO* __restrict__ C, long long ldc, int M, int N,
-                                                const float* __restrict__ bias, const TO* __restrict__ R,
-                                                long long ldr, int act) {
-  const bool geglu = act == FD_ACT_GEGLU;
-  const int W = geglu ? F8_BN / 2 : F8_BN;
-  __syncthreads();  // every wave is done reading the operand ring
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int lr = wm + i * 16 + (lane >> 4) * 4 + r;
-      const float s = a_scale[min(m0 + lr, M - 1)] * w_scale;
-      if (geglu) {
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          const int nh = min(n0 + wn + g * 32, N - 32) + (lane & 15);  // whole groups past N: clamped, unused
-          const float hv = __builtin_fmaf(acc[i][2 * g][r], s, bias ? bias[nh] : 0.f);
-          const float gv = __builtin_fmaf(acc[i][2 * g + 1][r], s, bias ? bias[nh + 16] : 0.f);
-          ep[lr * W + (wn / 32 + g) * 16 + (lane & 15)] = hv * gelu_f(gv);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int lc = wn + j * 16 + (lane & 15);
-          float v = __fmul_rn(acc[i][j][r], s);
-          if (bias) v += bias[min(n0 + lc, N - 1)];
-          if (act != FD_ACT_NONE) v = act_f(v, act);
-          ep[lr * W + lc] = v;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  const int nout = geglu ? N / 2 : N, c0 = geglu ? n0 / 2 : n0;
-  const int cpr = W / 8;  // 8-column chunks per row
-  for (int c = threadIdx.x; c < BM * cpr; c += F8_NT) {
-    const int lr = c / cpr, lc = (c - lr * cpr) * 8;
-    const int m = m0 + lr, n = c0 + lc;
-    if (m >= M || n >= nout) continue;
-    float v[8];
-    const f32x4 a = *(const f32x4*)(ep + lr * W + lc), b = *(const f32x4*)(ep + lr * W + lc + 4);
-    v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
-    if (R) {
-      float rv[8];
-      F8Vec<TO>::ld(R + (long long)m * ldr + n, rv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += rv[e];
-    }
-    F8Vec<TO>::st(C + (long long)m * ldc + n, v);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void f8_wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// K % 128 == 0 variant: operands go global -> LDS by global_load_lds_dwordx4 (no VGPR round trip) into an
-// NS-deep ring, stages kt+1 .. kt+NS-2 in flight under stage kt's MFMAs (counted vmcnt, one raw barrier per
-// K-step).  A 128-byte K-step of e4m3 is byte-for-byte the 64-element bf16 K-step of gemm.hip, so the same
-// layout applies: 128-B LDS rows, the 16-B chunk c of row r stored at slot c ^ ((r >> 1) & 7) (applied on the
-// per-lane global source address, since the LDS-DMA destination is lane-linear), and the fragment's two
-// chunks 2*(lane >> 4) and 2*(lane >> 4) + 1 read back through the same XOR.  Rows past M / N are clamped.
-template <typename TO, int BM, int NS>
-__global__ __launch_bounds__(F8_NT) void gemm_e4m3_dma_kernel(const uint8_t* __restrict__ A, long long lda,
-                                                               const float* __restrict__ a_scale,
-                                                               const uint8_t* __restrict__ W, long long ldw,
-                                                               float w_scale, TO* __restrict__ C, long long ldc,
-                                                               int M, int N, int K, const float* __restrict__ bias,
-                                                               const TO* __restrict__ R, long long ldr, int act,
-                                                               int vec) {
-  constexpr int MI = BM / 32;
-  static_assert(NS * (BM + F8_BN) * 128 >= BM * F8_BN * 4, "vector epilogue tile must fit in the ring");
-  constexpr int A_INSTR = BM / 32, B_INSTR = F8_BN / 32;  // 1-KB DMA instructions per wave per stage
-  constexpr int PER = A_INSTR + B_INSTR;
-  constexpr int A_BYTES = BM * 128, STAGE = (BM + F8_BN) * 128;
-  __shared__ __attribute__((aligned(1024))) uint8_t smem[NS * STAGE];
-  const int tn = (N + F8_BN - 1) / F8_BN, tm = (M + BM - 1) / BM;
-  const int b = xcd_remap(blockIdx.x, tn * tm);
-  const int m0 = (b / tn) * BM, n0 = (b % tn) * F8_BN;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = (wid >> 1) * (BM / 2), wn = (wid & 1) * 64;
-
-  // loader: instruction i of wave w fills LDS rows (i*4 + w)*8 .. +7; lane -> row (lane >> 3), slot (lane & 7)
-  const int lrow = lane >> 3, slot = lane & 7;
-  const uint8_t* a_src[A_INSTR];
-  const uint8_t* b_src[B_INSTR];
-#pragma unroll
-  for (int i = 0; i < A_INSTR; ++i) {
-    const int r = (i * 4 + wid) * 8 + lrow;
-    a_src[i] = A + (long long)min(m0 + r, M - 1) * lda + ((slot ^ ((r >> 1) & 7)) << 4);
-  }
-#pragma unroll
-  for (int i = 0; i < B_INSTR; ++i) {
-    const int r = (i * 4 + wid) * 8 + lrow;
-    b_src[i] = W + (long long)min(n0 + r, N - 1) * ldw + ((slot ^ ((r >> 1) & 7)) << 4);
-  }
-  auto stage = [&](int kt, int buf) {
-    const int k0 = kt * F8_BK;
-    uint8_t* sa = smem + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < A_INSTR; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(a_src[i] + k0), LDS_PTR(sa + (i * 4 + wid) * 1024), 16, 0, 0);
-    uint8_t* sb = sa + A_BYTES;
-#pragma unroll
-    for (int i = 0; i < B_INSTR; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + k0), LDS_PTR(sb + (i * 4 + wid) * 1024), 16, 0, 0);
-  };
-
-  f32x4 acc[MI][4];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / F8_BK;
-#pragma unroll
-  for (int s0 = 0; s0 < NS - 1; ++s0)
-    if (s0 < nk) stage(s0, s0);
-  const int fr = lane & 15, c0 = 2 * (lane >> 4);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = min(NS - 2, nk - 1 - kt);
-    if (NS >= 4 && ahead >= 2) f8_wait_vmcnt<(NS >= 4 ? 2 * PER : 0)>();
-    else if (NS >= 3 && ahead >= 1) f8_wait_vmcnt<(NS >= 3 ? PER : 0)>();
-    else f8_wait_vmcnt<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (kt + NS - 1 < nk) stage(kt + NS - 1, (kt + NS - 1) % NS);
-    const uint8_t* sa = smem + (kt % NS) * STAGE;
-    const uint8_t* sb = sa + A_BYTES;
-    i32x8 fa[MI], fb[4];
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int r = wm + i * 16 + fr, sw = (r >> 1) & 7;
-      const u32x4 lo = *(const u32x4*)(sa + r * 128 + ((c0 ^ sw) << 4));
-      const u32x4 hi = *(const u32x4*)(sa + r * 128 + (((c0 + 1) ^ sw) << 4));
-      fa[i] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = wn + j * 16 + fr, sw = (r >> 1) & 7;
-      const u32x4 lo = *(const u32x4*)(sb + r * 128 + ((c0 ^ sw) << 4));
-      const u32x4 hi = *(const u32x4*)(sb + r * 128 + (((c0 + 1) ^ sw) << 4));
-      fb[j] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-    }
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma_e4m3(fa[i], fb[j], acc[i][j]);
-  }
-  if (vec)
-    f8_epilogue_vec<TO, BM, MI>(acc, (float*)smem, m0, n0, wm, wn, lane, a_scale, w_scale, C, ldc, M, N, bias, R,
-                                ldr, act);
-  else
-    f8_epilogue<TO, MI>(acc, m0, n0, wm, wn, lane, a_scale, w_scale, C, ldc, M, N, bias, R, ldr, act);
-}
-
 // One workgroup per row: amax over the row, q = RNE_e4m3(x * 448 / amax), scale = amax / 448.
 template <typename T>
 __global__ __launch_bounds__(256) void quant_rows_e4m3_kernel(const T* __restrict__ x, long long ldx,
@@ -526,12 +364,10 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
   const int tn = (N + F8_BN - 1) / F8_BN, t128 = ((M + 127) / 128) * tn;
   const bool small = t128 < 256;
   const int tiles = small ? ((M + 63) / 64) * tn : t128;
-  // K % 128 == 0: LDS-DMA ring kernel -- 64-row tiles with 3 stages (72 KB: two workgroups per CU), 128-row
-  // tiles with 2 stages (64 KB; a 3-stage 96-KB ring leaves one workgroup per CU: 8192x640x640 23 -> 38 us).
-  // Ragged K, or FD_F8_KERNEL=reg (A/B timing): the register-staged kernel.
-  const int kf = fd_knob(FDK_F8_KERNEL);  // tests compare the kernels in one process
-  // K % 128 == 0: the eight-wave kernel family (gemm8.hip, 256-row tiles) unless knob FD_F8_KERNEL selects one of these
-  if (kf == 0) {
+  // K % 128 == 0: the eight-wave kernel family (gemm8.hip, every tile shape); ragged K (K % 128 != 0, e.g. the 128^2
+  // level's K = 320 projections) or a shape it declines: the register-staged 4-wave kernel below.  (Round 6: the
+  // 4-wave LDS-DMA ring kernel, selectable only by a knob since round 3, was removed.)
+  {
     fd_gemm_params p{};
     p.A = A;
     p.B = W;
@@ -554,22 +390,10 @@ extern "C" int fd_gemm_e4m3(const void* A, long long lda, const float* a_scale, 
     if (r8 < 0) return r8;
     if (r8 == 1) return FD_OK;
   }
-  const bool dma = (K % F8_BK) == 0 && kf != 2;
-  // 16-B vector epilogue when every output row / residual row starts 16-B aligned (FD_F8_KERNEL=scalar: off)
-  const int vec = (nout % 8) == 0 && (ldc % 8) == 0 && (((unsigned long long)C) & 15) == 0 &&
-                  (!residual || ((ldr % 8) == 0 && (((unsigned long long)residual) & 15) == 0)) &&
-                  kf != 3;
   FD_DISPATCH_O(out_dtype, {
-    if (dma) {
-      auto kern = small ? gemm_e4m3_dma_kernel<TO, 64, 3> : gemm_e4m3_dma_kernel<TO, 128, 2>;
-      hipLaunchKernelGGL(kern, dim3(tiles), dim3(F8_NT), 0, (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
-                         (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr, act,
-                         vec);
-    } else {
-      auto kern = small ? gemm_e4m3_kernel<TO, 64> : gemm_e4m3_kernel<TO, 128>;
-      hipLaunchKernelGGL(kern, dim3(tiles), dim3(F8_NT), 0, (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
-                         (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr, act);
-    }
+    auto kern = small ? gemm_e4m3_kernel<TO, 64> : gemm_e4m3_kernel<TO, 128>;
+    hipLaunchKernelGGL(kern, dim3(tiles), dim3(F8_NT), 0, (hipStream_t)stream, (const uint8_t*)A, lda, a_scale,
+                       (const uint8_t*)W, ldw, w_scale, (TO*)C, ldc, M, N, K, bias, (const TO*)residual, ldr, act);
   });
   FD_LAUNCH_CHECK();
   return FD_OK;

@@ -17,20 +17,11 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_GEMM8", 1},          // eight-wave 256-row kernels on (0: everything on the 4-wave kernel)
     {"FD_GEMM8_S", 0},        // force the split count (0: planner)
     {"FD_GEMM8_GM", 0},       // force the tile-walk group height (0: planner)
-    {"FD_GEMM_R4", 0},        // 64 x 160 one-wave-per-SIMD instance (measured slower in the step)
-    {"FD_GEMM_P128", 0},      // pairwise 128-row split for M = 2048 (measured slower)
-    {"FD_GEMM_R4_NS", 3},     // ring depth of that instance
-    {"FD_GEMM_B4", 0},        // 4-deep ring for the 256-row kernels (measured slower)
     {"FD_GEMM8_W160", 3},     // bit 0: 256 x 160 tiles where faster; bit 1: take N = 320 from the 4-wave kernel
-    {"FD_GEMM8_N128", 0},     // 128-channel convs at >= 512^2 on the 4-wave 128 x 128 tiles (decode 0.1 ms slower)
-    {"FD_GEMM8_LNP", 1},      // LN-fold producers with K >= 4096 on the 128 x 160 pairwise split
-    {"FD_GEMM8_LNP_S", 4},    // split count of the 256 x 160 producer form (LNP = 2)
+    {"FD_GEMM8_LNP", 1},      // LN-fold producers with K >= 4096 on the eight-wave 128 x 160 pairwise split
     {"FD_GEMM8_MIDK", 3},     // K splits for the mid-K launches of the 32^2 level (0: off)
     {"FD_F8_TILE", 0},        // force the e4m3 eight-wave tile (256160 / 256128 / 128160 / 64160; 0: planner)
-    {"FD_F8_KERNEL", 0},      // e4m3 kernel: 0 eight-wave family, 1 4-wave LDS-DMA, 2 register-staged, 3 scalar epilogue
     {"FD_GEMM_CFG", -1},      // 4-wave kernel: force the tile config (-1: planner)
-    {"FD_GEMM_NS", 0},        // 4-wave kernel: force the ring depth (0: per config)
-    {"FD_GEMM_KS", 0},        // 4-wave kernel: force the K split across wave groups (0: per config)
     {"FD_GEMM_SWZ", 1},       // 4-wave kernel: XCD-aware tile order
     {"FD_GEMM_MODE", 0},      // 4-wave kernel diagnostic build mode (1 loads only, 2 MFMA only; probes only)
     {"FD_GEMV", 1},           // few-row GEMV for M <= 4
@@ -46,18 +37,13 @@ const KnobDef kDefs[FDK_COUNT] = {
     {"FD_CONV_HALO", 1},           // 3x3 stride-1 convs on the halo-staged kernel where eligible (1: not the gemm256 ones; 2: all)
     {"FD_CONV_HALO_MIN_TILES", 192},  // ... when it has at least this many tiles (per TLC tile's rows, m_ref)
     {"FD_CONV_HALO_SPLIT", 1},     // ... or twice that many with the input channels split in two (pairwise combine)
-    {"FD_CONV_HALO_NS8", 3},       // weight-ring depth of its 128-row tiles (3 or 5: no faster, profiles/r04d_*)
     {"FD_GEMM_GMP", 1},            // 4-wave kernel: tile-row group height planned per launch (0: fixed 4)
-    {"FD_GEMM8_W128", 1},          // gemm8 128 x 160 tiles on eight waves of 32 x 80 (0: four of 64 x 80)
-    {"FD_GEMM8_LNP_K", 4096},      // least K of the LN-fold producers taken by the 128 x 160 pairwise split
-    {"FD_XATTN_SPLIT", 0},         // cross-attention score GEMM: 128 x 160 tiles with K split in two
     {"FD_CONV_HALO_PT", 3},        // halo conv persistent over tiles (next tile's chunk 0 DMA'd in the K loop) for launches
                                    // of >= 2 tiles per CU: 3 GroupNorm-folded convs without residual, 1 all, 2 also the
                                    // gemm256-eligible ones, 0 off
     {"FD_CONV_HALO_NS16", 3},      // weight-ring depth of its 256 x 128 tiles (3 or 4)
     {"FD_CONV_HALO_SPLIT16", 1},   // 256-row tiles with a pairwise input-channel split before 128-row tiles
-    {"FD_GEMM8_LNP_BIG", 0},       // LN-fold producers of >= 256 256-row tiles per TLC tile (the information transformer
-                                   // at 128^2: out_proj / c_proj, M = 32768) on gemm8 256 x 160 instead of 4-wave 64 x 160
+    {"FD_CONV_HALO_PP", 1},        // halo conv per-tile forms on the two-group ping-pong K loop (0: one-barrier loop)
 };
 int g_knobs[FDK_COUNT];
 bool g_init = false;
@@ -105,4 +91,23 @@ extern "C" const char* fd_knob_name(int id) { return (id >= 0 && id < FDK_COUNT)
 extern "C" void fd_reset_knobs(void) {
   g_init = false;
   init_knobs();
+}
+
+// Split-K hand-off health (include/faithdiff_hip.h): the pairwise split-K waits (gemm8, halo conv) that timed out
+// since the last reset.  Synchronous (reads device symbols); the host calls it at its own sync points.
+extern "C" int fd_splitk_health(unsigned* timeouts, int reset) {
+  if (!timeouts) return FD_ERR_ARG;
+  *timeouts = 0;
+  int rc = g8_splitk_health(timeouts, reset, -1);
+  if (rc == FD_OK) rc = halo_splitk_health(timeouts, reset, -1);
+  return rc;
+}
+
+// Test hook only: drop = 1 makes every pairwise split-K publisher skip its flag, so the waiting split times out
+// (~1 s per tile wave), poisons its tile with NaN and counts the timeout; 0 restores the product behaviour.
+extern "C" int fd_splitk_test_drop(int drop) {
+  if (drop < 0) return FD_ERR_ARG;
+  int rc = g8_splitk_health(nullptr, 0, drop);
+  if (rc == FD_OK) rc = halo_splitk_health(nullptr, 0, drop);
+  return rc;
 }

@@ -17,9 +17,7 @@ HOST_DEFAULTS = {
     "FD_LN_FOLD": 1,        # LayerNorms folded into the transformer GEMM pairs (0: separate LayerNorm launches)
     "FD_ITL_FOLD": 1,       # ... and into the information transformer's in_proj / c_fc (with FD_LN_FOLD)
     "FD_UNET_GN_EPI": 1,    # UNet GroupNorm statistics from the producing GEMM / conv epilogue
-    "FD_SIDE_STREAM": 0,    # time / add embeddings on a second stream inside the UNet graph (measured slower)
     "FD_FP8_MFMA": 0,       # use_fp8 model on the e4m3 MFMA (quantize_8bit(fp8_mfma=...) / FaithDiff_pipeline arg)
-    "FD_FP8_MX": 0,         # fp8 model: MX e4m3 activations everywhere
     "FD_FP8_MX_ATTN": 1,    # fp8 model: MX e4m3 attention outputs only (the measured-fastest form)
     "FD_FP8_MX_GEGLU": 0,   # fp8 model: MX output straight from the GEGLU epilogue
     "FD_VAE_NARROW": 1,     # VAE conv_norm_out + SiLU + conv_out in the narrow strip kernel (fd_conv3x3_narrow_gn)
@@ -32,8 +30,6 @@ HOST_DEFAULTS = {
     "FD_D512_SPLIT": 1,     # VAE d=512 attention on 8 waves (128 queries per K/V fetch) with the keys split + merged
 }
 _host = dict(HOST_DEFAULTS)
-# string spellings some scripts use for the e4m3 kernel choice
-_F8_KERNEL = {"dma": 1, "reg": 2, "scalar": 3}
 
 
 def _lib_names():
@@ -90,7 +86,7 @@ class override:
 
     def __enter__(self):
         for k, v in self.kw.items():
-            self.old[k] = set(k, _F8_KERNEL.get(v, v) if isinstance(v, str) else v)
+            self.old[k] = set(k, v)
         return self
 
     def __exit__(self, *exc):
@@ -105,6 +101,6 @@ def apply_env(environ=None):
     for n in names():
         if n in environ:
             v = environ[n]
-            done[n] = _F8_KERNEL[v] if v in _F8_KERNEL else int(v)
+            done[n] = int(v)
             set(n, done[n])
     return done

@@ -108,6 +108,8 @@ _SIGS = {
     "fd_get_knob": (c_int, [c_char_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "fd_knob_name": (c_char_p, [c_int]),
     "fd_reset_knobs": (None, []),
+    "fd_splitk_health": (c_int, [ctypes.POINTER(ctypes.c_uint), c_int]),
+    "fd_splitk_test_drop": (c_int, [c_int]),
     "fd_device_check": (c_int, []),
     "fd_version": (c_char_p, []),
 }

@@ -4,6 +4,7 @@ Layout conventions: activations NHWC, flattened to [M, C] with M = n*H*W; Linear
 3x3 conv weights pre-packed [Cout, 9*Cin] (tap-major, see pack_conv3x3).
 """
 import ctypes
+import weakref
 
 import torch
 
@@ -43,6 +44,7 @@ def reserve_gn_workspace(nbytes, device):
 
 # --------------------------------------------------------------------------------------- GEMM workspace
 _GEMM_WS = {}
+_ALL_GEMM_WS = weakref.WeakSet()  # every split-K workspace still alive (the current ones and those graphs hold)
 _TILE_GROUPS = [1]
 
 
@@ -73,7 +75,29 @@ def reserve_gemm_workspace(nbytes, device):
             torch.cuda.synchronize(key)
             grow = 2 * ws.numel()
         _GEMM_WS[key] = torch.zeros(max(nbytes, grow, 1 << 20), dtype=torch.uint8, device=key)
+        _ALL_GEMM_WS.add(_GEMM_WS[key])
     return _GEMM_WS[key]
+
+
+_SK_HEAD = 65536 * 4  # tile counters + flags at the head of a split-K workspace
+
+
+def split_k_health(raise_on_timeout=True):
+    """Check the pairwise split-K hand-offs (fd_splitk_health; a host sync).  A timed-out wait poisoned its tile with
+    NaN and left that tile's counter / flag slot stale, so on any timeout every live split-K workspace's counter
+    head is re-zeroed (later launches start clean) and, by default, RuntimeError is raised: the outputs computed
+    since the last check are not to be trusted.  Returns the timeout count."""
+    n = ctypes.c_uint(0)
+    L.check(L.load().fd_splitk_health(ctypes.byref(n), 1), "fd_splitk_health")
+    if n.value:
+        torch.cuda.synchronize()
+        for ws in list(_ALL_GEMM_WS):
+            ws[:_SK_HEAD].zero_()
+        torch.cuda.synchronize()
+        if raise_on_timeout:
+            raise RuntimeError(f"{n.value} split-K hand-off wait(s) timed out: the affected tiles were poisoned with "
+                               "NaN; the split-K counters have been reset")
+    return n.value
 
 
 def _attach_ws(p, device):
@@ -226,10 +250,14 @@ class GnStats:
         self.done = self.rows > 0
 
 
-def _rows(t, ld):
-    """Rows of ``ld`` elements readable from t.data_ptr() within t's own extent (fd_gemm_params.*_rows)."""
+def _rows(t, ld, ncols):
+    """Rows r of ``ld`` elements whose first ``ncols`` elements (the launch's columns) all lie inside t's own extent:
+    r * ld + ncols - 1 <= span - 1 (fd_gemm_params.*_rows).  A view whose last row is shorter than the launch's
+    columns does not count that row (the first-element count let such a row pass the extent check)."""
     span = 1 + sum((n - 1) * st for n, st in zip(t.shape, t.stride()) if n > 0)
-    return 0 if t.numel() == 0 or ld <= 0 else (span - 1) // ld + 1
+    if t.numel() == 0 or ld <= 0 or ncols <= 0 or span < ncols:
+        return 0
+    return (span - ncols) // ld + 1
 
 
 def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=1, alpha=1.0, act="none",
@@ -266,10 +294,10 @@ def gemm(a, w, out=None, bias=None, residual=None, rowbias=None, rows_per_group=
         p.residual = residual.data_ptr()
         p.ldr = residual.stride(-2) if ldr is None else ldr
         p.strideR = stride_r
-        p.residual_rows = _rows(residual, p.ldr)
+        p.residual_rows = _rows(residual, p.ldr, N // 2 if act == "geglu" else N)
     if rowbias is not None:
         p.rowbias, p.rowbias_ld = rowbias.data_ptr(), rowbias.stride(0)
-        p.rowbias_rows = _rows(rowbias, p.rowbias_ld)
+        p.rowbias_rows = _rows(rowbias, p.rowbias_ld, N // 2 if act == "geglu" else N)
     p.rows_per_group = rows_per_group
     p.alpha = alpha
     p.act = L.ACT[act]
@@ -536,10 +564,10 @@ def _conv_params(x, wp, bias, nimg, H, W, stride, pad, upsample, x2, C1, out, ro
     p.bias = bias.data_ptr() if bias is not None else None
     if residual is not None:
         p.residual, p.ldr = residual.data_ptr(), residual.stride(-2)
-        p.residual_rows = _rows(residual, p.ldr)
+        p.residual_rows = _rows(residual, p.ldr, Cout)
     if rowbias is not None:
         p.rowbias, p.rowbias_ld, p.rows_per_group = rowbias.data_ptr(), rowbias.stride(0), Hout * Wout
-        p.rowbias_rows = _rows(rowbias, p.rowbias_ld)
+        p.rowbias_rows = _rows(rowbias, p.rowbias_ld, Cout)
     else:
         p.rows_per_group = 1
     p.alpha, p.act = alpha, L.ACT[act]

@@ -42,12 +42,9 @@ class HipUNet:
         separate LayerNorm path is used (the fold needs W * gamma, which is not an e4m3 weight)."""
         L.require_device()
         self.fp8_mfma = bool(fp8_mfma)
-        # fp8 activations as OCP MX e4m3 (32-element blocks, E8M0 scales) written by their producers -- flash
-        # attention, LayerNorm -- instead of per-row scales from separate quantization launches.  Opt-in
-        # (FD_FP8_MX=1): on one box the C2 step measured 21.00 ms MX vs 20.88 ms per-row (profiles/r03_fp8_ab_*.json):
-        # the 140 quantization launches it removes are paid back by the MX GEMMs' per-K-step scale traffic
-        # (ff out 23.2 -> 25.0 us, profiles/r03_f8_tiles_mx.jsonl) and the MX epilogues
-        self.fp8_mx = self.fp8_mfma and knobs.get("FD_FP8_MX") == 1
+        # (MX e4m3 activations everywhere -- LayerNorm / flash attention writing OCP MX, FD_FP8_MX -- measured slower
+        # than per-row scales (C2 21.00 vs 20.88 ms, C4 69.5 vs 71.3 tile-steps/s: profiles/r03_fp8_ab_*.json,
+        # r05af_c4_mx_ab.txt) and was removed in round 6; MX stays where it is free, below)
         # MX output straight from the GEGLU epilogue (forces 256 x 128 tiles; profiles/r03_f8_tiles_mx.jsonl: 48.1 vs
         # 39.7 + a 2048 x 5120 quantization for the 256 x 160 bf16 form); FD_FP8_MX_GEGLU=1 turns it on (A/B)
         self.fp8_mx_geglu = knobs.get("FD_FP8_MX_GEGLU") == 1
@@ -55,7 +52,7 @@ class HipUNet:
         # (K = C: the MX GEMM's speed, profiles/r03_f8_tiles_mx.jsonl) read it, removing the two activation
         # quantization launches per block.  C2 step on one box, alternated: 20.57 / 20.57 ms vs 20.65 / 20.67 per-row
         # everywhere vs 20.84 / 20.89 MX everywhere (profiles/r03_fp8_mxattn_ab_*.json).  FD_FP8_MX_ATTN=0: per-row
-        self.fp8_mx_attn = self.fp8_mfma and not self.fp8_mx and knobs.get("FD_FP8_MX_ATTN") != 0
+        self.fp8_mx_attn = self.fp8_mfma and knobs.get("FD_FP8_MX_ATTN") != 0
         self.device, self.dtype = torch.device(device), dtype
         f32 = torch.float32
         W = lambda k: _dev(sd[k], self.device, dtype)  # noqa: E731
@@ -307,8 +304,6 @@ class HipUNet:
         h = ops.group_norm(x, *t["norm"], B, HW, C, 32, 1e-6, silu=False, stats=self._gn_stats_of(x))
         if self.ln_fold:
             return self._t2d_folded(t, x, h, B, H, Wd)
-        if self.fp8_mx:
-            return self._t2d_mx(t, x, h, B, H, Wd)
         lin = self._lin
         h = lin(h, t["pin"][0], bias=t["pin"][1])
         qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
@@ -353,40 +348,8 @@ class HipUNet:
             lin(ff, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
         return self._proj_out(t, h, x, B, HW)
 
-    def _t2d_mx(self, t, x, hn, B, H, Wd):
-        """_t2d of the fp8 model with MX e4m3 activations: every transformer Linear is fd_gemm_mxe4m3, its A operand
-        written as MX by the producer -- LayerNorm (norm1/2/3), flash attention (out-projections), the GEGLU epilogue
-        (ff out); only proj_in / proj_out inputs (GroupNorm output, residual stream) take a quantization launch."""
-        C, heads, HW = t["c"], t["heads"], H * Wd
-        M = B * HW
-        h = ops.gemm_mx(ops.quant_rows_mx(hn), t["pin"][0], bias=t["pin"][1], out_dtype=self.dtype)
-        qkv = torch.empty((M, 3 * C), dtype=self.dtype, device=self.device)
-        n8, att8, ff8 = ops.MX(M, C, self.device), ops.MX(M, C, self.device), ops.MX(M, 4 * C, self.device)
-        for b in t["blocks"]:
-            ops.gemm_mx(ops.layer_norm_mx(h, *b["n1"], 1e-5, out=n8), b["qkv"], out=qkv)
-            ops.flash_attn_mx(qkv, qkv[:, C:], qkv[:, 2 * C:], att8, B, heads, HW, HW, 3 * C, 3 * C, 3 * C,
-                              HW * 3 * C, HW * 3 * C, HW * 3 * C, kv_mod=0, scale=0.125)
-            ops.gemm_mx(att8, b["o1"][0], bias=b["o1"][1], residual=h, out=h)
-            ops.gemm_mx(ops.layer_norm_mx(h, *b["n2"], 1e-5, out=n8), b["q2"], out=qkv[:, :C])
-            kv = self._kv[self._kv_row0:, b["kv_off"]:]
-            Lk, ldkv = self.Lk, self.kv_total
-            ops.flash_attn_mx(qkv, kv, kv[:, C:], att8, B, heads, HW, Lk, 3 * C, ldkv, ldkv,
-                              HW * 3 * C, Lk * ldkv, Lk * ldkv, kv_mod=self._kv_mod, scale=0.125)
-            ops.gemm_mx(att8, b["o2"][0], bias=b["o2"][1], residual=h, out=h)
-            if self.fp8_mx_geglu:  # GEGLU epilogue writes MX (256 x 128 tiles: 32-column output blocks)
-                ops.gemm_mx(ops.layer_norm_mx(h, *b["n3"], 1e-5, out=n8), b["ff1"][0], bias=b["ff1"][1],
-                            act="geglu", out=ff8)
-            else:  # GEGLU on its faster 256 x 160 tiles in bf16, then one MX quantization launch
-                ff = ops.gemm_mx(ops.layer_norm_mx(h, *b["n3"], 1e-5, out=n8), b["ff1"][0], bias=b["ff1"][1],
-                                 act="geglu", out_dtype=self.dtype)
-                ops.quant_rows_mx(ff, out=ff8)
-            ops.gemm_mx(ff8, b["ff2"][0], bias=b["ff2"][1], residual=h, out=h)
-        return self._proj_out(t, h, x, B, HW)
-
     def _proj_out(self, t, h, x, B, HW):
         """proj_out + residual; its epilogue also writes the next GroupNorm's statistics (16-bit GEMM)."""
-        if self.fp8_mx:
-            return ops.gemm_mx(ops.quant_rows_mx(h), t["pout"][0], bias=t["pout"][1], residual=x)
         if self.fp8_mfma:
             return ops.linear_e4m3(h, t["pout"][0], bias=t["pout"][1], residual=x)
         s = self._gn_new(B, HW)
@@ -508,13 +471,6 @@ class HipUNet:
         ops.unary(emb, semb, "silu")
         return ops.gemm(semb, self.temb_w, bias=self.temb_b, out_dtype=torch.float32)  # [B, sum C_out]
 
-    def _side_stream(self):
-        if knobs.get("FD_SIDE_STREAM") == 0:
-            return None
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.device)
-        return self._side
-
     def run(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample=True, cond_embedded=False, kv_pair0=0):
         """forward() through the graph cache (fdhip/graphs.py): eager on the first call of a shape, captured on
         the second, one hipGraph replay after that.  The result is the graph's static output buffer (valid
@@ -554,20 +510,10 @@ class HipUNet:
             return self._forward(x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample, cond_embedded)
 
     def _forward(self, x, t, time_ids, text_embeds, cond, B, H, Wd, add_sample, cond_embedded=False):
-        # The time / add embeddings (six M = 2 launches) depend on nothing the input path computes: they can run
-        # on a second stream beside conv_in and the FaithDiff extras (a fork / join inside the captured graph;
-        # no split-K, so the streams never share the GEMM workspace).  Opt-in (FD_SIDE_STREAM=1): measured
-        # 0.39 ms/step SLOWER at C2 when it also carried the prompt K/V GEMM (now in set_context).
+        # (the time / add embeddings on a second stream inside the graph measured 0.39 ms/step slower at C2 and
+        # were removed in round 6: FD_SIDE_STREAM, git history)
         self._gn_src = None
-        cur = torch.cuda.current_stream(self.device)
-        side = self._side_stream()
-        if side is not None:
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                temb = self.embeddings(t, time_ids, text_embeds, B)
-            temb.record_stream(cur)
-        else:
-            temb = self.embeddings(t, time_ids, text_embeds, B)
+        temb = self.embeddings(t, time_ids, text_embeds, B)
         x0 = ops.conv_direct(x, *self.conv_in, B, H, Wd, 4, 3, 1, 1, out_dtype=self.dtype)
         if cond is not None and self.has_extras:
             feat = self._extras(x0, cond, B, H, Wd, embedded=cond_embedded)
@@ -575,8 +521,6 @@ class HipUNet:
                 x0 = ops.gemm(feat, self.scp[0], bias=self.scp[1], residual=x0)
             else:
                 x0 = ops.gemm(feat, self.scp[0], bias=self.scp[1])
-        if side is not None:
-            cur.wait_stream(side)
         skips = [(x0, 320, H, Wd)]
         h, hh, ww = x0, H, Wd
         for i, blk in enumerate(self.down):

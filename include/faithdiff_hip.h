@@ -363,7 +363,7 @@ int fd_time_features(const float* t, const float* time_ids, const float* text_em
 int fd_tlc_scale_input(const float* canvas, const int* row_org, int nr, const int* col_org, int nc, int H, int W,
                        int kh, int kw, int tile_begin, int ntiles, int cfg, float sigma, void* out, int dtype,
                        void* stream);
-/* The same, also writing the step's UNet timestep into t_out[0 .. t_n) (t_n <= 256; the `t` row of the UNet call,
+/* The same, also writing the step's UNet timestep into t_out[0 .. t_n) (any t_n >= 0; the `t` row of the UNet call,
  * :1350-1360) from inside the same launch: the denoise loop's per-step host-side fill of the timestep buffer (a
  * separate elementwise launch) is gone. */
 int fd_tlc_scale_input_t(const float* canvas, const int* row_org, int nr, const int* col_org, int nc, int H, int W,
@@ -412,6 +412,15 @@ int fd_set_knob(const char* name, int value, int* previous);
 int fd_get_knob(const char* name, int* value, int* dflt);
 const char* fd_knob_name(int id); /* NULL past the last knob */
 void fd_reset_knobs(void);
+
+/* Split-K hand-off health.  The pairwise split-K forms (gemm8 S = 2, the halo conv's channel split) hand a partial tile
+ * from one workgroup to its partner through a flag with a bounded wait; a wait that times out (should never happen:
+ * the publisher is already running) poisons its tile with NaN and is counted here.  After a timeout that tile's
+ * counter / flag slot is stale, so the host must re-zero the first 256 KiB of every split-K workspace
+ * (fdhip/ops.py split_k_health does, and raises).  Synchronous; *timeouts = count since the last reset.
+ * fd_splitk_test_drop(1) is a test hook only: every publisher skips its flag (forces the timeout path). */
+int fd_splitk_health(unsigned* timeouts, int reset);
+int fd_splitk_test_drop(int drop);
 
 /* library / device checks */
 int fd_device_check(void);

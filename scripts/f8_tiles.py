@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""e4m3 GEMM kernel A/B on the use_fp8 UNet's Linear shapes: the 4-wave kernels (FD_F8_KERNEL=dma), the eight-wave
+"""e4m3 GEMM kernel A/B on the use_fp8 UNet's Linear shapes: the eight-wave
 family with its own tile choice, each forced tile shape (FD_F8_TILE), the bf16 fd_gemm of the same shape, and the MX
 (block-scaled A) form, GEGLU also with the MX output (PROBE_MX_TILES=1: every MX tile shape).
 REP launches per variant are captured into one hipGraph and replayed between HIP events (no Python enqueue in
@@ -68,25 +68,24 @@ for arg in SHAPES:
     bf = lambda: ops.gemm(a, wb, out=out, act=act)  # noqa: E731
     flop = 2.0 * M * N * K
     rec = {"shape": arg}
-    rec["f8_4wave_us"] = with_env({"FD_F8_KERNEL": "dma", "FD_F8_TILE": None}, f8)
-    rec["f8_8wave_us"] = with_env({"FD_F8_KERNEL": None, "FD_F8_TILE": None}, f8)
+    rec["f8_8wave_us"] = with_env({"FD_F8_TILE": None}, f8)
     for t in ("256160", "256128", "128160", "64160"):
         if act == "geglu" and t in ("128160", "64160"):
             continue
-        rec[f"f8_tile{t}_us"] = with_env({"FD_F8_KERNEL": None, "FD_F8_TILE": t}, f8)
+        rec[f"f8_tile{t}_us"] = with_env({"FD_F8_TILE": t}, f8)
     rec["bf16_us"] = graph_us(bf)
     amx = ops.quant_rows_mx(a)
-    rec["mx_us"] = with_env({"FD_F8_KERNEL": None, "FD_F8_TILE": None},
+    rec["mx_us"] = with_env({"FD_F8_TILE": None},
                             lambda: ops.gemm_mx(amx, w8, out=out, act=act))
     if act == "geglu":
         omx = ops.MX(M, N // 2, dev)
-        rec["mx_out_us"] = with_env({"FD_F8_KERNEL": None, "FD_F8_TILE": None},
+        rec["mx_out_us"] = with_env({"FD_F8_TILE": None},
                                     lambda: ops.gemm_mx(amx, w8, out=omx, act=act))
     if os.environ.get("PROBE_MX_TILES"):
         for t in ("256160", "256128", "128160", "64160"):
             if act == "geglu" and t in ("128160", "64160"):
                 continue
-            rec[f"mx_tile{t}_us"] = with_env({"FD_F8_KERNEL": None, "FD_F8_TILE": t},
+            rec[f"mx_tile{t}_us"] = with_env({"FD_F8_TILE": t},
                                              lambda: ops.gemm_mx(amx, w8, out=out, act=act))
     rec = {k: (round(v, 2) if isinstance(v, float) else v) for k, v in rec.items()}
     rec["f8_8wave_tflops"] = round(flop / rec["f8_8wave_us"] / 1e6, 1)

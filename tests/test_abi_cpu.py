@@ -65,8 +65,8 @@ def test_knob_table_defaults_and_no_environment_reads():
     from fdhip import knobs
     from fdhip import lib
     assert knobs.changed() == {}
-    with knobs.override(FD_GEMM256=0, FD_F8_KERNEL="dma", FD_LN_FOLD=0):
-        assert knobs.changed() == {"FD_GEMM256": 0, "FD_F8_KERNEL": 1, "FD_LN_FOLD": 0}
+    with knobs.override(FD_GEMM256=0, FD_F8_TILE=256128, FD_LN_FOLD=0):
+        assert knobs.changed() == {"FD_GEMM256": 0, "FD_F8_TILE": 256128, "FD_LN_FOLD": 0}
     assert knobs.changed() == {}
     assert lib.load().fd_set_knob(b"FD_NO_SUCH_KNOB", 1, None) != 0
     assert knobs.apply_env({"FD_GEMM8_MIDK": "2", "UNRELATED": "1"}) == {"FD_GEMM8_MIDK": 2}
@@ -129,7 +129,14 @@ def test_rows_helper_counts_reachable_rows():
     import torch
     from fdhip import ops
     t = torch.empty(7, 320)
-    assert ops._rows(t, 320) == 7
-    assert ops._rows(torch.empty(5, 1280)[:, 640:960], 1280) == 5  # a column slice of the time-embedding table
-    assert ops._rows(torch.empty(3, 4, 160), 160) == 12
-    assert ops._rows(torch.empty(0, 8), 8) == 0
+    assert ops._rows(t, 320, 320) == 7
+    assert ops._rows(torch.empty(5, 1280)[:, 640:960], 1280, 320) == 5  # a column slice of the time-embedding table
+    assert ops._rows(torch.empty(3, 4, 160), 160, 160) == 12
+    assert ops._rows(torch.empty(0, 8), 8, 8) == 0
+    # a flat view whose last row is shorter than the launch's columns -- that row is not readable
+    flat = torch.empty(1000)
+    assert ops._rows(flat, 320, 320) == 3  # rows 0..2 whole (960 elements); row 3 has only 40 of 320
+    assert ops._rows(flat[:960], 320, 320) == 3
+    assert ops._rows(flat[:959], 320, 320) == 2
+    assert ops._rows(torch.empty(5, 1280)[:, 640:960], 1280, 640) == 4  # wider than the slice: last row overruns
+    assert ops._rows(flat[:100], 320, 320) == 0

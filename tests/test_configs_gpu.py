@@ -194,3 +194,83 @@ def test_band_x4_wo_llava_tile_batch_bitwise():
     assert fixed.size == c["image"].size == (4316, 3112)
     parity.record("band_x4_image_std", float(a25.std()), bar=">1")
     assert a25.std() > 1.0
+
+
+def test_balanced_vs_unbalanced_tile_batches_bitwise():
+    """30 TLC tiles at tile_batch 25 run as 25 + 5 (tile_balance 0) or 15 + 15 (tile_balance 1, the
+    default) UNet forwards -- the hoisted condition embedding now rides in the same batches as the loop's forwards --
+    and both give bitwise the same latents and pixels.  1536 x 1792 image, target 512 (64-latent tiles, 5 x 6 grid),
+    one Euler step of the 20-step schedule."""
+    from FaithDiff.pipelines.tlc import TileGrid, tile_batches
+    H, W = 1536, 1792
+    assert TileGrid(H // 8, W // 8, (64, 64), 0.5).ntiles == 30
+    assert tile_batches(30, 25, False) == [(0, 25), (25, 5)] and tile_batches(30, 25, True) == [(0, 15), (15, 15)]
+    pipe = _build(seed=6)
+    img = synthetic_degraded(H, W, 13)
+    noise, post = det_tensor((1, 4, H // 8, W // 8), 53), det_tensor((1, 4, H // 8, W // 8), 54)
+    res = []
+    saved = (pipe.tile_batch, pipe.tile_balance)
+    try:
+        for bal in (0, 1):
+            pipe.tile_batch, pipe.tile_balance = 25, bal
+            cap = {}
+
+            def cb(p, i, t, k):
+                cap["lat"] = k["latents"].detach().float().cpu().clone()
+                return {}
+            out = pipe(lr_img=img, prompt="a restored photo of a tiled wall", negative_prompt="", guidance_scale=5.0,
+                       start_point="lr", height=H, width=W, overlap=0.5, target_size=(512, 512), latents=noise,
+                       posterior_noise=post, num_inference_steps=20, denoising_end=0.05, callback_on_step_end=cb,
+                       output_type="np").images
+            res.append((cap["lat"], np.asarray(out)))
+    finally:
+        pipe.tile_batch, pipe.tile_balance = saved
+    assert torch.isfinite(res[0][0]).all()
+    assert torch.equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])
+
+
+@pytest.mark.timeout(900)
+def test_c4_literal_8k_input_x4_1947_tiles():
+    """BASELINE configs[3] in its literal reading (test_wo_llava.py:18,78-86): a 7680 x 4320
+    input upscaled x4 (LANCZOS) to 30720 x 17280, restored with the use_fp8 UNet on the e4m3 MFMA, the tiled VAE
+    encode / decode and the tiled denoise encoder -- a 3840 x 2160 latent in 1947 TLC tiles -- for one Euler step of
+    the 20-step schedule (denoising_end).  The full 20-step run is scripts/c4_literal.py (profiles/r05ai_*, 567 s).
+    Size-independent checks: the tile count, every final latent finite, the output size, a non-flat image, and the
+    peak HBM of the call below 150 GB (the 288 GB budget of one MI355X, with room for a second image)."""
+    from FaithDiff.pipelines.tlc import TileGrid
+    w0, h0 = 7680, 4320
+    W, H = 4 * w0, 4 * h0
+    assert TileGrid(H // 8, W // 8, (128, 128), 0.5).ntiles == 1947
+    pipe = _build(seed=7, use_fp8=True, fp8_mfma=True)
+    assert pipe.unet.hip().fp8_mfma
+    pipe.enable_vae_tiling()
+    rng = np.random.default_rng(17)  # a smooth seeded test card (content does not change the work)
+    yy, xx = np.mgrid[0:h0, 0:w0].astype(np.float32)
+    card = np.stack([np.sin(xx / w0 * (3 + c) * 6.28) * np.cos(yy / h0 * (2 + c) * 6.28) for c in range(3)], -1)
+    card = card + rng.normal(0, 0.1, card.shape).astype(np.float32)
+    card = ((card - card.min()) / (card.max() - card.min()) * 255).astype(np.uint8)
+    img = Image.fromarray(card).resize((W, H), Image.LANCZOS)
+    del card, yy, xx
+    cap = {}
+
+    def cb(p, i, t, k):
+        cap["finite"] = bool(torch.isfinite(k["latents"]).all())
+        cap["shape"] = tuple(k["latents"].shape)
+        cap["steps"] = i + 1
+        return {}
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    out = pipe(lr_img=img, prompt="A high quality photo restored from a degraded capture.", negative_prompt="",
+               num_inference_steps=20, denoising_end=0.05, guidance_scale=5.0, start_point="lr", height=H, width=W,
+               overlap=0.5, target_size=(1024, 1024), callback_on_step_end=cb).images[0]
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated()
+    assert cap["steps"] == 1 and cap["shape"] == (1, 4, H // 8, W // 8) and cap["finite"]
+    assert out.size == (W, H)
+    arr = np.asarray(out)
+    std = float(arr[::8, ::8].std())
+    parity.record("c4_literal_image_std", std, bar=">1")
+    parity.record("c4_literal_peak_hbm_gb", peak / 1e9, bar="<150")
+    assert std > 1.0
+    assert peak < 150e9, peak

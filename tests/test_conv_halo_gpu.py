@@ -377,3 +377,57 @@ def test_short_rowbias_or_residual_is_refused_on_the_device_path():
         g = ops.gemm(a, wt, residual=torch.zeros(64, 160, device=DEV, dtype=torch.bfloat16))
     torch.cuda.synchronize()
     assert torch.isfinite(y.float()).all() and g.shape == (64, 160)
+
+
+@pytest.mark.parametrize("case", ["th16_n160", "gn_res_rowbias_stats", "th8", "split_k", "phase_f16", "phase_bf16",
+                                  "ragged_gn", "f16_n128_ns4"])
+def test_ping_pong_loop_is_bitwise_the_one_barrier_loop(case):
+    """The two-group ping-pong K loop (FD_CONV_HALO_PP = 1, the default) against the round-5 one-barrier loop
+    (FD_CONV_HALO_PP = 0): the per-element K order is the same (chunk by chunk, tap by tap, half 0 then half 1), so
+    the outputs and the epilogue's GroupNorm statistics must be bitwise equal -- 256 x 160 and 256 x 128 tiles, 128-row
+    tiles, the pairwise channel split, the Upsample2D phase form, the GroupNorm folded into the staging (its patch
+    transformed in the ping-pong LOAD segments), residual + row bias + SiLU, a ragged 23 x 33 image, fp16 with the
+    4-deep weight ring."""
+    from fdhip import ops
+    nimg, H, W, Cin, Cout, dt, knob = {
+        "th16_n160": (2, 64, 64, 320, 320, torch.bfloat16, dict(FD_CONV_HALO_MIN_TILES=1)),
+        "gn_res_rowbias_stats": (2, 64, 48, 640, 320, torch.bfloat16, dict(FD_CONV_HALO_MIN_TILES=1)),
+        "th8": (2, 64, 64, 320, 320, torch.bfloat16, dict(FD_CONV_HALO_MIN_TILES=100, FD_CONV_HALO_SPLIT16=0)),
+        "split_k": (2, 32, 32, 1280, 1280, torch.bfloat16, {}),
+        "phase_f16": (1, 32, 48, 256, 256, torch.float16, {}),
+        "phase_bf16": (2, 32, 32, 1280, 1280, torch.bfloat16, {}),
+        "ragged_gn": (2, 23, 33, 320, 320, torch.bfloat16, dict(FD_CONV_HALO_MIN_TILES=1)),
+        "f16_n128_ns4": (1, 128, 64, 256, 128, torch.float16, dict(FD_CONV_HALO_MIN_TILES=1, FD_CONV_HALO_NS16=4)),
+    }[case]
+    phase = case.startswith("phase")
+    g = torch.Generator().manual_seed(41)
+    x, w, b = _inputs(nimg, 2 * H if phase else H, 2 * W if phase else W, Cin, Cout, dt, seed=40,
+                      up=(H, W) if phase else None)
+    xs, bd = _nhwc(x).to(DEV), b.float().to(DEV)
+    gn_in = case in ("gn_res_rowbias_stats", "ragged_gn", "split_k", "f16_n128_ns4")
+    epi = case in ("gn_res_rowbias_stats", "ragged_gn")
+    gamma = (1 + 0.1 * torch.randn(Cin, generator=g)).to(DEV)
+    beta = (0.1 * torch.randn(Cin, generator=g)).to(DEV)
+    temb = torch.randn(nimg, Cout, generator=g).to(DEV)
+    res = _nhwc(torch.randn(nimg, Cout, H, W, generator=g).to(dt)).to(DEV)
+    outs = []
+    for pp in (0, 1):
+        with _knobs(FD_CONV_HALO_PP=pp, **knob):
+            st = ops.GnStats(nimg, (4 if phase else 1) * H * W, 32, DEV)
+            if phase:
+                wph = ops.pack_conv3x3_up2(w.float()).to(DEV, dt)
+                y = ops.conv3x3_up2(xs, wph, bd, nimg, H, W, gn=st)
+            else:
+                wp = ops.pack_conv3x3(w.float()).to(DEV, dt)
+                assert ops.halo_conv_rows(xs, wp, nimg, H, W) > 0
+                kw = dict(rowbias=temb, residual=res, act="silu") if epi else {}
+                if gn_in:
+                    kw["gn_in"] = (ops.group_norm_affine(xs, gamma, beta, nimg, H * W, Cin, 32, 1e-5), True)
+                y = ops.conv3x3(xs, wp, bd, nimg, H, W, gn=st, **kw)
+            torch.cuda.synchronize()
+            hw = (4 if phase else 1) * H * W  # the written partial blocks: [nimg][hw / rows][32] float2
+            outs.append((y.clone(), st.part[:nimg * (hw // st.rows) * 32 * 2].clone() if st.done else None))
+    assert torch.isfinite(outs[1][0].float()).all()
+    assert torch.equal(outs[0][0], outs[1][0])
+    if outs[0][1] is not None:
+        assert torch.equal(outs[0][1], outs[1][1])

@@ -394,6 +394,25 @@ def test_tlc_scale_input_and_euler_step():
     torch.testing.assert_close(out2, ref2, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("t_n", [2, 256, 600])
+def test_tlc_scale_input_writes_every_timestep_row(t_n):
+    """fd_tlc_scale_input_t fills t_out[0 .. t_n) from the same launch for any t_n (only block 0 wrote it,
+    so more than 256 UNet rows -- FD_TILE_BATCH > 128 with CFG -- were refused); the tiles equal the plain launch's."""
+    from fdhip import ops
+    H, W, k, nt = 200, 136, 64, 6
+    canvas = torch.randn(4, H, W, device=DEV) * 5
+    rows = torch.tensor([0, 64, 136], dtype=torch.int32, device=DEV)
+    cols = torch.tensor([0, 72], dtype=torch.int32, device=DEV)
+    a = torch.empty(nt * 2, k * k, 4, dtype=torch.bfloat16, device=DEV)
+    b = torch.empty_like(a)
+    t_out = torch.full((t_n,), -1.0, device=DEV)
+    ops.tlc_scale_input(canvas, rows, cols, H, W, k, k, 0, nt, 2, 11.0, a)
+    ops.tlc_scale_input(canvas, rows, cols, H, W, k, k, 0, nt, 2, 11.0, b, t_out=t_out, timestep=961.0)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert bool((t_out == 961.0).all())
+
+
 def test_tlc_grids_nhwc():
     from fdhip import ops
     H, W, C, k = 200, 136, 512, 128
@@ -456,7 +475,7 @@ def test_flash_attn_d512_key_splits(ks):
     (1, 128, 128, 128, 256, True, True),    # gemm256 upsample conv (256^2 out), cpg 8
     (2, 128, 128, 128, 256, False, True),   # gemm256, two images
     (1, 256, 256, 128, 128, False, True),   # gemm8 256x128, cpg 4 (chunks straddle groups)
-    (1, 512, 512, 128, 128, False, True),   # 128-channel conv on a 512^2 image (4-wave 128x128 under FD_GEMM8_N128=1)
+    (1, 512, 512, 128, 128, False, True),   # 128-channel conv on a 512^2 image
     (1, 1024, 1024, 128, 128, False, True),  # the VAE decoder's 1024^2 level: 4096 partial blocks (wide finalize)
     (2, 128, 128, 320, 320, False, True),   # gemm8 256x160 (the UNet's 128^2 level), cpg 10
     (2, 64, 64, 640, 640, False, None),     # the 64^2 level, cpg 20 (256x160 when the planner takes it)
@@ -480,9 +499,7 @@ def test_conv_groupnorm_statistics_from_epilogue(nimg, H, W, Cin, Cout, up, expe
     if expect is not None:
         assert st.done == expect
     if st.done:
-        from fdhip import knobs
-        routed = knobs.get("FD_GEMM8_N128") != 0 and Cout == 128 and nimg * Ho * Wo >= 262144
-        assert st.rows == (halo if halo else 128 if routed else 256)
+        assert st.rows == (halo if halo else 256)
     g, be = torch.randn(Cout, device=DEV), torch.randn(Cout, device=DEV)
     got = ops.group_norm(y, g, be, nimg, Ho * Wo, Cout, 32, 1e-6, silu=True, stats=st)
     want = ops.group_norm(y, g, be, nimg, Ho * Wo, Cout, 32, 1e-6, silu=True)
