@@ -1022,12 +1022,16 @@ int launch8(const fd_gemm_params* p, const Plan8& pl, hipStream_t s) {
   dim3 grid(pl.tiles * pl.S), block(64 * NW);
   float* slabs = (float*)((char*)p->ws + 65536 * sizeof(unsigned));
   unsigned* cnt = (unsigned*)p->ws;
-  if constexpr (BM < 256) {  // 128 / 64-row tiles: plan8 gives them only plain GEMMs (LN-fold producers, score GEMMs)
-    if (p->conv || p->act == FD_ACT_GEGLU || p->ln_in) return FD_ERR_ARG;
-  }
   if constexpr (BM < 256) {
-    hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO>), grid, block, 0, s, *p, pl.S,
-                       pl.group_m, slabs, cnt, f8_args{});
+    // 128 / 64-row tiles: plan8 gives them only the LN-fold producers (plain) and the cross-attention score GEMMs
+    // (plain, or LN-fold consumers: the attn2 LayerNorm is folded into the score GEMM)
+    if (p->conv || p->act == FD_ACT_GEGLU) return FD_ERR_ARG;
+    if (p->ln_in)
+      hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO, true>), grid, block, 0, s, *p,
+                         pl.S, pl.group_m, slabs, cnt, f8_args{});
+    else
+      hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, false, false, TO>), grid, block, 0, s, *p, pl.S,
+                         pl.group_m, slabs, cnt, f8_args{});
   } else if (p->conv) {
     hipLaunchKernelGGL((gemm8_kernel<T, BM, BN, NW, WAVES_M, NS, true, false, TO>), grid, block, 0, s, *p, pl.S,
                        pl.group_m, slabs, cnt, f8_args{});
