@@ -121,14 +121,27 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // erff, whose two polynomial branches both run in a mixed-sign wave (~40 VALU per element: the GEGLU epilogue
 // of the 2048 x 10240 projection spent ~10 us in it).  Both far below the bf16 / fp16 rounding of the stored value.
 __device__ __forceinline__ float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
-__device__ __forceinline__ float erf_fast(float x) {
-  const float a = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
-  const float y =
-      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
-  return copysignf(fmaf(-y, __expf(-a * a), 1.0f), x);
+// GELU(x) = x * Phi(x) (diffusers GELU / GEGLU, approximate="none") as x * sigmoid(z(x)) with z = logit(Phi(x)) fitted as
+// an odd polynomial x * (c0 + c1 x^2 + c2 x^4) on |x| <= 5.5, x clamped there (beyond it Phi is 0 or 1 to within 2e-8);
+// -log2(e) folded into the coefficients (scripts/gelu_fit.py).  Max |error| 2.6e-5 over the real line in fp32, far
+// inside the bf16 rounding of the output; 7 plain + 2 transcendental VALU ops where the Abramowitz-Stegun 7.1.26 erf
+// form (max |error| 1.5e-7) took 14 + 2 -- the GEGLU epilogue runs with no MFMA beside it.
+#ifndef FD_GELU_AS
+#define FD_GELU_AS 0  // A/B builds only: 1 = the round-5 Abramowitz-Stegun 7.1.26 erf form
+#endif
+__device__ __forceinline__ float gelu_f(float x) {
+  if constexpr (FD_GELU_AS) {
+    const float z = x * 0.70710678118654752f, a = fabsf(z);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
+    const float y =
+        t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+    return 0.5f * x * (1.0f + copysignf(fmaf(-y, __expf(-a * a), 1.0f), z));
+  }
+  const float xc = __builtin_amdgcn_fmed3f(x, -5.5f, 5.5f);
+  const float x2 = xc * xc;
+  const float p = fmaf(fmaf(1.014481299e-03f, x2, -1.067767218e-01f), x2, -2.301120520e+00f) * xc;
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(p));
 }
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float quickgelu_f(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x)); }
 // LeakyReLU(negative_slope = 0.2) of the BSRNet pre-pass (bsrnet_arch.py:52, nn.LeakyReLU(0.2))
 __device__ __forceinline__ float lrelu_f(float x) { return x >= 0.f ? x : 0.2f * x; }

@@ -58,6 +58,7 @@ class Clock:
         torch.cuda.synchronize()
         n = int(self.cnt.item())
         s = self.buf[:n].cpu().tolist()
+        self.raw = s
         mhz = [(c1 - c0) / (r1 - r0) * 100.0 for (r0, c0), (r1, c1) in zip(s[:-1], s[1:]) if r1 > r0]
         k = len(mhz) // 20  # drop the ramp-in / ramp-out edges
         return mhz[k:len(mhz) - k] if len(mhz) > 40 else mhz
@@ -112,6 +113,7 @@ def main():
     clk = None if a.no_clock else Clock(dev)
     mk_in = torch.zeros(64, dtype=torch.float32, device=dev)
     mk_out = torch.empty(64, dtype=torch.uint8, device=dev)
+    raw = {}
     res = {"what": "C2 UNet forward in context vs kernel-family graphs: replay ms and the shader clock (MHz) sampled "
                    "every 20 us by a one-wave side-stream sampler (s_memtime / s_memrealtime)",
            "proj_launches_per_forward": len(proj), "phases": {}}
@@ -119,6 +121,7 @@ def main():
         clk.start()
         torch.cuda._sleep(int(2e7))
         res["phases"]["idle"] = {"clock_mhz": stats(clk.finish())}
+        raw["idle"] = clk.raw
         print("idle", res["phases"]["idle"], flush=True)
     for name, (g, n) in phases.items():
         g.replay()
@@ -133,6 +136,8 @@ def main():
             g.replay()
         e1.record()
         mhz = clk.finish() if clk is not None else []
+        if clk is not None:
+            raw[name] = clk.raw
         torch.cuda.synchronize()
         ops.postprocess_u8(mk_in, mk_out)
         res["phases"][name] = {"replays": reps, "ms_per_replay": round(e0.elapsed_time(e1) / reps, 4),
@@ -144,6 +149,10 @@ def main():
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"{a.tag}_clock.json"), "w") as f:
         json.dump(res, f, indent=1)
+    if raw:  # (s_memrealtime, s_memtime) samples per phase, for aligning with a kernel trace (incontext_report.py)
+        import numpy as np
+        np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"{a.tag}_samples.npz"),
+                            **{k: np.asarray(v, dtype=np.int64) for k, v in raw.items()})
     print(json.dumps(res))
 
 

@@ -17,4 +17,5 @@ python3 scripts/roofline_check.py $T gpurun_out/${TAG}_prof_bench.log 3 > gpurun
 python3 scripts/prof_gemm_breakdown.py $T 3 > gpurun_out/${TAG}_gemm_instances.txt 2>&1 || true
 python3 scripts/prof_positions.py $T 3 > gpurun_out/${TAG}_positions.txt 2>&1 || true
 cp $(find $D -name "*kernel_stats.csv" | head -1) gpurun_out/${TAG}_kernel_stats.csv
+gzip -c $T > gpurun_out/${TAG}_kernel_trace.csv.gz  # the raw trace, for off-box analysis (scripts/prof_*.py read .gz)
 head -20 gpurun_out/${TAG}_step_window.txt; cat gpurun_out/${TAG}_roofline_check.json
