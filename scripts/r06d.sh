@@ -16,7 +16,7 @@ grep -E "^(idle|forward|proj|flash|gemm) " gpurun_out/${TAG}_trace.log
    -- python3 $R/scripts/incontext_probe.py --tag ${TAG}_pmc --no-clock --reps 2 > $R/gpurun_out/${TAG}_pmc.log 2>&1) || { tail -5 gpurun_out/${TAG}_pmc.log; exit 1; }
 T=$(find $D/trace -name "*kernel_trace.csv" | head -1)
 P=$(find $D/pmc -name "*counter_collection.csv" | head -1)
-gzip -c $T > gpurun_out/${TAG}_kernel_trace.csv.gz
+gzip -c $T > gpurun_out/${TAG}_incontext_trace.csv.gz
 gzip -c $P > gpurun_out/${TAG}_tcc.csv.gz
 python3 scripts/incontext_report.py $T --samples gpurun_out/${TAG}_samples.npz --pmc $P > gpurun_out/${TAG}_incontext.json; rc=$?
 cat gpurun_out/${TAG}_incontext.json | head -80; exit $rc
