@@ -70,6 +70,9 @@ def parse(argv=None):
     ap.add_argument("--size", type=int, default=1024, help="C2 image side (latent = size/8)")
     ap.add_argument("--fp8", action="store_true", help="use_fp8 model (quantize_8bit weights; transformer Linears "
                                                        "on the e4m3 MFMA): the C4 arithmetic")
+    ap.add_argument("--unet-fp16", action="store_true", help="UNet computing in fp16 (the reference's own UNet dtype, "
+                                                             "create_FaithDiff_model.py:21-22) instead of bf16 "
+                                                             "(BASELINE configs[1], the default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-vae", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the C2 pipe(...) s/image leg")
@@ -149,14 +152,15 @@ def max_over_ranks(x, world, dev):
 
 
 # ------------------------------------------------------------------------------------------------ model
-def build_pipe(dev, fp8, world=1):
+def build_pipe(dev, fp8, world=1, unet_dtype=torch.bfloat16):
     """The product factory; with N ranks it is built collectively (process_group=WORLD): rank 0 alone reads / draws
     the weights and broadcasts them over RCCL before anything is packed (pipe.last_broadcast_bytes)."""
     from CKPT_PTH import FAITHDIFF_PATH, SDXL_PATH, VAE_FP16_PATH  # 'random-init' sentinels offline
     from FaithDiff.create_FaithDiff_model import FaithDiff_pipeline
     t0 = time.perf_counter()
     pipe = FaithDiff_pipeline(SDXL_PATH, VAE_FP16_PATH, FAITHDIFF_PATH, use_fp8=fp8, fp8_mfma=fp8 or None, seed=0,
-                              init_device=dev, process_group=dist.group.WORLD if world > 1 else None)
+                              init_device=dev, process_group=dist.group.WORLD if world > 1 else None,
+                              unet_dtype=unet_dtype)
     pipe.build_s = time.perf_counter() - t0
     pipe = pipe.to(dev)
     pipe.unet.release_host_weights()
@@ -580,9 +584,12 @@ def main(argv=None):
     knobs.apply_env()  # A/B runs set FD_* knobs in the environment; every non-default value is reported below
     L.require_device()
     dev = torch.device("cuda", local)
-    pipe = build_pipe(dev, args.fp8, world)
+    if args.fp8 and args.unet_fp16:
+        raise SystemExit("--fp8 and --unet-fp16 are exclusive")
+    udt = "fp16" if args.unet_fp16 else "bf16"
+    pipe = build_pipe(dev, args.fp8, world, torch.float16 if args.unet_fp16 else torch.bfloat16)
     result = {"n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
-              "vs_baseline": None, "dtype": "fp8-e4m3+bf16" if args.fp8 else "bf16",
+              "vs_baseline": None, "dtype": "fp8-e4m3+bf16" if args.fp8 else udt,
               "data": "synthetic (seeded random-init SDXL+FaithDiff weights, synthetic latents/conditions/images)",
               "knobs": knobs.changed()}
     if world > 1:  # rank 0 drew the weights, every other rank received them (FaithDiff_pipeline(process_group=))
@@ -659,7 +666,7 @@ def main(argv=None):
             "value": round(args.steps * world / t_max, 4), "unit": "steps/s",
             "ms_per_step": round(t_max / args.steps * 1e3, 3), "scaling": "weak",
             "config": {"workload": f"C2: {args.size}x{args.size} single TLC tile, CFG batch 2, Euler step + blend, "
-                                   f"UNet {'use_fp8: transformer Linears e4m3 MFMA, convs bf16' if args.fp8 else 'bf16'}"
+                                   f"UNet {'use_fp8: transformer Linears e4m3 MFMA, convs bf16' if args.fp8 else udt}"
                                    " (HipUNet.run: hipGraph replay), VAE fp16",
                        "model": "SDXL UNet + FaithDiff extras (2.58B params)", "global_batch": 2 * world,
                        "latent": [loop.h, loop.w], "parallelism": f"replicas x{world}"},

@@ -29,6 +29,7 @@ for ph in "$@"; do
       rc=$?; tail -4 $out.log ;;
     tfile)
       f=${arg%%:*}; k=${arg#*:}; [ "$k" = "$arg" ] && k=""; out=gpurun_out/${TAG}_$(basename $f .py)
+      export FD_PARITY_METRICS=$PWD/${out}_parity_metrics.json; rm -f $FD_PARITY_METRICS
       if [ -n "$k" ]; then K=(-k "$k"); else K=(); fi
       timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "$f" "${K[@]}" > $out.log 2>&1
       rc=$?; tail -8 $out.log ;;

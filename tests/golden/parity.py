@@ -43,9 +43,15 @@ def psnr(a, b, peak, name="psnr_db"):
 def dump(path=None):
     if not RECORDS:
         return None
+    default = "parity_metrics.json"
+    try:  # a CPU-only run (no device) writes its own file, never over a GPU run's merged metrics
+        import torch
+        if not torch.cuda.is_available():
+            default = "parity_metrics_cpu.json"
+    except ImportError:
+        default = "parity_metrics_cpu.json"
     path = path or os.environ.get("FD_PARITY_METRICS") or os.path.join(
-        os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "gpurun_out",
-        "parity_metrics.json")
+        os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "gpurun_out", default)
     os.makedirs(os.path.dirname(path), exist_ok=True)
     with open(path, "w") as f:
         json.dump({"tests": len(RECORDS), "metrics": RECORDS}, f, indent=1, sort_keys=True)

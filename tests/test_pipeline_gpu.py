@@ -28,6 +28,17 @@ def psnr(a, b, peak, name="psnr_db"):
     return parity.psnr(a, b, peak, name)
 
 
+def pipe_fp16_unet():
+    """The same seeded pipeline with the UNet computing in fp16 -- the reference's own UNet dtype
+    (reference create_FaithDiff_model.py:21-22, unet.to(torch.float16)); the product default is bf16 (BASELINE configs[1])."""
+    if "p16" not in _C:
+        from CKPT_PTH import FAITHDIFF_PATH, SDXL_PATH, VAE_FP16_PATH
+        from FaithDiff.create_FaithDiff_model import FaithDiff_pipeline
+        _C["p16"] = FaithDiff_pipeline(SDXL_PATH, VAE_FP16_PATH, FAITHDIFF_PATH, seed=0, init_device="cpu",
+                                       unet_dtype=torch.float16).to("cuda")
+    return _C["p16"]
+
+
 def pipe_and_oracle():
     if "p" not in _C:
         from CKPT_PTH import FAITHDIFF_PATH, SDXL_PATH, VAE_FP16_PATH
@@ -172,18 +183,19 @@ def test_tiled_vae_and_encoder_match_oracle():
             m.tile_sample_min_size, m.tile_latent_min_size, m.use_tiling = 1024, 128, False
 
 
-def test_c2_headline_matches_golden():
+@pytest.mark.parametrize("unet_dtype", ["bf16", "fp16"])
+def test_c2_headline_matches_golden(unet_dtype):
     """BASELINE configs[1] end to end: 1024^2, one TLC tile, 20 Euler steps, CFG 5, start_point 'lr', through the
     product ``pipe(...)`` (HipUNet.run graph replays, graph-captured VAE), against the fp32 CPU oracle pipeline run
     on the same seeded weights and inputs (tests/golden/make_c2_golden.py; pipeline_FaithDiff_tlc.py:1187-1459).
     Bars (about 2x the measured error): latent PSNR after steps 1 / 5 / 10 / 20 and final
-    image PSNR."""
+    image PSNR.  fp16: the same call with the UNet in the reference's own dtype (its own bars, C2_BARS16)."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2")
     gold = np.load(os.path.join(path, "c2_golden.npz"))
     ref_img = np.asarray(Image.open(os.path.join(path, "c2_image.png")))
     c = c2_inputs()
     assert hashlib.sha256(np.asarray(c["img"], dtype=np.uint8).tobytes()).hexdigest() == str(gold["input_sha256"])
-    pipe, *_ = pipe_and_oracle()
+    pipe = pipe_fp16_unet() if unet_dtype == "fp16" else pipe_and_oracle()[0]
     lats = {}
 
     def cb(p, i, t, kw):
@@ -202,13 +214,16 @@ def test_c2_headline_matches_golden():
     p_img = psnr(np.asarray(out), ref_img, 255.0, "image_psnr_db")
     print("C2 latent PSNR by step: " + ", ".join(f"{s}: {v:.2f} dB" for s, v in report.items())
           + f"; image PSNR {p_img:.2f} dB")
-    assert report[1] >= C2_BARS["step1"] and report[20] >= C2_BARS["final"] and p_img >= C2_BARS["image"]
+    bars = C2_BARS16 if unet_dtype == "fp16" else C2_BARS
+    assert report[1] >= bars["step1"] and report[20] >= bars["final"] and p_img >= bars["image"]
 
 
 C2_BARS = {"step1": 63.0, "final": 60.0, "image": 49.5}  # measured 69.1 / 66.1 / 55.6 dB (r02), 6 dB under
+C2_BARS16 = {"step1": 81.0, "final": 78.0, "image": 58.0}  # fp16 UNet: measured 87.2 / 84.1 / 61.3 dB (r06j)
 
 
-def test_c2_teacher_forced_eps():
+@pytest.mark.parametrize("unet_dtype", ["bf16", "fp16"])
+def test_c2_teacher_forced_eps(unet_dtype):
     """SURVEY 8(d) layer 4: per-step teacher-forced eps at C2, including the low-sigma end of the schedule.  The
     oracle's own trajectory (tests/golden/make_c2_golden.py -> c2/c2_eps_golden.npz) gives the step input latent, the
     UNet's noise prediction (both CFG rows) and the guided one (u + 5 (c - u), what the Euler step consumes) at steps
@@ -219,12 +234,14 @@ def test_c2_teacher_forced_eps():
     Step 1's input is the product's own initial canvas (its lr-start parity is the C2 latent test).
     Bars: UNet eps rel-L2 <= 2e-2 per step; guided eps rel-L2 <= 6e-2 -- CFG 5 amplifies the per-row
     error by up to |1 - 5| and 5 while the signal u + 5 (c - u) stays near |u| (first measured 2.6e-2 .. 3.3e-2).
+    fp16: the same with the UNet in the reference's own dtype (reference create_FaithDiff_model.py:21-22), where the guided eps
+    is 5x inside SURVEY 8(d)'s 2e-2 (bar 1e-2) -- the bf16 gap is bf16's 8-bit significand, not the algorithm.
     The conditioning (denoise encoder, prompt embeddings) is the product's own."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c2", "c2_eps_golden.npz")
     gold = np.load(path)
     c = c2_inputs()
     assert hashlib.sha256(np.asarray(c["img"], dtype=np.uint8).tobytes()).hexdigest() == str(gold["input_sha256"])
-    pipe, *_ = pipe_and_oracle()
+    pipe = pipe_fp16_unet() if unet_dtype == "fp16" else pipe_and_oracle()[0]
     steps = sorted(int(k[len("eps_step"):]) for k in gold.files if k.startswith("eps_step"))
     assert steps == [1, 10, 19, 20]
     out_lat, unet_eps = {}, {}
@@ -259,7 +276,8 @@ def test_c2_teacher_forced_eps():
     print("teacher-forced UNet eps rel-L2 by step: " + ", ".join(f"{s}: {r:.3e}" for s, r in rels.items())
           + "; guided: " + ", ".join(f"{s}: {r:.3e}" for s, r in grels.items()))
     assert all(r <= 2e-2 for r in rels.values()), rels
-    assert all(r <= 6e-2 for r in grels.values()), grels
+    # fp16 measured (r06j): UNet eps 1.2e-3 .. 7.4e-4, guided 4.2e-3 .. 3.2e-3
+    assert all(r <= (6e-2 if unet_dtype == "bf16" else 1e-2) for r in grels.values()), grels
 
 
 def test_band_matches_golden():
@@ -276,7 +294,7 @@ def test_band_matches_golden():
     ref_img = np.asarray(Image.open(os.path.join(path, "band_image.png")))
     c = band_inputs(1)
     assert hashlib.sha256(np.asarray(c["img"], dtype=np.uint8).tobytes()).hexdigest() == str(gold["input_sha256"])
-    pipe, *_ = pipe_and_oracle()
+    pipe = pipe_fp16_unet() if unet_dtype == "fp16" else pipe_and_oracle()[0]
     lats = {}
 
     def cb(p, i, t, kw):
