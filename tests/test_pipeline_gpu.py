@@ -294,7 +294,7 @@ def test_band_matches_golden():
     ref_img = np.asarray(Image.open(os.path.join(path, "band_image.png")))
     c = band_inputs(1)
     assert hashlib.sha256(np.asarray(c["img"], dtype=np.uint8).tobytes()).hexdigest() == str(gold["input_sha256"])
-    pipe = pipe_fp16_unet() if unet_dtype == "fp16" else pipe_and_oracle()[0]
+    pipe, *_ = pipe_and_oracle()
     lats = {}
 
     def cb(p, i, t, kw):
