@@ -1,6 +1,8 @@
 #!/bin/bash
-# r06l: final-tree rocprof evidence: C2 bench kernel trace (step window, GEMM instances, roofline cross-check), the UNet
-# GEMM-family traffic (FETCH_SIZE / WRITE_SIZE passes), the VAE decode and flash-attention counter passes
+# r06l: final-tree rocprof evidence -- C2 bench kernel trace (step window, GEMM instances, roofline cross-check), the
+# UNet GEMM-family traffic (FETCH_SIZE / WRITE_SIZE passes), the VAE decode and flash-attention counter passes -- and
+# the bf16 / fp16-UNet C2 lines back to back on one box
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-bash scripts/run.sh r06l trace pmc=unet pmc=vae pmc=attn
+bash scripts/run.sh r06l "bench=--no-c3,--no-pipeline,--no-cpu-baseline" "bench=--unet-fp16,--no-c3,--no-pipeline,--no-cpu-baseline" \
+  trace pmc=unet pmc=vae pmc=attn

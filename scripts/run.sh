@@ -34,6 +34,7 @@ for ph in "$@"; do
       timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu "$f" "${K[@]}" > $out.log 2>&1
       rc=$?; tail -8 $out.log ;;
     bench)
+      [ -n "$arg" ] && out=${out}_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_' | sed 's/_*$//')
       timeout -k 10 600 python bench.py ${arg//,/ } > $out.json 2> $out.err; rc=$?; tail -c 700 $out.json ;;
     trace)
       bash scripts/trace.sh $TAG > $out.log 2>&1; rc=$?; tail -30 $out.log ;;
