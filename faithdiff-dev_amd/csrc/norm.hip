@@ -495,6 +495,14 @@ extern "C" int fd_group_norm_affine(const void* x, const void* part, int part_ro
                                               (const T*)x, (float2*)ws, HW, C, groups, rpc));
     }
     FD_LAUNCH_CHECK();
+    if (nch <= 1024) {
+      // the fused fold + affine, the same fp64 order as gn_finalize_kernel: one ~5 us latency-bound launch fewer per
+      // halo conv whose input statistics no producer wrote (round 6)
+      hipLaunchKernelGGL(gn_finalize_affine_kernel, dim3(groups, nimg), dim3(64), 0, s, (const float2*)ws, gamma,
+                         beta, (float2*)affine, HW, C, groups, nch, eps);
+      FD_LAUNCH_CHECK();
+      return FD_OK;
+    }
     stats = (float2*)ws + (long long)nimg * nch * groups;
     gn_finalize_launch((const float2*)ws, stats, nimg, HW, C, groups, nch, eps, s);
   }
