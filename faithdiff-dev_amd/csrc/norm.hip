@@ -25,9 +25,14 @@ static inline int gn_rows_per_chunk(int nimg, int HW) {
   return r;
 }
 
-template <typename T, int NV>
+// CAT (fd_concat_channels_gn, round 6): x is the channel concat of a [.., C1] and b [.., C - C1], gathered per 8-channel
+// vector (C1 % 8 == 0) and also stored to y -- the up-block concat and its GroupNorm statistics pass in one launch,
+// the same values in the same order as the concat then this pass (bit-identical partials).
+template <typename T, int NV, bool CAT = false>
 __global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ x, float2* __restrict__ part, int HW,
-                                                         int C, int groups, int rows_per_chunk) {
+                                                         int C, int groups, int rows_per_chunk,
+                                                         const T* __restrict__ b = nullptr, int C1 = 0,
+                                                         T* __restrict__ y = nullptr) {
   typedef typename VecT<T>::v8 V8;
   // per-(row-slot, channel) partials, reduced in a fixed order (bitwise reproducible; no atomics)
   __shared__ float lds_s[256 * 8 * NV], lds_q[256 * 8 * NV];
@@ -50,13 +55,27 @@ __global__ void __launch_bounds__(256) gn_partial_kernel(const T* __restrict__ x
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int rr = r + u * RP;
-        const T* row = x + ((long long)img * HW + (rr < r1 ? rr : r)) * C;
+        const long long m = (long long)img * HW + (rr < r1 ? rr : r);
+        if constexpr (CAT) {
 #pragma unroll
-        for (int n = 0; n < NV; ++n) val[u][n] = *(const V8*)(row + (v + n * VPR) * 8);
+          for (int n = 0; n < NV; ++n) {
+            const int c = (v + n * VPR) * 8;
+            val[u][n] = c < C1 ? *(const V8*)(x + m * C1 + c) : *(const V8*)(b + m * (C - C1) + (c - C1));
+          }
+        } else {
+          const T* row = x + m * C;
+#pragma unroll
+          for (int n = 0; n < NV; ++n) val[u][n] = *(const V8*)(row + (v + n * VPR) * 8);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (r + u * RP >= r1) break;
+        if constexpr (CAT) {
+#pragma unroll
+          for (int n = 0; n < NV; ++n)
+            st_out16((V8*)(y + ((long long)img * HW + r + u * RP) * C + (v + n * VPR) * 8), val[u][n]);
+        }
 #pragma unroll
         for (int n = 0; n < NV; ++n)
 #pragma unroll
@@ -385,6 +404,36 @@ extern "C" int fd_group_norm(const void* x, void* y, const float* gamma, const f
   return gn_apply_launch(x, y, stats, gamma, beta, nimg, HW, C, groups, silu, dtype, s);
 }
 
+// Rows per statistics chunk of fd_group_norm's own pass (and of fd_concat_channels_gn's partials) for this image size.
+extern "C" int fd_group_norm_chunk_rows(int nimg, int HW) { return HW > 0 ? gn_rows_per_chunk(nimg, HW) : 0; }
+
+// y = concat(a [M, C1], b [M, C2]) along channels (M = nimg * HW) AND the GroupNorm statistics of y, per image,
+// fd_group_norm_chunk_rows(nimg, HW)-row chunk and group, into part[(img * HW / rows + chunk) * groups + g] (float2):
+// the input for fd_group_norm_partials / fd_group_norm_affine with part_rows = those rows.  One launch instead of the
+// concat and the statistics pass; the partials are bit for bit fd_group_norm's own.
+extern "C" int fd_concat_channels_gn(const void* a, int C1, const void* b, int C2, void* y, int nimg, int HW,
+                                     int groups, void* part, int dtype, void* stream) {
+  if (!a || !b || !y || !part) return FD_ERR_ARG;
+  const int C = C1 + C2;
+  if (C1 % 8 || C2 % 8 || C1 <= 0 || C2 <= 0 || nimg <= 0 || HW <= 0 || groups <= 0 || groups > 64 || C % groups ||
+      C > GN_MAXC)
+    return FD_ERR_SHAPE;
+  const int rpc = gn_rows_per_chunk(nimg, HW);
+  const int nch = (HW + rpc - 1) / rpc;
+  const int NV = (C / 8 > 256) ? 2 : 1;
+  if (NV == 2 && (C % 16)) return FD_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  if (NV == 1) {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_partial_kernel<T, 1, true>), dim3(nch, nimg), dim3(256), 0, s,
+                                            (const T*)a, (float2*)part, HW, C, groups, rpc, (const T*)b, C1, (T*)y));
+  } else {
+    FD_DISPATCH_T(dtype, hipLaunchKernelGGL((gn_partial_kernel<T, 2, true>), dim3(nch, nimg), dim3(256), 0, s,
+                                            (const T*)a, (float2*)part, HW, C, groups, rpc, (const T*)b, C1, (T*)y));
+  }
+  FD_LAUNCH_CHECK();
+  return FD_OK;
+}
+
 // GroupNorm whose statistics the producing GEMM / conv epilogue already wrote (fd_gemm_params.gn_part, gn_done):
 // part[(img * HW/256 + b) * groups + g] = (sum, sumsq) of the 256-row block b.  Finalize (fp64 fold, fixed order)
 // into stats (nimg * groups float2, caller's) + apply: the gn_partial pass (one full read of x) is gone.
@@ -392,7 +441,9 @@ extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma
                                       int C, int groups, float eps, int silu, const void* part, int part_rows,
                                       void* stats, int dtype, void* stream) {
   if (!x || !y || !part || !stats) return FD_ERR_ARG;
-  if (part_rows != 128 && part_rows != 256) return FD_ERR_ARG;
+  // 256 / 128: the GEMM / conv epilogue partials; any power of two up to 8192 partials per image: the statistics-pass
+  // chunks of fd_concat_channels_gn (fd_group_norm_chunk_rows)
+  if (part_rows <= 0 || (part_rows & (part_rows - 1)) || HW % part_rows || HW / part_rows > 8192) return FD_ERR_ARG;
   if (nimg <= 0 || HW <= 0 || HW % part_rows || C <= 0 || groups <= 0 || groups > 64 || C % groups || C % 8 ||
       C > GN_MAXC)
     return FD_ERR_SHAPE;
@@ -471,7 +522,7 @@ extern "C" int fd_group_norm_affine(const void* x, const void* part, int part_ro
   hipStream_t s = (hipStream_t)stream;
   float2* stats;
   if (part) {
-    if ((part_rows != 128 && part_rows != 256) || HW % part_rows) return FD_ERR_ARG;
+    if (part_rows <= 0 || (part_rows & (part_rows - 1)) || HW % part_rows || HW / part_rows > 8192) return FD_ERR_ARG;
     stats = (float2*)ws;
     const int nch = HW / part_rows;
     if (nch <= 1024) {  // one launch (the wide fold's long lists keep the two-launch form)

@@ -17,6 +17,7 @@ HOST_DEFAULTS = {
     "FD_LN_FOLD": 1,        # LayerNorms folded into the transformer GEMM pairs (0: separate LayerNorm launches)
     "FD_ITL_FOLD": 1,       # ... and into the information transformer's in_proj / c_fc (with FD_LN_FOLD)
     "FD_UNET_GN_EPI": 1,    # UNet GroupNorm statistics from the producing GEMM / conv epilogue
+    "FD_UNET_CAT_GN": 1,    # ... and from the up blocks' skip concats (fd_concat_channels_gn; with FD_UNET_GN_EPI)
     "FD_FP8_MFMA": 0,       # use_fp8 model on the e4m3 MFMA (quantize_8bit(fp8_mfma=...) / FaithDiff_pipeline arg)
     "FD_FP8_MX_ATTN": 1,    # fp8 model: MX e4m3 attention outputs only (the measured-fastest form)
     "FD_FP8_MX_GEGLU": 0,   # fp8 model: MX output straight from the GEGLU epilogue

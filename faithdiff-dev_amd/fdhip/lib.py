@@ -85,6 +85,8 @@ _SIGS = {
     "fd_xattn_consts": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_ll, c_ll, c_vp, c_int, c_int, c_int, c_f, c_vp, c_vp,
                                 c_int, c_vp]),
     "fd_concat_channels": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_ll, c_int, c_vp]),
+    "fd_group_norm_chunk_rows": (c_int, [c_int, c_int]),
+    "fd_concat_channels_gn": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp]),
     "fd_unary": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_int, c_vp]),
     "fd_add_strided": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_int, c_int, c_vp]),
     "fd_axpby": (c_int, [c_vp, c_ll, c_vp, c_ll, c_vp, c_ll, c_int, c_int, c_f, c_f, c_int, c_vp]),

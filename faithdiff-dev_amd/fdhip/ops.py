@@ -841,7 +841,25 @@ def softmax_rows(s, out, R, C, scale, ldp=None):
 
 
 # --------------------------------------------------------------------------------------- elementwise
-def concat_channels(a, C1, b, C2, out, M):
+def concat_channels(a, C1, b, C2, out, M, gn=None):
+    """out = concat(a [M, C1], b [M, C2]) along channels.  gn: a GnStats for out's GroupNorm consumer -- the concat
+    then also writes fd_group_norm's own statistics partials (fd_concat_channels_gn, one launch instead of the concat
+    and the statistics pass; same bits); gn.done stays False where the shape does not allow it (HW not a multiple of
+    the chunk rows)."""
+    if gn is not None:
+        gn.done, gn.rows = False, 0
+        rows = int(L.load().fd_group_norm_chunk_rows(gn.nimg, gn.HW))
+        C = C1 + C2
+        if (rows > 0 and gn.HW % rows == 0 and gn.nimg * gn.HW == M and C % gn.groups == 0
+                and (C // 8 <= 256 or C % 16 == 0)):
+            need = gn.nimg * (gn.HW // rows) * gn.groups * 2
+            if gn.part.numel() < need:
+                gn.part = torch.empty((need,), dtype=torch.float32, device=out.device)
+            L.check(L.load().fd_concat_channels_gn(L.ptr(a), C1, L.ptr(b), C2, L.ptr(out), gn.nimg, gn.HW, gn.groups,
+                                                   L.ptr(gn.part), L.dtype_code(a.dtype), L.stream()),
+                    "fd_concat_channels_gn")
+            gn.done, gn.rows = True, rows
+            return out
     L.check(L.load().fd_concat_channels(L.ptr(a), C1, L.ptr(b), C2, L.ptr(out), M, L.dtype_code(a.dtype), L.stream()),
             "fd_concat_channels")
     return out

@@ -93,6 +93,7 @@ class HipUNet:
 
         # GroupNorm statistics from the producing conv / GEMM epilogue (256-row tiles; FD_UNET_GN_EPI=0: off)
         self.gn_epi = knobs.get("FD_UNET_GN_EPI") != 0
+        self.cat_gn = self.gn_epi and knobs.get("FD_UNET_CAT_GN") != 0
         self._gn_src = None
         # transformer Linear weights: e4m3 bytes for the fp8 MFMA, else the compute dtype
         LW = (lambda t: ops.pack_e4m3(t.to(self.device))) if self.fp8_mfma else \
@@ -275,8 +276,10 @@ class HipUNet:
         HW = H * Wd
         if x2 is not None:
             cat = torch.empty((B * HW, r["cin"]), dtype=self.dtype, device=self.device)
-            ops.concat_channels(x, C1, x2, r["cin"] - C1, cat, B * HW)
+            s0 = self._gn_new(B, HW) if self.cat_gn else None  # the concat also writes norm1's statistics
+            ops.concat_channels(x, C1, x2, r["cin"] - C1, cat, B * HW, gn=s0)
             x = cat
+            self._gn_src = (cat, s0) if s0 is not None and s0.done else None
         # norm1 -> SiLU -> conv1 (+ time embedding), norm2 -> SiLU -> conv2 (+ shortcut): each GroupNorm folded into
         # the halo-staged conv's staging pass where that kernel takes the conv (ops.gn_conv3x3), else its own pass
         s1 = self._gn_new(B, HW)

@@ -188,9 +188,11 @@ long long fd_group_norm_ws_bytes(int nimg, int HW, int C, int groups);
 int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
                   int groups, float eps, int silu, int dtype, void* ws, void* stream);
 /* fd_group_norm when the producing fd_gemm wrote the statistics (fd_gemm_params.gn_part, gn_done = part_rows):
- * part [nimg][HW / part_rows][groups] float2 (sum, sumsq), part_rows 256 or 128; stats: nimg * groups float2 of
- * caller memory.  HW % part_rows == 0.  Saves the statistics pass over x (one full read).  Same arithmetic as
- * fd_group_norm except the summation order of the statistics. */
+ * part [nimg][HW / part_rows][groups] float2 (sum, sumsq), part_rows 256 or 128 (or the chunk rows of
+ * fd_concat_channels_gn: any power of two, at most 8192 partials per image); stats: nimg * groups float2 of caller
+ * memory, written.  HW % part_rows == 0.  Saves the statistics pass over x (one full read).  Same arithmetic as
+ * fd_group_norm except the summation order of the statistics (identical to it with fd_concat_channels_gn's
+ * partials). */
 int fd_group_norm_partials(const void* x, void* y, const float* gamma, const float* beta, int nimg, int HW, int C,
                            int groups, float eps, int silu, const void* part, int part_rows, void* stats, int dtype,
                            void* stream);
@@ -326,6 +328,14 @@ int fd_xattn_consts(const void* B1, long long ldb, int rows, int K, const void* 
 /* y[m][0:C1] = a[m][0:C1], y[m][C1:C1+C2] = b[m][0:C2]  (up-block skip concat, diffusers
  * CrossAttnUpBlock2D / UpBlock2D torch.cat) */
 int fd_concat_channels(const void* a, int C1, const void* b, int C2, void* y, long long M, int dtype, void* stream);
+/* fd_concat_channels over M = nimg * HW rows plus the GroupNorm statistics of y for its consumer (the up-block
+ * resnet's norm1): part[(i * HW / R + k) * groups + g] = (sum, sum of squares) of image i, R-row chunk k, group g,
+ * R = fd_group_norm_chunk_rows(nimg, HW) -- fd_group_norm's own statistics pass, bit for bit, fused into the copy.
+ * part: nimg * (HW / R) * groups float2.  Consumer: fd_group_norm_partials / fd_group_norm_affine with
+ * part_rows = R.  Replaces: torch.cat + the first half of native_group_norm (diffusers UpBlock2D resnets). */
+int fd_group_norm_chunk_rows(int nimg, int HW);
+int fd_concat_channels_gn(const void* a, int C1, const void* b, int C2, void* y, int nimg, int HW, int groups,
+                          void* part, int dtype, void* stream);
 /* y = act(x) elementwise, n elements; also casts dtype -> out_dtype (act 0 = copy/cast). */
 int fd_unary(const void* x, void* y, long long n, int act, int dtype, int out_dtype, void* stream);
 /* y[m][n] = x[m][n] (+ a[m][n] if a != NULL), general row strides; dtype cast allowed. */

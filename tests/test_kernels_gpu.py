@@ -508,6 +508,70 @@ def test_conv_groupnorm_statistics_from_epilogue(nimg, H, W, Cin, Cout, up, expe
     assert rel_l2(got, ref.reshape(-1, Cout)) < 6e-3
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("nimg,HW,C,silu", [(2, 16384, 320, True), (2, 4096, 640, False), (2, 1024, 1280, True),
+                                            (2, 1024, 2560, False), (1, 256, 64, True)])
+def test_groupnorm_partials_fold_matches_affine_fold_bitwise(dtype, nimg, HW, C, silu):
+    """fd_group_norm_partials' (mean, rstd) from the producer's partials -- written to the caller's stats by
+    gn_finalize_kernel -- are bit for bit the fold of fd_group_norm_affine's fused finalize + affine launch (the same
+    fp64 order): with gamma = 1, beta = 0 the affine is exactly (rstd, -mean * rstd).  The output is x * scale + shift
+    (+ SiLU) of those statistics."""
+    import ctypes
+
+    from fdhip import lib as L
+    from fdhip import ops
+    x = rnd(nimg * HW, C, dtype=dtype)
+    st = ops.GnStats(nimg, HW, 32, DEV)
+    nblk = HW // 256
+    xs = x.float().view(nimg, nblk, 256, 32, C // 32)
+    part = torch.stack([xs.sum((2, 4)), (xs * xs).sum((2, 4))], -1)  # (sum, sumsq) per (image, block, group)
+    part = part * (1 + 1e-3 * torch.randn_like(part))  # not exactly the data's: the fold, not the data, is tested
+    st.part[:part.numel()] = part.reshape(-1)
+    st.done, st.rows = True, 256
+    one, zero = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    y = torch.empty_like(x)
+    stats = torch.zeros(nimg * 32 * 2, device=DEV)
+    L.check(L.load().fd_group_norm_partials(L.ptr(x), L.ptr(y), L.ptr(one), L.ptr(zero), nimg, HW, C, 32, 1e-6,
+                                            int(silu), L.ptr(st.part), 256, L.ptr(stats), L.dtype_code(dtype),
+                                            L.stream()), "fd_group_norm_partials")
+    aff = ops.group_norm_affine(x, one, zero, nimg, HW, C, 32, 1e-6, stats=st)[:nimg * C].view(nimg, C, 2)
+    torch.cuda.synchronize()
+    mean, rstd = stats.view(nimg, 32, 2).unbind(-1)
+    cpg = C // 32
+    assert torch.equal(aff[..., 0], rstd.repeat_interleave(cpg, 1))
+    assert torch.equal(aff[..., 1], (-mean * rstd).repeat_interleave(cpg, 1))
+    ref = x.double().view(nimg, HW, C) * aff[..., 0].double()[:, None] + aff[..., 1].double()[:, None]
+    if silu:
+        ref = ref * torch.sigmoid(ref)
+    assert rel_l2(y.view(nimg, HW, C), ref) < 4e-3
+
+
+@pytest.mark.parametrize("nimg,HW,C1,C2", [(2, 1024, 1280, 1280), (2, 1024, 1280, 640), (2, 4096, 1280, 640),
+                                           (2, 4096, 640, 320), (2, 16384, 640, 320), (2, 16384, 320, 320),
+                                           (1, 100, 64, 32), (1, 1001, 64, 32)])
+def test_concat_with_groupnorm_statistics_bitwise(nimg, HW, C1, C2):
+    """fd_concat_channels_gn: the up-block concat writes its GroupNorm consumer's statistics partials (fd_group_norm's
+    own pass, fused into the copy).  The concat is torch.cat exactly; the GroupNorm (+ SiLU) and the halo conv's
+    affine from those partials are bit for bit the ones computed from the concat by their own statistics pass.
+    HW = 1001 is not a multiple of its chunk rows (4): no partials (done False), the plain concat."""
+    from fdhip import lib as L
+    from fdhip import ops
+    a, b = rnd(nimg * HW, C1), rnd(nimg * HW, C2)
+    C = C1 + C2
+    st = ops.GnStats(nimg, HW, 32, DEV)
+    out = torch.empty((nimg * HW, C), dtype=torch.bfloat16, device=DEV)
+    ops.concat_channels(a, C1, b, C2, out, nimg * HW, gn=st)
+    assert torch.equal(out, torch.cat([a, b], 1))
+    assert st.done == (HW % L.load().fd_group_norm_chunk_rows(nimg, HW) == 0)
+    if not st.done:
+        return
+    g, be = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+    assert torch.equal(ops.group_norm(out, g, be, nimg, HW, C, 32, 1e-5, silu=True, stats=st),
+                       ops.group_norm(out, g, be, nimg, HW, C, 32, 1e-5, silu=True))
+    assert torch.equal(ops.group_norm_affine(out, g, be, nimg, HW, C, 32, 1e-5, stats=st),
+                       ops.group_norm_affine(out, g, be, nimg, HW, C, 32, 1e-5))
+
+
 @pytest.mark.parametrize("B,HW,C", [(2, 16384, 320), (2, 4096, 640), (4, 1024, 1280)])
 def test_gemm_groupnorm_statistics_from_epilogue(B, HW, C):
     """The UNet's transformer proj_out (GEMM + residual) asked for its output's GroupNorm statistics: group_norm from
