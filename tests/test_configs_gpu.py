@@ -129,6 +129,41 @@ def test_c5_images_batched_bitwise_single_calls():
         assert img.std() > 1.0
 
 
+def test_c5_full_50_step_schedule_8_images():
+    """C5 as BASELINE configs[4] states it: 8 images of 1024 px in one pipe() call through ALL 50 steps of the Euler
+    schedule (no denoising_end; VERDICT r05: the suite ran 4 of the 50).  Every step's latents are finite, the
+    timesteps are the 50-step schedule's (981, 961, ..., 1: leading spacing, steps_offset 1), the images are not flat,
+    and one image of the batch is bitwise its own 50-step pipe() call.  Reference loop: test_wo_llava.py:53-97."""
+    S, N = 1024, 8
+    pipe = _build(seed=4)
+    imgs = [synthetic_degraded(S, S, 41 + i) for i in range(N)]
+    prompts = [f"a restored photo, scene {i}" for i in range(N)]
+    noise = torch.cat([det_tensor((1, 4, S // 8, S // 8), 100 + i) for i in range(N)])
+    post = torch.cat([det_tensor((1, 4, S // 8, S // 8), 110 + i) for i in range(N)])
+    ts, finite, last = [], [], {}
+
+    def cb(p, i, t, k):
+        ts.append(int(t))
+        finite.append(bool(torch.isfinite(k["latents"]).all()))
+        last["lat"] = k["latents"].detach().float().cpu().clone()
+        return {}
+    out = pipe(lr_img=imgs, prompt=prompts, latents=noise, posterior_noise=post, negative_prompt="",
+               guidance_scale=5.0, start_point="lr", height=S, width=S, overlap=0.5, target_size=(1024, 1024),
+               num_inference_steps=50, callback_on_step_end=cb).images
+    assert len(out) == N
+    assert ts == [981 - 20 * i for i in range(50)], ts
+    assert all(finite)
+    stds = [float(np.asarray(o).std()) for o in out]
+    parity.record("c5_full_min_image_std", min(stds), bar=">1")
+    assert min(stds) > 1.0
+    k = 5
+    lat, img, n = _run(pipe, imgs[k], prompts[k], noise[k:k + 1], post[k:k + 1], S, (1024, 1024),
+                       num_inference_steps=50)
+    assert n == 50
+    assert torch.equal(last["lat"][k:k + 1], lat), "batched 50-step latents differ from the image's own call"
+    assert (np.asarray(out[k]) == img).all()
+
+
 def test_batched_call_forwards_embeddings_and_callbacks():
     """pipe(lr_img=[...]) forwards every argument the single-image call takes: precomputed
     prompt / negative / pooled embeddings (one row per image) give bitwise the prompts' result, the legacy
