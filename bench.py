@@ -329,6 +329,19 @@ def family_times(fn, kinds, reps=20):
     return out
 
 
+def load_traffic_floor():
+    """The newest committed 8-XCD traffic floor of the bf16 C2 forward (scripts/gemm_traffic_floor.py), or None."""
+    for path in sorted((os.path.join(ROOT, "profiles", f) for f in os.listdir(os.path.join(ROOT, "profiles"))
+                        if f.endswith("_gemm_traffic_floor.json")), reverse=True):
+        try:
+            with open(path) as f:
+                fl = json.load(f)
+            return (fl["read_floor_8xcd_gb"] + fl["write_gb"]) * 1e9, os.path.basename(path)
+        except (OSError, ValueError, KeyError):
+            continue
+    return None
+
+
 def load_traffic(workload):
     """The newest committed traffic file measured on this workload (its key), or None."""
     for path in TRAFFIC_FILES:
@@ -507,6 +520,13 @@ def roofline_leg(loop, fp8):
                   "events on the capture stream",
         "traffic_note": "HBM bytes per forward of these launches (rocprofv3 PMC pass, " + tr16["file"] + ")"
                         if tr16 else "no PMC pass committed for this workload"}
+    fl = None if fp8 or loop.h * 8 != 1024 else load_traffic_floor()
+    if fl is not None and tr16 is not None:
+        # the lower bound any XCD-contiguous tile order has: each XCD's L2 misses once on every A / W panel its tiles
+        # touch; traffic / floor is the part a tile order or L2 reuse could still remove
+        res["roofline"]["traffic_floor_8xcd"] = round(fl[0])
+        res["roofline"]["traffic_over_floor"] = round(tr16["hbm_bytes_per_forward"] / fl[0], 3)
+        res["roofline"]["traffic_floor_note"] = "scripts/gemm_traffic_floor.py, " + fl[1]
     if "flash_attn" in fam:
         n_a, fl_a, _, ms_a = fam["flash_attn"]
         a_tf = fl_a / (ms_a / 1e3) / 1e12

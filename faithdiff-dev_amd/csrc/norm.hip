@@ -441,9 +441,9 @@ extern "C" int fd_group_norm_partials(const void* x, void* y, const float* gamma
                                       int C, int groups, float eps, int silu, const void* part, int part_rows,
                                       void* stats, int dtype, void* stream) {
   if (!x || !y || !part || !stats) return FD_ERR_ARG;
-  // 256 / 128: the GEMM / conv epilogue partials; any power of two up to 8192 partials per image: the statistics-pass
-  // chunks of fd_concat_channels_gn (fd_group_norm_chunk_rows)
-  if (part_rows <= 0 || (part_rows & (part_rows - 1)) || HW % part_rows || HW / part_rows > 8192) return FD_ERR_ARG;
+  // 256 / 128: the GEMM / conv epilogue partials; other powers of two: the statistics-pass chunks of
+  // fd_concat_channels_gn (fd_group_norm_chunk_rows)
+  if (part_rows <= 0 || (part_rows & (part_rows - 1)) || HW % part_rows) return FD_ERR_ARG;
   if (nimg <= 0 || HW <= 0 || HW % part_rows || C <= 0 || groups <= 0 || groups > 64 || C % groups || C % 8 ||
       C > GN_MAXC)
     return FD_ERR_SHAPE;
@@ -522,7 +522,7 @@ extern "C" int fd_group_norm_affine(const void* x, const void* part, int part_ro
   hipStream_t s = (hipStream_t)stream;
   float2* stats;
   if (part) {
-    if (part_rows <= 0 || (part_rows & (part_rows - 1)) || HW % part_rows || HW / part_rows > 8192) return FD_ERR_ARG;
+    if (part_rows <= 0 || (part_rows & (part_rows - 1)) || HW % part_rows) return FD_ERR_ARG;
     stats = (float2*)ws;
     const int nch = HW / part_rows;
     if (nch <= 1024) {  // one launch (the wide fold's long lists keep the two-launch form)

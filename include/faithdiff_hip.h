@@ -189,7 +189,7 @@ int fd_group_norm(const void* x, void* y, const float* gamma, const float* beta,
                   int groups, float eps, int silu, int dtype, void* ws, void* stream);
 /* fd_group_norm when the producing fd_gemm wrote the statistics (fd_gemm_params.gn_part, gn_done = part_rows):
  * part [nimg][HW / part_rows][groups] float2 (sum, sumsq), part_rows 256 or 128 (or the chunk rows of
- * fd_concat_channels_gn: any power of two, at most 8192 partials per image); stats: nimg * groups float2 of caller
+ * fd_concat_channels_gn: any power of two); stats: nimg * groups float2 of caller
  * memory, written.  HW % part_rows == 0.  Saves the statistics pass over x (one full read).  Same arithmetic as
  * fd_group_norm except the summation order of the statistics (identical to it with fd_concat_channels_gn's
  * partials). */
